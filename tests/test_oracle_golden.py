@@ -1,0 +1,75 @@
+"""Pin the CPU oracle (oracle/gat_oracle.py) to the reference's own outputs (tests/golden/*.npz,
+produced by importing /root/reference/models/gat_layer.py — see tests/golden/make_goldens.py)."""
+import numpy as np
+import pytest
+
+from golden_io import LAYER_CASES, MODEL_CASES, grad_seeds, load_layer_case, load_model_case
+from oracle import gat_oracle as orc
+
+OUT_TOL = 1e-4          # outputs / alpha: absolute (north_star: within 1e-4 fp32)
+GRAD_TOL = 1e-4         # grads: max|d| <= 1e-4 * max(1, max|ref|)  
+
+
+def run_oracle(c, dtype=np.float32):
+    m = c["meta"]
+    keep = None
+    if m["dropout"] > 0:
+        E2 = c["edge_index_out"].shape[1]
+        keep = orc.dropout_keep(m["seed"], E2, m["num_heads"], m["dropout"])
+    out, ei2, alpha, cache = orc.gat_layer_forward(
+        c["x"], c["edge_index"], c["W"], c["a"], m["num_heads"], m["out_features"], m["concat"],
+        bias=c["bias"], add_self_loops=m["add_self_loops"], const_attention=m["const_attention"],
+        dropout_p=m["dropout"], keep=keep, dtype=dtype)
+    g_out, g_alpha = grad_seeds(out.shape, alpha.shape)
+    grads = orc.gat_layer_backward(cache, g_out, g_alpha if m["use_g_alpha"] else None)
+    return out, ei2, alpha, grads
+
+
+@pytest.mark.parametrize("name", LAYER_CASES)
+def test_oracle_matches_reference_layer(name):
+    c = load_layer_case(name)
+    out, ei2, alpha, grads = run_oracle(c)
+    e = c["expected"]
+    np.testing.assert_array_equal(ei2, c["edge_index_out"])
+    e["out"].check(out, OUT_TOL)
+    e["alpha"].check(alpha, OUT_TOL)
+    e["grad_x"].check(grads["x"], GRAD_TOL, rtol_scale=True)
+    e["grad_W"].check(grads["W"], GRAD_TOL, rtol_scale=True)
+    if "grad_a" in e:
+        e["grad_a"].check(grads["a"], GRAD_TOL, rtol_scale=True)
+    if "grad_bias" in e:
+        e["grad_bias"].check(grads["bias"], GRAD_TOL, rtol_scale=True)
+
+
+@pytest.mark.parametrize("name", ["adversarial_a1e3", "edge_ties_a_zero", "edge_dropout"])
+def test_oracle_fp64_agrees(name):
+    """The fp64 oracle agrees with the fp32 reference too (guards against matching fp32 noise)."""
+    c = load_layer_case(name)
+    out, _, alpha, grads = run_oracle(c, dtype=np.float64)
+    c["expected"]["out"].check(out, OUT_TOL)
+    c["expected"]["grad_W"].check(grads["W"], GRAD_TOL, rtol_scale=True)
+
+
+@pytest.mark.parametrize("name", MODEL_CASES)
+def test_oracle_matches_reference_model(name):
+    c = load_model_case(name)
+    cfg = c["cfg"]
+    out, ei2, alphas = orc.gat_model_forward(
+        c["x"], c["edge_index"], c["layers"], c["skips"], cfg["num_heads_per_layer"],
+        cfg["head_output_features_per_layer"][1:], cfg["heads_concat_per_layer"],
+        cfg["add_skip_connection"])
+    np.testing.assert_array_equal(ei2, c["edge_index_out"])
+    c["expected"]["out"].check(out, OUT_TOL)
+    for i, al in enumerate(alphas):
+        c["expected"][f"alpha{i}"].check(al, OUT_TOL)
+
+
+def test_self_loop_rewrite_order():
+    ei = np.array([[0, 1, 2, 2, 4], [1, 1, 0, 2, 3]])
+    got = orc.add_remaining_self_loops(ei)
+    np.testing.assert_array_equal(got, [[0, 2, 4, 0, 1, 2, 3, 4], [1, 0, 3, 0, 1, 2, 3, 4]])
+
+
+def test_empty_edge_index_raises():
+    with pytest.raises(RuntimeError):
+        orc.add_remaining_self_loops(np.zeros((2, 0), dtype=np.int64))
