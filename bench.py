@@ -1,0 +1,251 @@
+"""Benchmark: GAT-layer edges/s + achieved HBM GB/s, PPI 3-layer forward (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--graphs G] [--mode fwd|train]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
+
+Workload: per rank a synthetic PPI-shaped batch of G graphs (2245 nodes and 61318
+uniformly random directed edges per graph; x ~ N(0,1), 50 features), the reference PPI config
+(`run_config.py:18-33`: 3 layers, 4/4/6 heads, 256/256/121 features, concat/concat/mean, skip on
+layer 1, ELU between layers) with random (xavier) weights, eval mode. One step = graph
+preprocessing of a fresh batch (self-loop rewrite + CSR build, as every reference forward does
+per layer) + the 3-layer forward. Weak scaling: each rank processes its own G graphs; the forward
+has no exchange step, so there is no collective in the timed region (--mode train adds the
+backward and an RCCL gradient all-reduce, DDP-style).
+
+value = (sum over ranks of 3 layers x E' edges per step) / step time (max over ranks).
+roofline = the dominant kernel's algorithmic bytes (or flops) per launch / its average launch time,
+measured with HIP events on the launch stream during the timed steps. cpu_baseline = the numpy
+oracle (oracle/gat_oracle.py, the reference's dataflow restated) on a bounded sample, rank 0, N=1.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "gat-pytorch_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+FP32_MFMA_PEAK_TFS = 157.3   # v_mfma_f32_32x32x2_f32 dense peak (same table)
+
+
+def layer_dims(cfg):
+    heads = [1] + cfg["num_heads_per_layer"]
+    widths = cfg["head_output_features_per_layer"]
+    return [(heads[i] * widths[i], heads[i + 1], widths[i + 1], cfg["heads_concat_per_layer"][i])
+            for i in range(cfg["num_layers"])]
+
+
+def algorithmic(N, E2, F_in, NH, F, concat):
+    """SURVEY.md §8(d) per-layer algorithmic bytes / flops (fp32 = 4 B, int32 indices)."""
+    b_gemm = 4 * (N * F_in + F_in * NH * F + N * NH * F + 2 * N * NH)
+    f_gemm = 2 * N * F_in * NH * F + 4 * N * NH * NH * F
+    # edge_forward alone: rowptr + col + perm + s_src gathers + s_dst + Wh[src] rows + alpha
+    # write + den write + output write
+    b_edge_fwd = 4 * ((N + 1) + 2 * E2 + E2 * NH + N * NH + E2 * NH * F + E2 * NH + N * NH
+                      + (N * NH * F if concat else N * F))
+    # attention_max alone: col + rowidx + s gathers
+    b_max = 4 * (2 * E2 + 2 * E2 * NH)
+    b_edge_survey = 4 * (2 * (E2 + N + 1) + 2 * (E2 * NH + N * NH) + E2 * NH * F + E2 * NH
+                         + (N * NH * F if concat else N * F))
+    return dict(b_gemm=b_gemm, f_gemm=f_gemm, b_edge_fwd=b_edge_fwd, b_max=b_max,
+                b_edge=b_edge_survey)
+
+
+def cpu_baseline(model_np, cfg, budget_s=20.0):
+    """Time the numpy oracle (reference dataflow) on one PPI graph, 3-layer forward."""
+    from oracle import gat_oracle as orc
+    from gatx import data as gd
+    try:
+        from threadpoolctl import threadpool_limits
+    except Exception:  # pragma: no cover
+        threadpool_limits = None
+    cores = min(16, len(os.sched_getaffinity(0)))
+    b = gd.dataset_batch("PPI", 1, graph_seed=4242)
+    dims = layer_dims(cfg)
+    ctx = threadpool_limits(limits=cores) if threadpool_limits else None
+    times, e_tot = [], 0
+    try:
+        t_start = time.perf_counter()
+        while True:
+            t0 = time.perf_counter()
+            out, ei, alphas = orc.gat_model_forward(
+                b.x, b.edge_index, model_np["layers"], model_np["skips"],
+                cfg["num_heads_per_layer"], [d[2] for d in dims], cfg["heads_concat_per_layer"],
+                cfg["add_skip_connection"])
+            times.append(time.perf_counter() - t0)
+            e_tot = sum(a.shape[0] for a in alphas)
+            if time.perf_counter() - t_start > budget_s or len(times) >= 3:
+                break
+    finally:
+        if ctx is not None:
+            ctx.__exit__(None, None, None)
+    best = min(times)
+    return {"value": e_tot / best, "unit": "layer-edges/s", "cores": cores, "kind": "port",
+            "sample": f"numpy oracle (reference dataflow), PPI 3-layer fwd on 1 graph "
+                      f"(N={b.num_nodes}, sum E'={e_tot}), best of {len(times)}: {best:.2f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--graphs", type=int, default=20, help="PPI graphs per rank")
+    ap.add_argument("--mode", choices=["fwd", "train"], default="fwd")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cached-graph", action="store_true",
+                    help="reuse the CSR across steps (excludes graph preprocessing)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    dev = torch.device(f"cuda:{local}")
+
+    from gatx import GATModel, clear_graph_cache
+    from gatx import data as gd
+    from gatx.config import data_config
+    from gatx.functional import KernelTimer, set_kernel_timer
+
+    cfg = dict(data_config["PPI"])
+    torch.manual_seed(0)
+    model = GATModel(**cfg).to(dev)
+    model.train(args.mode == "train")
+    if args.mode == "fwd":
+        model.eval()
+    b = gd.dataset_batch("PPI", args.graphs, graph_seed=42 + 1000 * rank, feature_seed=1 + rank)
+    x = torch.from_numpy(b.x).to(dev)
+    ei = torch.from_numpy(b.edge_index).to(dev)
+    y = (torch.rand(b.num_nodes, cfg["num_classes"], device=dev) > 0.5).float()
+    opt = torch.optim.Adam(model.parameters(), lr=cfg["learning_rate"])
+    loss_fn = torch.nn.BCEWithLogitsLoss()
+    params = [p for p in model.parameters()]
+
+    def step():
+        if not args.cached_graph:
+            clear_graph_cache()
+        if args.mode == "fwd":
+            with torch.no_grad():
+                return model(x, ei)
+        out, _, atts = model.forward_and_return_attention(x, ei)
+        loss = loss_fn(out, y)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        if world > 1:   # DDP-style: one flat bucket (7.47 MB) all-reduced over RCCL
+            flat = torch.cat([p.grad.reshape(-1) for p in params])
+            dist.all_reduce(flat)
+            flat /= world
+            off = 0
+            for p in params:
+                n = p.numel()
+                p.grad.copy_(flat[off:off + n].view_as(p))
+                off += n
+        opt.step()
+        return out
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # per-layer E' of this batch
+    from gatx.graph import graph_cache
+    g = graph_cache.get(ei, b.num_nodes, True)
+    E2 = g.num_edges
+    N = b.num_nodes
+    dims = layer_dims(cfg)
+
+    timer = KernelTimer()
+    set_kernel_timer(timer)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    set_kernel_timer(None)
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms = elapsed / args.steps * 1e3
+
+    layer_edges = len(dims) * E2
+    alg = [algorithmic(N, E2, fin, NH, F, cc) for (fin, NH, F, cc) in dims]
+    bytes_step = sum(a["b_gemm"] + a["b_edge"] for a in alg)
+    value = layer_edges * world / (elapsed / args.steps)
+
+    # live per-kernel timing (HIP events on the launch stream) over the timed steps
+    summ = timer.summary()
+    kern = {}
+    for phase, recs in summ.items():
+        tot = sum(t for _, t in recs)
+        kern[phase] = {"launches": len(recs), "avg_ms": tot / len(recs), "total_ms_per_step":
+                       tot / args.steps}
+    edge_ms = sum(t for _, t in summ.get("edge_forward", []))
+    edge_b = sum(alg[i % 3]["b_edge_fwd"] for i in range(len(summ.get("edge_forward", []))))
+    gemm_ms = sum(t for _, t in summ.get("gemm", []))
+    gemm_f = sum(alg[i % 3]["f_gemm"] for i in range(len(summ.get("gemm", []))))
+    edge_gbs = edge_b / (edge_ms * 1e-3) / 1e9 if edge_ms else 0.0
+    gemm_tfs = gemm_f / (gemm_ms * 1e-3) / 1e12 if gemm_ms else 0.0
+    n_edge = max(1, len(summ.get("edge_forward", [])))
+    edge_roof = {"bound": "hbm", "kernel": "edge_forward", "achieved": round(edge_gbs, 1),
+                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(edge_gbs / HBM_PEAK_GBS, 4),
+                 "traffic": None, "bytes_per_launch": edge_b / n_edge,
+                 "avg_launch_ms": edge_ms / n_edge}
+    n_gemm = max(1, len(summ.get("gemm", [])))
+    gemm_roof = {"bound": "mfma", "kernel": "gemm_f32 (projection)", "achieved": round(gemm_tfs, 2),
+                 "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                 "frac": round(gemm_tfs / FP32_MFMA_PEAK_TFS, 4), "traffic": None,
+                 "flops_per_launch": gemm_f / n_gemm, "avg_launch_ms": gemm_ms / n_gemm}
+    dominant, other = (edge_roof, gemm_roof) if edge_ms >= gemm_ms else (gemm_roof, edge_roof)
+
+    result = {
+        "metric": "GAT-layer edges/sec + achieved HBM GB/s, PPI 3-layer fwd"
+                  + ("" if args.mode == "fwd" else " (+bwd, train step)"),
+        "value": round(value, 1), "unit": "layer-edges/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic PPI-shaped graphs (uniform random edges, N(0,1) features), xavier "
+                "weights",
+        "config": {"workload": f"PPI 3-layer GAT {args.mode} (4/4/6 heads, 256/256/121), "
+                               f"{args.graphs} graphs per GPU"
+                               + (", CSR cached" if args.cached_graph else ", CSR built per step"),
+                   "graphs_per_gpu": args.graphs, "nodes_per_gpu": N, "edges_per_layer": E2,
+                   "parallelism": f"graph-batch dp{world}"},
+        "achieved_GBps_algorithmic": round(bytes_step * world / (elapsed / args.steps) / 1e9 / world, 1),
+        "roofline_time_frac": round(sum(max((a["b_gemm"] + a["b_edge"]) / (HBM_PEAK_GBS * 1e9),
+                                            a["f_gemm"] / (FP32_MFMA_PEAK_TFS * 1e12))
+                                        for a in alg) / (ms * 1e-3), 4),
+        "roofline": dominant,
+        "roofline_other": other,
+        "kernels": kern,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.mode == "fwd":
+        model_np = {"layers": [(l.W.weight.detach().cpu().numpy(), l.a.weight.detach().cpu().numpy())
+                               for l in model.gat_layer_list],
+                    "skips": [None if isinstance(s, torch.nn.Identity) else s.weight.detach().cpu().numpy()
+                              for s in model.skip_layer_list]}
+        result["cpu_baseline"] = cpu_baseline(model_np, cfg)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

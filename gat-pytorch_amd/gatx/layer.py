@@ -1,0 +1,76 @@
+"""`GATLayer` — drop-in for the reference's `models/gat_layer.py:GATLayer`, running on libgatx.
+
+Same constructor signature, attributes, submodules and state-dict keys as the reference
+(`models/gat_layer.py:13-40`): `W` (nn.Linear, no bias), `a` (nn.Linear NH*2F -> NH, absent when
+const_attention), `bias_param` (when bias), `dropout_layer` (when dropout > 0), and the side effect
+`self.normalised_attention_coeffs = alpha` of every forward (`:110`). So it plugs into GATModel
+(`models/GATModel.py:69-79`), PPI_GAT / PlanetoidGAT / PatternGAT and their checkpoints unchanged.
+
+forward(x, edge_index, return_attention_weights=False) -> out, or (out, (edge_index', alpha)),
+exactly as `:42-140`. The computation is the reference's (including its quirks: the cross-head
+`a` mixing, one global max subtracted before LeakyReLU(0.01), the 1e-8 softmax epsilon with no
+per-segment max, isolated trailing nodes getting no self-loop), but fused into HIP kernels:
+no per-edge (E, NH, F) tensor is ever built. There is deliberately no CPU path.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from .functional import gat_layer
+
+
+class GATLayer(nn.Module):
+    def __init__(self, in_features, out_features, num_heads, concat, dropout=0,
+                 add_self_loops=False, bias=False, const_attention=False):
+        super().__init__()
+        self.in_features = in_features
+        self.out_features = out_features
+        self.num_heads = num_heads
+        self.concat = concat
+        self.dropout = dropout
+        self.add_self_loops = add_self_loops
+        self.bias = bias
+        self.const_attention = const_attention
+        self.device = "cuda" if torch.cuda.is_available() else "cpu"
+
+        self.W = nn.Linear(in_features=self.in_features,
+                           out_features=self.num_heads * self.out_features, bias=False)
+        if not const_attention:
+            self.a = nn.Linear(in_features=self.num_heads * (2 * self.out_features),
+                               out_features=self.num_heads, bias=False)
+        if self.dropout > 0:
+            self.dropout_layer = nn.Dropout(p=self.dropout)
+        if self.bias:
+            self.bias_param = nn.Parameter(torch.Tensor(self.num_heads * self.out_features))
+        self.normalised_attention_coeffs = None
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        nn.init.xavier_uniform_(self.W.weight)
+        if not self.const_attention:
+            nn.init.xavier_uniform_(self.a.weight)
+        if self.bias:
+            nn.init.zeros_(self.bias_param)
+
+    def _dropout_seed(self) -> int:
+        # one 64-bit draw from torch's CPU generator per forward: follows torch.manual_seed
+        return int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+
+    def forward(self, x, edge_index, return_attention_weights=False, *, graph=None):
+        p = float(self.dropout) if (self.dropout > 0 and self.training) else 0.0
+        seed = self._dropout_seed() if p > 0 else 0
+        out, edge_index_out, alpha = gat_layer(
+            x, edge_index, self.W.weight, None if self.const_attention else self.a.weight,
+            self.bias_param if self.bias else None, self.num_heads, self.out_features,
+            self.concat, self.add_self_loops, self.const_attention, p, seed, graph=graph)
+        self.normalised_attention_coeffs = alpha
+        if return_attention_weights:
+            return out, (edge_index_out, alpha)
+        return out
+
+    def extra_repr(self) -> str:
+        return (f"in_features={self.in_features}, out_features={self.out_features}, "
+                f"num_heads={self.num_heads}, concat={self.concat}, dropout={self.dropout}, "
+                f"add_self_loops={self.add_self_loops}, bias={self.bias}, "
+                f"const_attention={self.const_attention}")

@@ -1,0 +1,105 @@
+"""`GATModel` — the reference's layer stack (`models/GATModel.py:19-234`) without Lightning.
+
+Builds `num_layers` gatx GATLayers exactly as `GATModel.__init__` does (`:64-116`: heads list
+prefixed with 1, add_self_loops=True, bias=False, skip = Identity when widths match else a bias-free
+Linear), and runs the same `forward` (`:120-151`) / `forward_and_return_attention` (`:153-187`)
+wiring: input dropout -> layer -> skip (concat: add; mean: add head-mean of the skip) -> ELU except
+after the last layer. `calc_attention_norm` restates `:189-234`. Submodule names
+(`gat_layer_list.{i}.W.weight`, `.a.weight`, `skip_layer_list.{j}.weight`) match the reference's
+state-dict keys, so its checkpoints load (see gatx.checkpoint.read_state_dict).
+"""
+from __future__ import annotations
+
+from typing import List
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from .layer import GATLayer
+
+
+class GATModel(nn.Module):
+    def __init__(self, num_classes: int, num_input_node_features: int, num_layers: int,
+                 num_heads_per_layer: List[int], heads_concat_per_layer: List[bool],
+                 head_output_features_per_layer: List[int], add_skip_connection: List[bool],
+                 dropout: float, const_attention: bool = False, **kwargs):
+        super().__init__()
+        self.num_layers = num_layers
+        self.dropout = dropout
+        self.num_classes = num_classes
+        self.add_skip_connection = add_skip_connection
+        self.num_heads_per_layer = [1] + list(num_heads_per_layer)
+        self.head_output_features_per_layer = head_output_features_per_layer
+        self.heads_concat_per_layer = heads_concat_per_layer
+        self.const_attention = const_attention
+        self.lr = kwargs.get("learning_rate", 0.005)
+        self.l2_reg = kwargs.get("l2_reg", 0.0)
+        gat_layers, skip_layers = [], []
+        for i in range(num_layers):
+            fin = self.num_heads_per_layer[i] * head_output_features_per_layer[i]
+            gat_layers.append(GATLayer(
+                in_features=fin, out_features=head_output_features_per_layer[i + 1],
+                num_heads=self.num_heads_per_layer[i + 1], concat=heads_concat_per_layer[i],
+                dropout=dropout, bias=False, add_self_loops=True,
+                const_attention=const_attention))
+            if add_skip_connection[i]:
+                skip_out = self.num_heads_per_layer[i + 1] * head_output_features_per_layer[i + 1]
+                skip_layers.append(nn.Identity() if fin == skip_out
+                                   else nn.Linear(fin, skip_out, bias=False))
+        self.gat_layer_list = nn.ModuleList(gat_layers)
+        self.skip_layer_list = nn.ModuleList(skip_layers)
+
+    def _skip(self, i, skip_count, layer_input, x):
+        skip_output = self.skip_layer_list[skip_count](layer_input)
+        if self.heads_concat_per_layer[i]:
+            return x + skip_output
+        skip_output = skip_output.view(-1, self.num_heads_per_layer[i + 1],
+                                       self.head_output_features_per_layer[i + 1])
+        return x + skip_output.mean(dim=1)
+
+    def forward(self, x, edge_index):
+        skip_count = 0
+        for i in range(len(self.gat_layer_list)):
+            layer_input = x
+            x = F.dropout(x, p=self.dropout, training=self.training)
+            x = self.gat_layer_list[i](x, edge_index)
+            if self.add_skip_connection[i]:
+                x = self._skip(i, skip_count, layer_input, x)
+                skip_count += 1
+            if i != len(self.gat_layer_list) - 1:
+                x = F.elu(x)
+        return x
+
+    def forward_and_return_attention(self, x, edge_index, return_attention_weights=True):
+        attention_weights_list = []
+        skip_count = 0
+        for i in range(len(self.gat_layer_list)):
+            layer_input = x
+            x = F.dropout(x, p=self.dropout, training=self.training)
+            x, (edge_index, att) = self.gat_layer_list[i](
+                x, edge_index, return_attention_weights=return_attention_weights)
+            attention_weights_list.append(att)
+            if self.add_skip_connection[i]:
+                x = self._skip(i, skip_count, layer_input, x)
+                skip_count += 1
+            if i != len(self.gat_layer_list) - 1:
+                x = F.elu(x)
+        return x, edge_index, attention_weights_list
+
+    @staticmethod
+    def calc_attention_norm(edge_index, attention_list):
+        """mean over layers of ||alpha * in_degree[dst] - 1||_1 / E (`models/GATModel.py:189-234`)."""
+        dst = edge_index[1]
+        E = dst.numel()
+        first = attention_list[0]
+        deg = torch.zeros(E, dtype=first.dtype, device=first.device)
+        deg.scatter_add_(0, dst, torch.ones(E, dtype=first.dtype, device=first.device))
+        deg = deg.index_select(0, dst)
+        norm = torch.zeros((), dtype=first.dtype, device=first.device)
+        for att in attention_list:
+            norm = norm + torch.norm(att * deg.unsqueeze(-1) - 1.0, p=1) / E
+        return norm / len(attention_list)
+
+    def configure_optimizers(self):
+        return torch.optim.Adam(self.parameters(), lr=self.lr, weight_decay=self.l2_reg)

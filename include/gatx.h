@@ -1,0 +1,160 @@
+/*
+ * gatx — MI355X-native GATLayer hot path: C-ABI of libgatx.so.
+ *
+ * The reference (loodvn/gat-pytorch) is pure Python and has no FFI: its plugin point for this path
+ * is the nn.Module `GATLayer` (`models/gat_layer.py:6-148`), picked by `LayerType`
+ * (`run_config.py:4-6`) and constructed in `GATModel.__init__` (`models/GATModel.py:69-79`).
+ * The Python mirror of that module (gat-pytorch_amd/gatx/layer.py) binds the entry points below
+ * with ctypes; each one says which piece of the reference it replaces.
+ *
+ * Conventions
+ *   - All pointers are DEVICE pointers unless stated; all launches go to `stream` (the caller's
+ *     current HIP stream); nothing allocates, frees or synchronises, so every call is capturable
+ *     into a hipGraph. Scratch memory comes from the caller (`*_workspace_bytes` says how much).
+ *   - Node ids and edge positions are int32 (graphs up to 2^31-1 edges/nodes); features are fp32.
+ *   - Return value: 0 on success, otherwise a hipError_t code (launch errors are checked after each
+ *     launch) or GATX_EINVAL for unsupported shapes. gatx_last_error() gives a message.
+ *   - Layout (per layer): NH heads, F features per head, Fp = round_up(F, 4),
+ *     Dp = NH*Fp. Wh is [N][Dp] (head-major, each head padded to Fp so a float4 never straddles a
+ *     head); S is [N][2*NH] = (s_src | s_dst) per node, the attention logit factors; the augmented
+ *     projection weight W_aug is [Dp + 2*NH][F_in].
+ */
+#ifndef GATX_H
+#define GATX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* gatx_stream_t; /* == hipStream_t */
+
+#define GATX_EINVAL 1000
+#define GATX_ARGMAX_CAP 1024 /* argmax (edge, head) slots recorded for the max() gradient */
+
+const char* gatx_last_error(void);
+int gatx_version(void);
+
+/* ---------------------------------------------------------------- graph (models/utils.py) */
+
+/* min / max node id and self-loop count of an edge_index (2, E) (int64 if index_is_int64 else
+ * int32; rows `ld` elements apart). stats: device int64[3] = {min, max, n_selfloops}.
+ * Replaces the `index.max()` of maybe_num_nodes (models/utils.py:70-72) and the `row != col`
+ * mask count of add_remaining_self_loops (models/utils.py:58-60). */
+int gatx_edge_stats(const void* edge_index, int index_is_int64, int64_t E, int64_t ld,
+                    int64_t* stats, gatx_stream_t stream);
+
+/* Self-loop rewrite + destination CSR, one pass of device kernels.
+ * edge_index' = [edges with src != dst in input order | (i, i) for i < num_loops] when
+ * add_self_loops (models/utils.py:47-67; num_loops = max+1), else edge_index unchanged.
+ * Outputs (E2 = |edge_index'|): edge_index_out int64 (2, E2) (may be NULL), and the CSR of
+ * edge_index' by destination over num_nodes rows, stable in edge_index' order:
+ *   rowptr [num_nodes+1], col [E2] = source id, rowidx [E2] = destination id,
+ *   perm [E2] = position in edge_index' of each CSR slot.
+ * Replaces the per-layer `add_remaining_self_loops` call (models/gat_layer.py:53-54) and the
+ * scatter/gather index plumbing of sum_over_neighbourhood / explicit_broadcast. */
+size_t gatx_graph_build_workspace_bytes(int64_t E, int64_t E2, int64_t num_nodes);
+int gatx_graph_build(const void* edge_index, int index_is_int64, int64_t E, int64_t ld,
+                     int add_self_loops, int64_t num_loops, int64_t num_nodes, int64_t E2,
+                     int64_t* edge_index_out, int32_t* rowptr, int32_t* col, int32_t* rowidx,
+                     int32_t* perm, void* workspace, size_t workspace_bytes,
+                     gatx_stream_t stream);
+
+/* Source-ordered transpose of the CSR (for the backward's scatters to source nodes):
+ * srowptr [num_nodes+1], scol [E2] = destination id, seid [E2] = dst-CSR slot. */
+size_t gatx_graph_transpose_workspace_bytes(int64_t E2, int64_t num_nodes);
+int gatx_graph_transpose(const int32_t* col, const int32_t* rowidx, int64_t num_nodes, int64_t E2,
+                         int32_t* srowptr, int32_t* scol, int32_t* seid, void* workspace,
+                         size_t workspace_bytes, gatx_stream_t stream);
+
+/* ---------------------------------------------------------------- projection (gat_layer.py:64) */
+
+/* W_aug [(Dp + 2*NH) x F_in] from W.weight [NH*F x F_in] and a.weight [NH x NH*2F]:
+ * rows h*Fp+f = W[h*F+f] (pad rows 0); row Dp+h = (A_src W)[h]; row Dp+NH+h = (A_dst W)[h], where
+ * A_src[h][k*F+f] = a[h][k*2F+f], A_dst[h][k*F+f] = a[h][k*2F+F+f] (the src/dst halves of the
+ * (E, NH*2F) concatenation of gat_layer.py:76-82). a == NULL (const_attention): no extra rows. */
+int gatx_prepare_weights(const float* W, const float* a, int NH, int F, int64_t F_in,
+                         float* W_aug, gatx_stream_t stream);
+/* Floats the W_aug buffer must hold: (Dp + 2NH) * F_in plus split-K scratch behind it. */
+int64_t gatx_prepare_weights_floats(int NH, int F, int64_t F_in, int has_a);
+
+/* fp32 GEMM on MFMA (v_mfma_f32_32x32x2_f32): C = A * B (+ C if accumulate).
+ * A(m,k) = A[m*sam + k*sak], B(k,n) = B[k*sbk + n*sbn]; one of sam/sak and one of sbk/sbn must
+ * be 1. Output column n < n_split goes to C0[m*ldc0 + n], n >= n_split to C1[m*ldc1 + n-n_split].
+ * Used for Wh|S = x * W_aug^T (gat_layer.py:64 + the per-edge `a` GEMV of :82 folded into per-node
+ * scores), and for the backward's g_x = G_aug * W_aug and g_W_aug = G_aug^T * x. */
+int gatx_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t sam, int64_t sak,
+                  const float* B, int64_t sbk, int64_t sbn, float* C0, int64_t ldc0,
+                  int64_t n_split, float* C1, int64_t ldc1, int accumulate, gatx_stream_t stream);
+
+/* ---------------------------------------------------------------- attention + aggregation */
+
+/* Global max M = max_{e,h} s_src[col[e],h] + s_dst[rowidx[e],h]  (gat_layer.py:85), written as an
+ * order-preserving uint32 into *M_ord (device). */
+int gatx_attention_max(const int32_t* col, const int32_t* rowidx, int64_t E2, const float* S,
+                       int NH, uint32_t* M_ord, gatx_stream_t stream);
+
+/* Fused edge pass per destination segment (gat_layer.py:85-135):
+ *   ex = exp(0.01 * (s_src[src] + s_dst[dst] - M))   (LeakyReLU(0.01) of a non-positive value)
+ *   den[n,h] = sum_{e->n} ex;  alpha = ex / (den[dst] + 1e-8)   (no per-segment max: :96-109)
+ *   out[n,h,:] = sum_{e->n} alpha~ * Wh[src,h,:]   (alpha~ = dropout(alpha), :113-127)
+ *   concat: out [N][NH*F]; else out [N][F] = head mean (:129-132); + bias (:134-135, nullable).
+ * alpha is written in edge_index' order ([E2][NH], via perm); den [N][NH] is kept for the
+ * backward; argmax = int64[GATX_ARGMAX_CAP + 2]: count, then (csr_slot*NH + h) of raw == M
+ * entries, then one scratch slot for gatx_max_backward (zeroed by the caller). const_attention: ex = 1 (S, M, argmax unused).
+ * dropout_p > 0 applies the counter-based keep mask dropout_keep(seed, e', h) (gatx_common.h). */
+int gatx_edge_forward(const float* Wh, const float* S, const uint32_t* M_ord,
+                      const int32_t* rowptr, const int32_t* col, const int32_t* perm,
+                      int64_t num_nodes, int NH, int F, int concat, int const_attention,
+                      const float* bias, float dropout_p, uint64_t seed, float* out, float* alpha,
+                      float* den, int64_t* argmax, gatx_stream_t stream);
+
+/* ---------------------------------------------------------------- backward (autograd of above) */
+
+/* Destination pass. go = g_out (concat [N][NH*F]; mean [N][F], scaled by 1/NH inside).
+ *   g_alpha~[e,h] = <go[dst,h,:], Wh[src,h,:]>; g_alpha = g_alpha~ * keep/(1-p) + g_alpha_ret
+ *   c[n,h] = sum_{e->n} g_alpha * alpha; g_raw'[e,h] = 0.01 * ex * (g_alpha - c) / (den + 1e-8)
+ * Writes g_raw' [E2][NH] in CSR order, g_s_dst into G_aug[n][Dp+NH+h] and one partial sum of
+ * g_raw' per workgroup into partials [gatx_edge_backward_dst_partials(num_nodes)].
+ * g_alpha_ret (the returned alpha's gradient, edge_index' order) may be NULL. */
+int64_t gatx_edge_backward_dst_partials(int64_t num_nodes);
+int gatx_edge_backward_dst(const float* Wh, const float* S, const uint32_t* M_ord,
+                           const float* den, const int32_t* rowptr, const int32_t* col,
+                           const int32_t* perm, int64_t num_nodes, int NH, int F, int concat,
+                           float dropout_p, uint64_t seed, const float* g_out,
+                           const float* g_alpha_ret, float* g_raw, float* G_aug, int64_t ldg,
+                           float* partials, gatx_stream_t stream);
+
+/* max() backward (torch splits the gradient evenly over ties): g_M = -sum(partials);
+ * g_corr_src[src,h] += g_M/k and G_aug[dst][Dp+NH+h] += g_M/k for each recorded argmax entry.
+ * g_corr_src [N][NH] must be zeroed by the caller. Falls back to a full scan of the edges when
+ * more than GATX_ARGMAX_CAP entries tie. */
+int gatx_max_backward(const float* partials, int64_t n_partials, const int64_t* argmax,
+                      const float* S, const uint32_t* M_ord, const int32_t* col,
+                      const int32_t* rowidx, int64_t E2, int NH, float* g_corr_src, float* G_aug,
+                      int64_t ldg, int64_t Dp, gatx_stream_t stream);
+
+/* Source pass: G_aug[s][0:Dp] = sum_{e: src=s} alpha~[e,h] * go[dst_e,h,:] (the message
+ * gradient), G_aug[s][Dp+h] = sum_{e: src=s} g_raw'[e,h] + g_corr_src[s,h] (g_s_src). */
+int gatx_edge_backward_src(const float* S, const uint32_t* M_ord, const float* den,
+                           const int32_t* srowptr, const int32_t* scol, const int32_t* seid,
+                           const int32_t* perm, int64_t num_nodes, int NH, int F, int concat,
+                           int const_attention, float dropout_p, uint64_t seed,
+                           const float* g_out, const float* g_raw, const float* g_corr_src,
+                           float* G_aug, int64_t ldg, gatx_stream_t stream);
+
+/* From g_W_aug [(Dp+2NH) x F_in] (= G_aug^T x): g_W [NH*F x F_in] and g_a [NH x NH*2F]
+ * (a may be NULL for const_attention; then g_a is untouched). */
+int gatx_weight_grads(const float* gW_aug, const float* W, const float* a, int NH, int F,
+                      int64_t F_in, float* g_W, float* g_a, gatx_stream_t stream);
+
+/* Column sums: out[j] = sum_i X[i*ld + j], j < ncols (bias gradient). */
+int gatx_colsum(const float* X, int64_t nrows, int64_t ncols, int64_t ld, float* out,
+                gatx_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GATX_H */

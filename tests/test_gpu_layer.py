@@ -1,0 +1,222 @@
+"""GPU parity: the HIP path (libgatx.so via gatx.GATLayer) against the reference goldens and the
+CPU oracle. Tolerances: outputs / alpha 1e-4 absolute (north_star); gradients
+max|d| <= 1e-4 * max(1, max|ref|) (from the reference's own fp32-vs-fp64 noise)."""
+import numpy as np
+import pytest
+import torch
+
+from golden_io import LAYER_CASES, MODEL_CASES, grad_seeds, load_layer_case, load_model_case
+from oracle import gat_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+OUT_TOL = 1e-4
+GRAD_TOL = 1e-4
+
+
+def _gatx():
+    import gatx
+    from gatx import functional  # noqa: F401
+    return gatx
+
+
+def run_gpu_layer(c, device, with_grads=True):
+    gatx = _gatx()
+    m = c["meta"]
+    layer = gatx.GATLayer(m["in_features"], m["out_features"], m["num_heads"], m["concat"],
+                          dropout=m["dropout"], add_self_loops=m["add_self_loops"],
+                          bias=m["has_bias"], const_attention=m["const_attention"]).to(device)
+    with torch.no_grad():
+        layer.W.weight.copy_(torch.from_numpy(c["W"]))
+        if not m["const_attention"]:
+            layer.a.weight.copy_(torch.from_numpy(c["a"]))
+        if m["has_bias"]:
+            layer.bias_param.copy_(torch.from_numpy(c["bias"]))
+    if m["dropout"] > 0:
+        layer._dropout_seed = lambda: m["seed"]
+        layer.train()
+    x = torch.from_numpy(np.ascontiguousarray(c["x"])).to(device).requires_grad_(with_grads)
+    ei = torch.from_numpy(np.ascontiguousarray(c["edge_index"])).to(device)
+    out, (ei2, alpha) = layer(x, ei, return_attention_weights=True)
+    res = dict(out=out.detach().cpu().numpy(), alpha=alpha.detach().cpu().numpy(),
+               edge_index=ei2.cpu().numpy(), layer=layer)
+    if with_grads:
+        g_out, g_alpha = grad_seeds(tuple(out.shape), tuple(alpha.shape))
+        loss = (out * torch.from_numpy(g_out).to(device)).sum()
+        if m["use_g_alpha"]:
+            loss = loss + (alpha * torch.from_numpy(g_alpha).to(device)).sum()
+        loss.backward()
+        res["grad_x"] = x.grad.cpu().numpy()
+        res["grad_W"] = layer.W.weight.grad.cpu().numpy()
+        if not m["const_attention"]:
+            res["grad_a"] = layer.a.weight.grad.cpu().numpy()
+        if m["has_bias"]:
+            res["grad_bias"] = layer.bias_param.grad.cpu().numpy()
+    return res
+
+
+@pytest.mark.parametrize("name", LAYER_CASES)
+def test_layer_matches_reference_goldens(name, device):
+    c = load_layer_case(name)
+    r = run_gpu_layer(c, device)
+    np.testing.assert_array_equal(r["edge_index"], c["edge_index_out"])
+    e = c["expected"]
+    e["out"].check(r["out"], OUT_TOL, what="gpu ")
+    e["alpha"].check(r["alpha"], OUT_TOL, what="gpu ")
+    for k in ("grad_x", "grad_W", "grad_a", "grad_bias"):
+        if k in e:
+            e[k].check(r[k], GRAD_TOL, rtol_scale=True, what="gpu ")
+
+
+@pytest.mark.parametrize("name", MODEL_CASES)
+def test_model_matches_reference_goldens(name, device):
+    gatx = _gatx()
+    c = load_model_case(name)
+    cfg = c["cfg"]
+    model = gatx.GATModel(**cfg).to(device).eval()
+    skip_i = 0
+    with torch.no_grad():
+        for i, (W, a) in enumerate(c["layers"]):
+            model.gat_layer_list[i].W.weight.copy_(torch.from_numpy(W))
+            model.gat_layer_list[i].a.weight.copy_(torch.from_numpy(a))
+        for j, s in enumerate(c["skips"]):
+            if s is not None:
+                model.skip_layer_list[j].weight.copy_(torch.from_numpy(s))
+    x = torch.from_numpy(c["x"]).to(device)
+    ei = torch.from_numpy(c["edge_index"]).to(device)
+    with torch.no_grad():
+        out, ei2, alphas = model.forward_and_return_attention(x, ei)
+    np.testing.assert_array_equal(ei2.cpu().numpy(), c["edge_index_out"])
+    c["expected"]["out"].check(out.cpu().numpy(), OUT_TOL, what="gpu ")
+    for i, al in enumerate(alphas):
+        c["expected"][f"alpha{i}"].check(al.cpu().numpy(), OUT_TOL, what="gpu ")
+    with torch.no_grad():
+        out2 = model(x, ei)
+    np.testing.assert_array_equal(out2.cpu().numpy(), out.cpu().numpy())
+
+
+def test_gemm_mfma_layout(device):
+    """A = I with an asymmetric B (catches row/col swaps), plus ragged sizes and all four operand
+    layouts against a float64 matmul."""
+    from gatx._lib import call, ptr, stream
+    torch.manual_seed(0)
+    for (M, N, K) in [(64, 64, 64), (130, 97, 33), (257, 1032, 50), (5, 3, 1), (300, 20, 1100)]:
+        A = torch.randn(M, K, device=device)
+        B = torch.randn(K, N, device=device)
+        ref = (A.double() @ B.double()).float()
+        for a_t in (False, True):
+            for b_t in (False, True):
+                Am = A.t().contiguous() if a_t else A   # stored transposed: A(m,k) = Am[k, m]
+                Bm = B.t().contiguous() if b_t else B
+                sam, sak = (1, M) if a_t else (K, 1)
+                sbk, sbn = (1, K) if b_t else (N, 1)
+                C = torch.full((M, N), float("nan"), device=device)
+                call("gatx_gemm_f32", M, N, K, ptr(Am), sam, sak, ptr(Bm), sbk, sbn, ptr(C), N,
+                     N, None, 0, 0, stream())
+                torch.cuda.synchronize()
+                err = (C - ref).abs().max().item()
+                assert err < 1e-4 * max(1.0, K ** 0.5), (M, N, K, a_t, b_t, err)
+    # identity check with asymmetric B and a split output
+    M = N = K = 96
+    I = torch.eye(M, device=device)
+    B = torch.arange(K * N, device=device, dtype=torch.float32).reshape(K, N) / 7.0
+    C0 = torch.zeros(M, 64, device=device)
+    C1 = torch.zeros(M, N - 64, device=device)
+    call("gatx_gemm_f32", M, N, K, ptr(I), K, 1, ptr(B), N, 1, ptr(C0), 64, 64, ptr(C1), N - 64,
+         0, stream())
+    torch.cuda.synchronize()
+    assert torch.equal(torch.cat([C0, C1], 1), B)
+
+
+def test_graph_build_matches_oracle(device):
+    gatx = _gatx()
+    from gatx import data as gd
+    b = gd.uniform_graph_batch(3, 500, 4000, 4)
+    ei = b.edge_index.copy()
+    ei[:, :50] = ei[0, :50]            # some self-loops
+    ei = np.concatenate([ei, ei[:, :100]], 1)   # duplicates
+    t = torch.from_numpy(ei).to(device)
+    g = gatx.Graph(t, b.num_nodes + 7, True)   # trailing isolated nodes too
+    ref = orc.add_remaining_self_loops(ei)
+    np.testing.assert_array_equal(g.edge_index.cpu().numpy(), ref)
+    rowptr, col, perm = (v.numpy() for v in g.csr_host())
+    dst = ref[1]
+    order = np.argsort(dst, kind="stable")
+    np.testing.assert_array_equal(perm, order)
+    np.testing.assert_array_equal(col, ref[0][order])
+    counts = np.bincount(dst, minlength=b.num_nodes + 7)
+    np.testing.assert_array_equal(np.diff(rowptr), counts)
+    g.ensure_transpose()
+    srow = g.srowptr.cpu().numpy()
+    scol = g.scol[:g.num_edges].cpu().numpy()
+    seid = g.seid[:g.num_edges].cpu().numpy()
+    np.testing.assert_array_equal(np.diff(srow), np.bincount(ref[0], minlength=b.num_nodes + 7))
+    np.testing.assert_array_equal(col[seid], np.sort(ref[0], kind="stable"))
+    np.testing.assert_array_equal(scol, dst[order][seid])
+
+
+def _layer_vs_oracle(device, G, n, e, fin, NH, F, concat, seed=5, grads=True, dropout=0.0):
+    gatx = _gatx()
+    from gatx import data as gd
+    b = gd.uniform_graph_batch(G, n, e, fin, feature_seed=seed)
+    W = gd.xavier_uniform(seed + 1, NH * F, fin)
+    a = gd.xavier_uniform(seed + 2, NH, NH * 2 * F)
+    c = dict(meta=dict(in_features=fin, out_features=F, num_heads=NH, concat=concat,
+                       dropout=dropout, add_self_loops=True, has_bias=False,
+                       const_attention=False, seed=77, use_g_alpha=True),
+             x=b.x, edge_index=b.edge_index, W=W, a=a, bias=None)
+    r = run_gpu_layer(c, device, with_grads=grads)
+    keep = orc.dropout_keep(77, r["alpha"].shape[0], NH, dropout) if dropout > 0 else None
+    out, ei2, alpha, cache = orc.gat_layer_forward(b.x, b.edge_index, W, a, NH, F, concat,
+                                                   dropout_p=dropout, keep=keep)
+    np.testing.assert_array_equal(r["edge_index"], ei2)
+    assert np.abs(r["out"] - out).max() <= OUT_TOL
+    assert np.abs(r["alpha"] - alpha).max() <= OUT_TOL
+    if grads:
+        g_out, g_alpha = grad_seeds(out.shape, alpha.shape)
+        gr = orc.gat_layer_backward(cache, g_out, g_alpha)
+        for k in ("x", "W", "a"):
+            ref = gr[k]
+            err = np.abs(r[f"grad_{k}"] - ref).max()
+            assert err <= GRAD_TOL * max(1.0, np.abs(ref).max()), (k, err, np.abs(ref).max())
+    return r
+
+
+@pytest.mark.parametrize("layer", ["l0", "l1", "l2"])
+def test_ppi_full_graph_vs_oracle(layer, device):
+    """PPI layer shapes on one full-size PPI graph (n=2245, e=61318), fwd + bwd vs the oracle."""
+    fin, NH, F, cc = {"l0": (50, 4, 256, True), "l1": (1024, 4, 256, True),
+                      "l2": (1024, 6, 121, False)}[layer]
+    _layer_vs_oracle(device, 1, 2245, 61318, fin, NH, F, cc)
+
+
+def test_cora_shape_dropout_vs_oracle(device):
+    _layer_vs_oracle(device, 1, 2708, 10556, 64, 8, 8, True, dropout=0.6)
+
+
+@pytest.mark.parametrize("NH,F,concat", [(1, 1, False), (4, 3, True), (2, 5, True), (3, 17, False),
+                                         (8, 64, True), (6, 121, True), (16, 128, True),
+                                         (2, 1024, True)])
+def test_geometries_vs_oracle(NH, F, concat, device):
+    """Every lane geometry (lanes per edge 1..64, 1..8 float4 chunks per lane), padding of F."""
+    _layer_vs_oracle(device, 2, 60, 700, 9, NH, F, concat)
+
+
+def test_deterministic(device):
+    """Fixed-order reductions everywhere: two runs are bitwise identical."""
+    a = _layer_vs_oracle(device, 2, 300, 5000, 32, 4, 16, True, grads=True)
+    b = _layer_vs_oracle(device, 2, 300, 5000, 32, 4, 16, True, grads=True)
+    for k in ("out", "alpha", "grad_x", "grad_W", "grad_a"):
+        assert np.array_equal(a[k], b[k]), k
+
+
+def test_errors_mirror_reference(device):
+    gatx = _gatx()
+    layer = gatx.GATLayer(4, 3, 2, True, add_self_loops=True).to(device)
+    x = torch.randn(5, 4, device=device)
+    with pytest.raises(RuntimeError):
+        layer(x, torch.zeros((2, 0), dtype=torch.int64, device=device))
+    with pytest.raises(IndexError):
+        layer(x, torch.tensor([[0, 7], [1, 2]], device=device))
+    with pytest.raises(RuntimeError):
+        layer(x.cpu(), torch.tensor([[0, 1], [1, 2]]))
