@@ -18,11 +18,16 @@ namespace gatx {
 namespace {
 
 // ------------------------------------------------------------------ global max pre-pass
+// Two launches: per-block maxima into a partials array (no single-address atomic contention:
+// thousands of workgroups hitting one word serialise at the memory side), then one block folds
+// them. max is order-independent, so the result is exact and deterministic.
+constexpr int kMaxBlocks = 2048;
+
 __global__ void __launch_bounds__(256) attention_max_kernel(const int32_t* __restrict__ col,
                                                             const int32_t* __restrict__ rowidx,
                                                             int64_t E2,
                                                             const float* __restrict__ S, int NH,
-                                                            uint32_t* M_ord) {
+                                                            float* __restrict__ part) {
   const int S2 = 2 * NH;
   float m = -INFINITY;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E2;
@@ -35,132 +40,277 @@ __global__ void __launch_bounds__(256) attention_max_kernel(const int32_t* __res
   __shared__ float red[4];
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
+  if (threadIdx.x == 0)
+    part[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+__global__ void __launch_bounds__(256) max_final_kernel(const float* __restrict__ part, int nb,
+                                                        uint32_t* __restrict__ M_ord) {
+  float m = -INFINITY;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) m = fmaxf(m, part[b]);
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
   if (threadIdx.x == 0) {
-    for (int k = 1; k < (int)(blockDim.x >> 6); ++k) m = fmaxf(m, red[k]);
-    if (m > -INFINITY) atomicMax(M_ord, float_to_ord(m));
+    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    *M_ord = m > -INFINITY ? float_to_ord(m) : 0u;
   }
 }
 
 // ------------------------------------------------------------------ fused edge pass
-// LPE lanes per edge, CPL float4 chunks per lane; lane l of edge group g owns chunks
-// q = c*LPE + (l % LPE), c < CPL, of the padded row (D4 = NH*Fp/4 chunks; head of q = q/(Fp/4)).
-template <int LPE, int CPL>
-__global__ void __launch_bounds__(256)
-edge_forward_kernel(const float* __restrict__ Wh, const float* __restrict__ S,
-                    const uint32_t* __restrict__ M_ord, const int32_t* __restrict__ rowptr,
-                    const int32_t* __restrict__ col, const int32_t* __restrict__ perm,
-                    int64_t N, int NH, int F, int Fp, int concat, int const_att,
-                    const float* __restrict__ bias, float p_drop, uint64_t seed,
-                    float* __restrict__ out, float* __restrict__ alpha,
-                    float* __restrict__ den_out, long long* __restrict__ argmax, int lds_row) {
+struct EdgeFwdArgs {
+  const float* rows;       // gathered source rows: Wh [N][NH][Fp] (or x [N][Fp], head_stride4 0)
+  int64_t row_stride4;     // float4s per source row
+  int head_stride4;        // float4s between heads inside a source row
+  const float* S;
+  const uint32_t* M_ord;
+  const int32_t* rowptr;
+  const int32_t* col;
+  const int32_t* perm;
+  int64_t N;
+  int NH, F, Fp, HS;       // heads, features (output), padded features, heads per work item
+  int concat, const_att;
+  const float* bias;
+  float p_drop;
+  uint64_t seed;
+  float* out;
+  int64_t out_ld;
+  const float* resid;      // fused epilogue: out = elu?(agg + bias + resid)
+  int64_t resid_ld;
+  int elu;
+  float* den;
+  int lds_row;
+  int64_t chunk;           // destination nodes per (chunk, head-group) sweep
+  int64_t n_items;
+  int dbg;                 // diagnostic ablations (gatx_set_debug); 0 in production
+};
+
+int g_debug = 0;
+
+// XCD-contiguous block order: blocks are dealt round-robin to the 8 XCDs (b % 8); hand XCD x
+// the x-th contiguous range of work items so one XCD sweeps one (node chunk, head group) at a
+// time and its 4 MB L2 holds that head's slice of the gathered rows. Speed only, never results.
+__device__ inline int64_t xcd_contiguous(int64_t b, int64_t nb) {
+  const int64_t q = nb / 8, r = nb % 8, xcd = b % 8, j = b / 8;
+  return (xcd < r) ? xcd * (q + 1) + j : r * (q + 1) + (xcd - r) * q + j;
+}
+
+__device__ inline float epilogue(float v, const EdgeFwdArgs& g, int64_t n, int64_t col) {
+  if (g.resid) v += g.resid[n * g.resid_ld + col];
+  if (g.elu) v = v > 0.f ? v : expm1f(v);
+  return v;
+}
+
+constexpr int kMaxHS = 8;   // heads per work item held in registers by the batch phase
+
+__device__ inline int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ inline float lane_f(float v, int j) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+}
+
+// One wavefront per work item = (destination node n, group of HS heads). Edges are taken in
+// batches of 64: lane j loads batch edge j's source id (one coalesced load) and computes its HS
+// attention weights ex = exp(0.01 (s_src[src] + s_dst[n] - M)) (one gather of s_src per head).
+// The gather phase then streams the source rows with no dependent address latency:
+//  - LPE == 64 (one edge per wave step): the source id is wave-uniform (readlane -> SGPR, scalar
+//    row address); with one head per item (SCALAR_W) so is its weight.
+//  - LPE < 64 (narrow rows, 64/LPE edges per step): ids and weights through LDS.
+// Lane l of edge group grp owns chunks q = c*LPE + (l % LPE) of the item's HS*Fp/4; chunks past
+// the row end load a valid address of the same row and are never stored (branch-free loop).
+// Everything that indexes work (item, node, edge range) is made wave-uniform explicitly.
+template <int LPE, int CPL, int U, bool SCALAR_W>
+__global__ void __launch_bounds__(256) edge_forward_kernel(EdgeFwdArgs g) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int EPW = 64 / LPE;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = uni(threadIdx.x >> 6);
   const int grp = lane / LPE, li = lane % LPE;
-  const int D4 = NH * Fp / 4, F4 = Fp / 4, S2 = 2 * NH;
-  float* row_lds = smem + wave * lds_row;      // Dp floats (head-mean staging)
-  float* den_lds = row_lds + NH * Fp;          // NH floats
-  const float M = const_att ? 0.f : ord_to_float(*M_ord);
-  const bool drop = p_drop > 0.f;
-  const float drop_scale = drop ? 1.f / (1.f - p_drop) : 1.f;
-  const float4* __restrict__ Wh4 = (const float4*)Wh;
+  const int64_t item = xcd_contiguous(blockIdx.x, gridDim.x) * 4 + wave;
+  if (item >= g.n_items) return;
+  const int NG = g.NH / g.HS;
+  const int64_t per_chunk = g.chunk * NG;
+  const int64_t ck = item / per_chunk, rem = item - ck * per_chunk;
+  const int hg = (int)(rem / g.chunk);
+  const int64_t n = ck * g.chunk + (rem - (int64_t)hg * g.chunk);
+  if (n >= g.N) return;
+  const int h0 = hg * g.HS, HS = g.HS;
+  const int NH = g.NH, F = g.F, Fp = g.Fp, F4 = Fp / 4, S2 = 2 * NH;
+  const int D4 = HS * F4;
+  // per-wave LDS: [HS*Fp head-mean staging][HS den][64 src ids][HS*64 edge weights]
+  float* row_lds = smem + wave * g.lds_row;
+  float* den_lds = row_lds + HS * Fp;
+  int* src_lds = (int*)(den_lds + HS);
+  float* w_lds = (float*)(src_lds + 64);
+  const float M = g.const_att ? 0.f : ord_to_float(*g.M_ord);
+  const bool drop = g.p_drop > 0.f;
+  const float drop_scale = drop ? 1.f / (1.f - g.p_drop) : 1.f;
+  const float4* __restrict__ rows4 = (const float4*)g.rows;
+  const float* __restrict__ S = g.S;
+  const int32_t* __restrict__ col = g.col;
 
-  int q[CPL], hc[CPL];
+  int q[CPL], hl[CPL], off4[CPL];
   bool vq[CPL];
 #pragma unroll
   for (int c = 0; c < CPL; ++c) {
     q[c] = c * LPE + li;
     vq[c] = q[c] < D4;
-    hc[c] = vq[c] ? q[c] / F4 : 0;
+    const int qq = vq[c] ? q[c] : 0;
+    hl[c] = qq / F4;
+    off4[c] = (h0 + hl[c]) * g.head_stride4 + (qq - hl[c] * F4);
   }
+  float sdst[kMaxHS], dnl[kMaxHS];
+#pragma unroll
+  for (int h = 0; h < kMaxHS; ++h) {
+    sdst[h] = (h < HS && !g.const_att) ? S[n * S2 + NH + h0 + h] : 0.f;
+    dnl[h] = 0.f;
+  }
+  float4 acc[CPL];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) acc[c] = make_float4(0.f, 0.f, 0.f, 0.f);
 
-  for (int64_t n = blockIdx.x * 4ll + wave; n < N; n += gridDim.x * 4ll) {
-    const int beg = rowptr[n], end = rowptr[n + 1];
-    float sd[CPL], dn[CPL];
-    float4 acc[CPL];
+  const int beg = uni(g.rowptr[n]), end = uni(g.rowptr[n + 1]);
+  for (int base = beg; base < end; base += 64) {
+    const int cnt = min(64, end - base);
+    // batch phase: lane j <-> edge base + j (lanes past the segment reuse its last edge, w = 0)
+    const bool valid = lane < cnt;
+    const int e = base + min(lane, cnt - 1);
+    const int my_src = col[e];
+    float my_w0 = 0.f;
+    {
+      float ssv[kMaxHS];
+#pragma unroll
+      for (int h = 0; h < kMaxHS; ++h)
+        ssv[h] = (h < HS && !g.const_att) ? S[(int64_t)my_src * S2 + h0 + h] : 0.f;
+      const int64_t ep = drop ? (int64_t)g.perm[e] : 0;
+#pragma unroll
+      for (int h = 0; h < kMaxHS; ++h) {
+        if (h < HS) {
+          float ex = g.const_att ? 1.f : att_exp(ssv[h] + sdst[h], M);
+          if (g.dbg & 2) ex = 1.f;
+          ex = valid ? ex : 0.f;
+          dnl[h] += ex;
+          float w = ex;
+          if (drop) w = dropout_keep(g.seed, ep * NH + h0 + h, g.p_drop) ? ex * drop_scale : 0.f;
+          if (h == 0) my_w0 = w;
+          if (!SCALAR_W) w_lds[h * 64 + lane] = w;
+        }
+      }
+    }
+    if (EPW > 1) src_lds[lane] = my_src;
+    if (EPW > 1 || !SCALAR_W) wave_lds_sync();
+    if constexpr (EPW == 1) {
+      for (int j0 = 0; j0 < cnt; j0 += U) {
+        const float4* rp[U];
+        float wsc[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int j = min(j0 + u, cnt - 1);
+          rp[u] = rows4 + (int64_t)__builtin_amdgcn_readlane(my_src, j) * g.row_stride4;
+          wsc[u] = (j0 + u < cnt) ? lane_f(my_w0, j) : 0.f;
+        }
+        float4 v[U][CPL];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int c = 0; c < CPL; ++c)
+            v[u][c] = rp[u][off4[c]];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int j = min(j0 + u, cnt - 1);
+          const bool live = j0 + u < cnt;
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) {
+            const float w = SCALAR_W ? wsc[u] : (live ? w_lds[hl[c] * 64 + j] : 0.f);
+            acc[c] = fma4(w, v[u][c], acc[c]);
+          }
+        }
+      }
+    } else {
+      for (int j0 = grp; j0 < cnt; j0 += EPW * U) {
+        int sv[U];
+        bool live[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int j = j0 + u * EPW;
+          live[u] = j < cnt;
+          sv[u] = src_lds[live[u] ? j : cnt - 1];
+        }
+        float4 v[U][CPL];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int c = 0; c < CPL; ++c)
+            v[u][c] = rows4[(int64_t)sv[u] * g.row_stride4 + off4[c]];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int j = j0 + u * EPW;
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) {
+            const float w = live[u] ? w_lds[hl[c] * 64 + j] : 0.f;
+            acc[c] = fma4(w, v[u][c], acc[c]);
+          }
+        }
+      }
+    }
+    if (EPW > 1 || !SCALAR_W) wave_lds_sync();
+  }
+  // softmax denominators: per-lane partials -> wave sums (fixed butterfly order)
+#pragma unroll
+  for (int h = 0; h < kMaxHS; ++h) {
+    if (h < HS) {
+      float t = dnl[h];
+      for (int off = 1; off < 64; off <<= 1) t += __shfl_xor(t, off);
+      dnl[h] = t;
+    }
+  }
+  if (lane < HS) {
+    float d = 0.f;
+#pragma unroll
+    for (int h = 0; h < kMaxHS; ++h)
+      if (h == lane) d = dnl[h];
+    den_lds[lane] = d;
+    g.den[n * NH + h0 + lane] = d;
+  }
+  // combine the EPW edge groups (butterfly: every group ends with the totals)
+#pragma unroll
+  for (int off = LPE; off < 64; off <<= 1) {
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) acc[c] = add4(acc[c], shfl_xor4(acc[c], off));
+  }
+  wave_lds_sync();
+  if (grp == 0) {
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
-      sd[c] = const_att ? 0.f : S[n * S2 + NH + hc[c]];
-      dn[c] = 0.f;
-      acc[c] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    for (int e = beg + grp; e < end; e += EPW) {
-      const int64_t s = col[e];
-      const int64_t ep = drop ? (int64_t)perm[e] : 0;
-#pragma unroll
-      for (int c = 0; c < CPL; ++c) {
-        if (!vq[c]) continue;
-        const float4 v = Wh4[s * D4 + q[c]];
-        const float ex = const_att ? 1.f : att_exp(S[s * S2 + hc[c]] + sd[c], M);
-        dn[c] += ex;
-        float w = ex;
-        if (drop) w = dropout_keep(seed, ep * NH + hc[c], p_drop) ? ex * drop_scale : 0.f;
-        acc[c] = fma4(w, v, acc[c]);
-      }
-    }
-    // combine the EPW edge groups (butterfly: every group ends with the totals)
-#pragma unroll
-    for (int off = LPE; off < 64; off <<= 1) {
-#pragma unroll
-      for (int c = 0; c < CPL; ++c) {
-        acc[c] = add4(acc[c], shfl_xor4(acc[c], off));
-        dn[c] += __shfl_xor(dn[c], off);
-      }
-    }
-    if (grp == 0) {
-#pragma unroll
-      for (int c = 0; c < CPL; ++c) {
-        if (!vq[c]) continue;
-        const float inv = 1.f / (dn[c] + kSoftmaxEps);
-        const float4 o = acc[c] * inv;
-        const int h = hc[c], f0 = q[c] * 4 - h * Fp;
-        if (f0 == 0) {
-          den_lds[h] = dn[c];
-          den_out[n * NH + h] = dn[c];
-        }
-        if (concat) {
-          float* orow = out + n * (int64_t)(NH * F) + h * F;
-          if ((F & 3) == 0) {
-            float4 b = bias ? *(const float4*)(bias + h * F + f0) : make_float4(0.f, 0.f, 0.f, 0.f);
-            *(float4*)(orow + f0) = add4(o, b);
-          } else {
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (f0 + j < F) orow[f0 + j] = get4(o, j) + (bias ? bias[h * F + f0 + j] : 0.f);
-          }
+      if (!vq[c]) continue;
+      const float inv = 1.f / (den_lds[hl[c]] + kSoftmaxEps);
+      const float4 o = acc[c] * inv;
+      const int h = h0 + hl[c], f0 = q[c] * 4 - hl[c] * Fp;
+      if (g.concat) {
+        float* orow = g.out + n * g.out_ld;
+        const int64_t cb = (int64_t)h * F + f0;
+        if ((F & 3) == 0 && !g.resid && !g.elu) {
+          const float4 b = g.bias ? *(const float4*)(g.bias + cb) : make_float4(0.f, 0.f, 0.f, 0.f);
+          *(float4*)(orow + cb) = add4(o, b);
         } else {
-          *(float4*)(row_lds + q[c] * 4) = o;
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (f0 + j < F)
+              orow[cb + j] = epilogue(get4(o, j) + (g.bias ? g.bias[cb + j] : 0.f), g, n, cb + j);
         }
-      }
-    }
-    wave_lds_sync();
-    if (!concat) {
-      const float inv_nh = 1.f / (float)NH;
-      for (int f = lane; f < F; f += 64) {
-        float sum = 0.f;
-        for (int h = 0; h < NH; ++h) sum += row_lds[h * Fp + f];
-        out[n * F + f] = sum * inv_nh + (bias ? bias[f] : 0.f);
-      }
-    }
-    // alpha in edge_index' order (pre-dropout, as the reference returns/stores it, :109-110)
-    const int pairs = (end - beg) * NH;
-    for (int idx = lane; idx < pairs; idx += 64) {
-      const int eo = idx / NH, h = idx - eo * NH;
-      const int e = beg + eo;
-      float a;
-      if (const_att) {
-        a = 1.f / (den_lds[h] + kSoftmaxEps);
       } else {
-        const float raw = S[(int64_t)col[e] * S2 + h] + S[n * S2 + NH + h];
-        a = att_exp(raw, M) / (den_lds[h] + kSoftmaxEps);
-        if (raw == M) {
-          unsigned long long k = atomicAdd((unsigned long long*)argmax, 1ull);
-          if (k < GATX_ARGMAX_CAP) argmax[1 + k] = (long long)e * NH + h;
-        }
+        *(float4*)(row_lds + q[c] * 4) = o;
       }
-      alpha[(int64_t)perm[e] * NH + h] = a;
     }
-    wave_lds_sync();
+  }
+  wave_lds_sync();
+  if (!g.concat) {   // head mean (HS == NH)
+    const float inv_nh = 1.f / (float)NH;
+    for (int f = lane; f < F; f += 64) {
+      float sum = 0.f;
+      for (int h = 0; h < NH; ++h) sum += row_lds[h * Fp + f];
+      g.out[n * g.out_ld + f] = epilogue(sum * inv_nh + (g.bias ? g.bias[f] : 0.f), g, n, f);
+    }
   }
 }
 
@@ -228,21 +378,149 @@ __global__ void __launch_bounds__(256) waug_assemble_kernel(const float* __restr
   }
 }
 
+__global__ void __launch_bounds__(256) pad_rows_kernel(const float* __restrict__ src,
+                                                       int64_t rows, int64_t cols, int64_t lds,
+                                                       float* __restrict__ dst, int64_t ldd) {
+  const int64_t total = rows * ldd;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = t / ldd, c = t - r * ldd;
+    dst[t] = c < cols ? src[r * lds + c] : 0.f;
+  }
+}
+
+// S[n] = (Wh[n] . A_src^T | Wh[n] . A_dst^T): the per-node logit factors, in the reference's
+// own association (raw = cat(Wh[src], Wh[dst]) . a^T, gat_layer.py:76-82, split per half).
+// One wave per node; A2 = [A_src; A_dst] (2NH x Dp, head-padded) staged in LDS once per block.
+__global__ void __launch_bounds__(256) node_scores_kernel(const float* __restrict__ Wh,
+                                                          int64_t N, int NH, int F, int Fp,
+                                                          const float* __restrict__ a,
+                                                          float* __restrict__ S) {
+  extern __shared__ __attribute__((aligned(16))) float a2[];   // [2NH][Dp]
+  const int Dp = NH * Fp, D = NH * F, H2 = 2 * NH;
+  for (int t = threadIdx.x; t < H2 * Dp; t += blockDim.x) {
+    const int h2 = t / Dp, c = t - h2 * Dp, k = c / Fp, f = c - k * Fp;
+    const int hh = h2 < NH ? h2 : h2 - NH;
+    a2[t] = f < F ? a[(int64_t)hh * 2 * D + k * 2 * F + (h2 < NH ? 0 : F) + f] : 0.f;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int D4 = Dp / 4;
+  for (int64_t n = blockIdx.x * 4ll + wave; n < N; n += gridDim.x * 4ll) {
+    const float4* row = (const float4*)(Wh + n * Dp);
+    float acc[32];
+#pragma unroll
+    for (int h = 0; h < 32; ++h) acc[h] = 0.f;
+    for (int q = lane; q < D4; q += 64) {
+      const float4 v = row[q];
+#pragma unroll
+      for (int h = 0; h < 32; ++h) {
+        if (h >= H2) break;
+        const float4 w = *(const float4*)(a2 + h * Dp + 4 * q);
+        acc[h] += v.x * w.x + v.y * w.y + v.z * w.z + v.w * w.w;
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 32; ++h) {
+      if (h >= H2) break;
+      float t = acc[h];
+      for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+      if (lane == 0) S[n * H2 + h] = t;
+    }
+  }
+}
+
+// alpha in edge_index' order (pre-dropout, as the reference returns and stores it,
+// models/gat_layer.py:109-110): alpha[e', h] = ex / (den[dst] + 1e-8), one thread per CSR slot,
+// all heads of an edge written together (one random 4*NH-byte store per edge instead of NH
+// scattered dwords). Also records the argmax (edge, head) entries for max()'s gradient.
+template <int NHC>
+__global__ void __launch_bounds__(256) attention_alpha_kernel(
+    const int32_t* __restrict__ col, const int32_t* __restrict__ rowidx,
+    const int32_t* __restrict__ perm, int64_t E2, const float* __restrict__ S,
+    const uint32_t* __restrict__ M_ord, const float* __restrict__ den, int NH_rt, int const_att,
+    float* __restrict__ alpha, long long* __restrict__ argmax) {
+  constexpr int VEC = (NHC % 4 == 0) ? 4 : ((NHC % 2 == 0) ? 2 : 1);
+  const int NH = NHC > 0 ? NHC : NH_rt, S2 = 2 * NH;
+  const float M = const_att ? 0.f : ord_to_float(*M_ord);
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E2;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = col[e], d = rowidx[e];
+    float* out = alpha + (int64_t)perm[e] * NH;
+    if constexpr (NHC > 0) {
+      float ss[NHC], sd[NHC], dn[NHC], a[NHC];
+#pragma unroll
+      for (int h = 0; h < NHC; h += VEC) {
+        if constexpr (VEC == 4) {
+          const float4 x = *(const float4*)(S + s * S2 + h);
+          const float4 y = *(const float4*)(S + d * S2 + NHC + h);
+          const float4 z = *(const float4*)(den + d * NHC + h);
+          ss[h] = x.x; ss[h + 1] = x.y; ss[h + 2] = x.z; ss[h + 3] = x.w;
+          sd[h] = y.x; sd[h + 1] = y.y; sd[h + 2] = y.z; sd[h + 3] = y.w;
+          dn[h] = z.x; dn[h + 1] = z.y; dn[h + 2] = z.z; dn[h + 3] = z.w;
+        } else if constexpr (VEC == 2) {
+          const float2 x = *(const float2*)(S + s * S2 + h);
+          const float2 y = *(const float2*)(S + d * S2 + NHC + h);
+          const float2 z = *(const float2*)(den + d * NHC + h);
+          ss[h] = x.x; ss[h + 1] = x.y; sd[h] = y.x; sd[h + 1] = y.y; dn[h] = z.x; dn[h + 1] = z.y;
+        } else {
+          ss[h] = S[s * S2 + h]; sd[h] = S[d * S2 + NHC + h]; dn[h] = den[d * NHC + h];
+        }
+      }
+      bool hit = false;
+#pragma unroll
+      for (int h = 0; h < NHC; ++h) {
+        const float raw = ss[h] + sd[h];
+        hit |= (!const_att && raw == M);
+        a[h] = (const_att ? 1.f : att_exp(raw, M)) / (dn[h] + kSoftmaxEps);
+      }
+#pragma unroll
+      for (int h = 0; h < NHC; h += VEC) {
+        if constexpr (VEC == 4) *(float4*)(out + h) = make_float4(a[h], a[h + 1], a[h + 2], a[h + 3]);
+        else if constexpr (VEC == 2) *(float2*)(out + h) = make_float2(a[h], a[h + 1]);
+        else out[h] = a[h];
+      }
+      if (hit) {   // rare: record every tied argmax (edge, head) for max()'s gradient
+#pragma unroll
+        for (int h = 0; h < NHC; ++h)
+          if (ss[h] + sd[h] == M) {
+            unsigned long long k = atomicAdd((unsigned long long*)argmax, 1ull);
+            if (k < GATX_ARGMAX_CAP) argmax[1 + k] = (long long)e * NHC + h;
+          }
+      }
+    } else {
+      for (int h = 0; h < NH; ++h) {
+        float a;
+        if (const_att) {
+          a = 1.f / (den[d * NH + h] + kSoftmaxEps);
+        } else {
+          const float raw = S[s * S2 + h] + S[d * S2 + NH + h];
+          a = att_exp(raw, M) / (den[d * NH + h] + kSoftmaxEps);
+          if (raw == M) {
+            unsigned long long k = atomicAdd((unsigned long long*)argmax, 1ull);
+            if (k < GATX_ARGMAX_CAP) argmax[1 + k] = (long long)e * NH + h;
+          }
+        }
+        out[h] = a;
+      }
+    }
+  }
+}
+
 inline unsigned grid_for(int64_t n, int block = 256, int64_t cap = 16384) {
   int64_t g = ceil_div(n > 0 ? n : 1, block);
   return (unsigned)(g < cap ? g : cap);
 }
 
 template <int LPE, int CPL>
-int launch_edge_forward(unsigned grid, size_t lds, hipStream_t st, const float* Wh,
-                        const float* S, const uint32_t* M_ord, const int32_t* rowptr,
-                        const int32_t* col, const int32_t* perm, int64_t N, int NH, int F, int Fp,
-                        int concat, int const_att, const float* bias, float p, uint64_t seed,
-                        float* out, float* alpha, float* den, int64_t* argmax, int lds_row) {
-  edge_forward_kernel<LPE, CPL><<<grid, 256, lds, st>>>(Wh, S, M_ord, rowptr, col, perm, N, NH,
-                                                        F, Fp, concat, const_att, bias, p, seed,
-                                                        out, alpha, den, (long long*)argmax,
-                                                        lds_row);
+int launch_edge_forward(unsigned grid, size_t lds, hipStream_t st, const EdgeFwdArgs& g) {
+  constexpr int U = CPL <= 1 ? 8 : (CPL <= 2 ? 4 : (CPL <= 4 ? 2 : 1));
+  // one head per item with whole 64-lane chunks: every chunk's weight is wave-uniform
+  const bool scalar_w = (LPE == 64) && g.HS == 1 && ((g.Fp / 4) % 64 == 0);
+  if (scalar_w)
+    edge_forward_kernel<LPE, CPL, U, true><<<grid, 256, lds, st>>>(g);
+  else
+    edge_forward_kernel<LPE, CPL, U, false><<<grid, 256, lds, st>>>(g);
   GATX_LAUNCH_CHECK("edge_forward");
   return 0;
 }
@@ -281,50 +559,132 @@ extern "C" int64_t gatx_prepare_weights_floats(int NH, int F, int64_t F_in, int 
   return (NH * Fp + H2 + ceil_div((int64_t)NH * F, 128) * H2) * F_in;
 }
 
-extern "C" int gatx_attention_max(const int32_t* col, const int32_t* rowidx, int64_t E2,
-                                  const float* S, int NH, uint32_t* M_ord, gatx_stream_t s) {
-  hipStream_t st = (hipStream_t)s;
-  hipError_t r = hipMemsetAsync(M_ord, 0, sizeof(uint32_t), st);
-  if (r != hipSuccess) { set_error("memset: %s", hipGetErrorString(r)); return (int)r; }
-  if (E2 == 0) return 0;
-  attention_max_kernel<<<grid_for(E2, 256, 4096), 256, 0, st>>>(col, rowidx, E2, S, NH, M_ord);
-  GATX_LAUNCH_CHECK("attention_max");
+extern "C" void gatx_set_debug(int flags) { g_debug = flags; }
+
+extern "C" int gatx_node_scores(const float* Wh, int64_t N, int NH, int F, const float* a,
+                                float* S, gatx_stream_t s) {
+  const int Fp = (int)round_up(F, 4);
+  GATX_REQUIRE(2 * NH <= kMaxH2, "node_scores: num_heads > %d unsupported", kMaxH2 / 2);
+  const size_t lds = (size_t)2 * NH * NH * Fp * sizeof(float);
+  GATX_REQUIRE(lds <= 64 * 1024, "node_scores: attention vector too large for LDS");
+  if (N == 0) return 0;
+  node_scores_kernel<<<(unsigned)std::min<int64_t>(ceil_div(N, 4), 1024), 256, lds,
+                       (hipStream_t)s>>>(Wh, N, NH, F, Fp, a, S);
+  GATX_LAUNCH_CHECK("node_scores");
   return 0;
 }
 
-extern "C" int gatx_edge_forward(const float* Wh, const float* S, const uint32_t* M_ord,
-                                 const int32_t* rowptr, const int32_t* col, const int32_t* perm,
-                                 int64_t N, int NH, int F, int concat, int const_att,
-                                 const float* bias, float p, uint64_t seed, float* out,
-                                 float* alpha, float* den, int64_t* argmax, gatx_stream_t s) {
+extern "C" int gatx_attention_alpha(const int32_t* col, const int32_t* rowidx,
+                                    const int32_t* perm, int64_t E2, const float* S,
+                                    const uint32_t* M_ord, const float* den, int NH,
+                                    int const_att, float* alpha, int64_t* argmax,
+                                    gatx_stream_t s) {
+  if (E2 == 0) return 0;
+  hipStream_t st = (hipStream_t)s;
+  const unsigned grid = grid_for(E2, 256, 8192);
+#define GATX_AL(C)                                                                             \
+  attention_alpha_kernel<C><<<grid, 256, 0, st>>>(col, rowidx, perm, E2, S, M_ord, den, NH,   \
+                                                  const_att, alpha, (long long*)argmax)
+  switch (NH) {
+    case 1: GATX_AL(1); break; case 2: GATX_AL(2); break; case 4: GATX_AL(4); break;
+    case 6: GATX_AL(6); break; case 8: GATX_AL(8); break; default: GATX_AL(0); break;
+  }
+#undef GATX_AL
+  GATX_LAUNCH_CHECK("attention_alpha");
+  return 0;
+}
+
+extern "C" int gatx_pad_rows(const float* src, int64_t rows, int64_t cols, int64_t ld_src,
+                             float* dst, int64_t ld_dst, gatx_stream_t s) {
+  GATX_REQUIRE(ld_dst >= cols, "pad_rows: destination narrower than source");
+  if (rows == 0) return 0;
+  pad_rows_kernel<<<grid_for(rows * ld_dst), 256, 0, (hipStream_t)s>>>(src, rows, cols, ld_src,
+                                                                       dst, ld_dst);
+  GATX_LAUNCH_CHECK("pad_rows");
+  return 0;
+}
+
+extern "C" int gatx_attention_max(const int32_t* col, const int32_t* rowidx, int64_t E2,
+                                  const float* S, int NH, uint32_t* M_ord, void* workspace,
+                                  gatx_stream_t s) {
+  hipStream_t st = (hipStream_t)s;
+  const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(E2, 256), kMaxBlocks));
+  float* part = (float*)workspace;
+  attention_max_kernel<<<nb, 256, 0, st>>>(col, rowidx, E2, S, NH, part);
+  GATX_LAUNCH_CHECK("attention_max");
+  max_final_kernel<<<1, 256, 0, st>>>(part, nb, M_ord);
+  GATX_LAUNCH_CHECK("attention_max_final");
+  return 0;
+}
+
+extern "C" size_t gatx_attention_max_workspace_bytes(void) { return sizeof(float) * kMaxBlocks; }
+
+extern "C" int gatx_edge_forward_ex(
+    const float* rows, int64_t row_stride, int64_t head_stride, const float* S,
+    const uint32_t* M_ord, const int32_t* rowptr, const int32_t* col, const int32_t* perm,
+    int64_t N, int NH, int F, int heads_per_item, int concat, int const_att, const float* bias,
+    float p, uint64_t seed, float* out, int64_t out_ld, const float* resid, int64_t resid_ld,
+    int elu, float* den, int64_t chunk, gatx_stream_t s) {
   hipStream_t st = (hipStream_t)s;
   GATX_REQUIRE(NH >= 1 && F >= 1, "edge_forward: bad sizes");
   GATX_REQUIRE(concat || bias == nullptr || NH == 1,
                "edge_forward: bias with head-mean needs num_heads == 1");
+  const int HS = heads_per_item <= 0 ? NH : heads_per_item;
+  GATX_REQUIRE(NH % HS == 0, "edge_forward: heads_per_item must divide num_heads");
+  GATX_REQUIRE(concat || HS == NH, "edge_forward: head-mean needs all heads in one item");
+  GATX_REQUIRE(row_stride % 4 == 0 && head_stride % 4 == 0 && ((uintptr_t)rows % 16) == 0,
+               "edge_forward: source rows must be float4-aligned");
+  GATX_REQUIRE(p >= 0.f && p < 1.f, "edge_forward: dropout must be in [0, 1)");
   if (N == 0) return 0;
   const int Fp = (int)round_up(F, 4);
-  const int64_t D4 = (int64_t)NH * Fp / 4;
-  const RowGeom g = row_geom(D4);
-  GATX_REQUIRE(g.cpl <= 8, "edge_forward: num_heads*out_features > 2048 unsupported");
-  GATX_REQUIRE(p >= 0.f && p < 1.f, "edge_forward: dropout must be in [0, 1)");
-  const int lds_row = (int)round_up((int64_t)NH * Fp + NH, 4);
-  const size_t lds = (size_t)4 * lds_row * sizeof(float);
+  GATX_REQUIRE(!(concat && (F & 3) == 0 && !resid && !elu) || out_ld % 4 == 0,
+               "edge_forward: out row stride must be a multiple of 4");
+  const int64_t D4 = (int64_t)HS * Fp / 4;
+  const RowGeom rg = row_geom(D4);
+  GATX_REQUIRE(rg.cpl <= 8, "edge_forward: heads_per_item*out_features > 2048 unsupported");
+  EdgeFwdArgs g;
+  g.rows = rows; g.row_stride4 = row_stride / 4; g.head_stride4 = (int)(head_stride / 4);
+  g.S = S; g.M_ord = M_ord; g.rowptr = rowptr; g.col = col; g.perm = perm;
+  g.N = N; g.NH = NH; g.F = F; g.Fp = Fp; g.HS = HS; g.concat = concat; g.const_att = const_att;
+  g.bias = bias; g.p_drop = p; g.seed = seed; g.out = out; g.out_ld = out_ld;
+  g.resid = resid; g.resid_ld = resid_ld; g.elu = elu;
+  g.den = den;
+  GATX_REQUIRE(HS <= kMaxHS, "edge_forward: more than %d heads per work item", kMaxHS);
+  g.lds_row = (int)round_up((int64_t)HS * Fp + HS + 64 + (int64_t)HS * 64, 4);
+  g.chunk = chunk > 0 ? chunk : 2048;
+  g.dbg = g_debug;
+  g.n_items = ceil_div(N, g.chunk) * g.chunk * (NH / HS);
+  const size_t lds = (size_t)4 * g.lds_row * sizeof(float);
   GATX_REQUIRE(lds <= 160 * 1024, "edge_forward: row too wide for LDS staging");
-  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(N, 4), 65536);
-#define GATX_EF(L, C)                                                                          \
-  return launch_edge_forward<L, C>(grid, lds, st, Wh, S, M_ord, rowptr, col, perm, N, NH, F,   \
-                                   Fp, concat, const_att, bias, p, seed, out, alpha, den,      \
-                                   argmax, lds_row)
-  if (g.lpe == 64) {
-    switch (g.cpl) {
+  const int64_t blocks = ceil_div(g.n_items, 4);
+  GATX_REQUIRE(blocks < (1ll << 31), "edge_forward: too many work items");
+  const unsigned grid = (unsigned)blocks;
+#define GATX_EF(L, C) return launch_edge_forward<L, C>(grid, lds, st, g)
+  if (rg.lpe == 64) {
+    switch (rg.cpl) {
       case 1: GATX_EF(64, 1); case 2: GATX_EF(64, 2); case 3: GATX_EF(64, 3);
       case 4: GATX_EF(64, 4); case 5: GATX_EF(64, 5); case 6: GATX_EF(64, 6);
       case 7: GATX_EF(64, 7); default: GATX_EF(64, 8);
     }
   }
-  switch (g.lpe) {
+  switch (rg.lpe) {
     case 1: GATX_EF(1, 1); case 2: GATX_EF(2, 1); case 4: GATX_EF(4, 1);
     case 8: GATX_EF(8, 1); case 16: GATX_EF(16, 1); default: GATX_EF(32, 1);
   }
 #undef GATX_EF
+}
+
+extern "C" int gatx_edge_forward(const float* Wh, const float* S, const uint32_t* M_ord,
+                                 const int32_t* rowptr, const int32_t* col,
+                                 const int32_t* rowidx, const int32_t* perm, int64_t N,
+                                 int64_t E2, int NH, int F, int concat, int const_att,
+                                 const float* bias, float p,
+                                 uint64_t seed, float* out, float* alpha, float* den,
+                                 int64_t* argmax, gatx_stream_t s) {
+  const int64_t Fp = round_up(F, 4);
+  GATX_CALL(gatx_edge_forward_ex(Wh, NH * Fp, Fp, S, M_ord, rowptr, col, perm, N, NH, F,
+                                 concat ? 0 : NH, concat, const_att, bias, p, seed, out,
+                                 concat ? (int64_t)NH * F : F, nullptr, 0, 0, den, 0, s));
+  return gatx_attention_alpha(col, rowidx, perm, E2, S, M_ord, den, NH, const_att,
+                              alpha, argmax, s);
 }

@@ -19,9 +19,12 @@ __device__ inline int64_t ld_idx(const void* p, int64_t i) {
   return (int64_t)((const I*)p)[i];
 }
 
+constexpr int kStatsBlocks = 1024;
+
+// Per-block {min, max, self-loops} partials (no 64-bit atomics), reduced by stats_final_kernel.
 template <typename I>
 __global__ void __launch_bounds__(256) edge_stats_kernel(const void* ei, int64_t E, int64_t ld,
-                                                         long long* stats) {
+                                                         long long* part) {
   long long mn = LLONG_MAX, mx = LLONG_MIN, loops = 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < E;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -43,16 +46,33 @@ __global__ void __launch_bounds__(256) edge_stats_kernel(const void* ei, int64_t
     for (int k = 1; k < (int)(blockDim.x >> 6); ++k) {
       mn = min(mn, red[0][k]); mx = max(mx, red[1][k]); loops += red[2][k];
     }
-    atomicMin(&stats[0], mn);
-    atomicMax(&stats[1], mx);
-    atomicAdd((unsigned long long*)&stats[2], (unsigned long long)loops);
+    part[3 * blockIdx.x + 0] = mn;
+    part[3 * blockIdx.x + 1] = mx;
+    part[3 * blockIdx.x + 2] = loops;
   }
 }
 
-__global__ void init_stats_kernel(long long* stats) {
-  stats[0] = LLONG_MAX;
-  stats[1] = LLONG_MIN;
-  stats[2] = 0;
+__global__ void __launch_bounds__(256) stats_final_kernel(const long long* part, int nb,
+                                                          long long* stats) {
+  long long mn = LLONG_MAX, mx = LLONG_MIN, loops = 0;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+    mn = min(mn, part[3 * b]); mx = max(mx, part[3 * b + 1]); loops += part[3 * b + 2];
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    mn = min(mn, (long long)__shfl_xor(mn, o));
+    mx = max(mx, (long long)__shfl_xor(mx, o));
+    loops += __shfl_xor(loops, o);
+  }
+  __shared__ long long red[3][4];
+  int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (l == 0) { red[0][w] = mn; red[1][w] = mx; red[2][w] = loops; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < (int)(blockDim.x >> 6); ++k) {
+      mn = min(mn, red[0][k]); mx = max(mx, red[1][k]); loops += red[2][k];
+    }
+    stats[0] = mn; stats[1] = mx; stats[2] = loops;
+  }
 }
 
 // keep flag of input edge i (1 = survives the self-loop rewrite)
@@ -198,18 +218,22 @@ int graph_build_impl(const void* ei, int64_t E, int64_t ld, int add_loops, int64
 using namespace gatx;
 
 extern "C" int gatx_edge_stats(const void* edge_index, int is64, int64_t E, int64_t ld,
-                               int64_t* stats, gatx_stream_t s) {
+                               int64_t* stats, void* workspace, gatx_stream_t s) {
   hipStream_t stream = (hipStream_t)s;
-  init_stats_kernel<<<1, 1, 0, stream>>>((long long*)stats);
-  GATX_LAUNCH_CHECK("init_stats");
-  if (E == 0) return 0;
-  unsigned g = grid_for(E, 256, 2048);
+  const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(E, 256), kStatsBlocks));
+  long long* part = (long long*)workspace;
   if (is64)
-    edge_stats_kernel<int64_t><<<g, 256, 0, stream>>>(edge_index, E, ld, (long long*)stats);
+    edge_stats_kernel<int64_t><<<nb, 256, 0, stream>>>(edge_index, E, ld, part);
   else
-    edge_stats_kernel<int32_t><<<g, 256, 0, stream>>>(edge_index, E, ld, (long long*)stats);
+    edge_stats_kernel<int32_t><<<nb, 256, 0, stream>>>(edge_index, E, ld, part);
   GATX_LAUNCH_CHECK("edge_stats");
+  stats_final_kernel<<<1, 256, 0, stream>>>(part, nb, (long long*)stats);
+  GATX_LAUNCH_CHECK("edge_stats_final");
   return 0;
+}
+
+extern "C" size_t gatx_edge_stats_workspace_bytes(void) {
+  return (size_t)3 * sizeof(long long) * kStatsBlocks;
 }
 
 extern "C" size_t gatx_graph_build_workspace_bytes(int64_t E, int64_t E2, int64_t N) {

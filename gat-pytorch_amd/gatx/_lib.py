@@ -28,7 +28,8 @@ P = ctypes.c_void_p
 SIGNATURES = {
     "gatx_last_error": (ctypes.c_char_p, []),
     "gatx_version": (c_i, []),
-    "gatx_edge_stats": (c_i, [P, c_i, c_i64, c_i64, P, P]),
+    "gatx_edge_stats_workspace_bytes": (c_sz, []),
+    "gatx_edge_stats": (c_i, [P, c_i, c_i64, c_i64, P, P, P]),
     "gatx_graph_build_workspace_bytes": (c_sz, [c_i64, c_i64, c_i64]),
     "gatx_graph_build": (c_i, [P, c_i, c_i64, c_i64, c_i, c_i64, c_i64, c_i64, P, P, P, P, P, P,
                                c_sz, P]),
@@ -38,9 +39,23 @@ SIGNATURES = {
     "gatx_prepare_weights_floats": (c_i64, [c_i, c_i, c_i64, c_i]),
     "gatx_gemm_f32": (c_i, [c_i64, c_i64, c_i64, P, c_i64, c_i64, P, c_i64, c_i64, P, c_i64,
                             c_i64, P, c_i64, c_i, P]),
-    "gatx_attention_max": (c_i, [P, P, c_i64, P, c_i, P, P]),
-    "gatx_edge_forward": (c_i, [P, P, P, P, P, P, c_i64, c_i, c_i, c_i, c_i, P, c_f, c_u64, P, P,
-                                P, P, P]),
+    "gatx_gemm_f32_batched": (c_i, [c_i64, c_i64, c_i64, c_i64, P, c_i64, c_i64, c_i64, P,
+                                    c_i64, c_i64, c_i64, P, c_i64, c_i64, c_i, P, c_i64, P, c_i64,
+                                    c_i64, c_i, P]),
+    "gatx_edge_forward_ex": (c_i, [P, c_i64, c_i64, P, P, P, P, P, c_i64, c_i, c_i, c_i, c_i, c_i,
+                                   P, c_f, c_u64, P, c_i64, P, c_i64, c_i, P, c_i64, P]),
+    "gatx_pad_rows": (c_i, [P, c_i64, c_i64, c_i64, P, c_i64, P]),
+    "gatx_set_gemm_rows": (None, [c_i]),
+    "gatx_set_debug": (None, [c_i]),
+    "gatx_gemm_splitk_workspace_bytes": (c_sz, [c_i64, c_i64, c_i64]),
+    "gatx_gemm_f32_splitk": (c_i, [c_i64, c_i64, c_i64, P, c_i64, c_i64, P, c_i64, c_i64, P, c_i64,
+                                   c_i, P, c_sz, P]),
+    "gatx_node_scores": (c_i, [P, c_i64, c_i, c_i, P, P, P]),
+    "gatx_attention_max_workspace_bytes": (c_sz, []),
+    "gatx_attention_max": (c_i, [P, P, c_i64, P, c_i, P, P, P]),
+    "gatx_edge_forward": (c_i, [P, P, P, P, P, P, P, c_i64, c_i64, c_i, c_i, c_i, c_i, P, c_f,
+                                c_u64, P, P, P, P, P]),
+    "gatx_attention_alpha": (c_i, [P, P, P, c_i64, P, P, P, c_i, c_i, P, P, P]),
     "gatx_edge_backward_dst_partials": (c_i64, [c_i64]),
     "gatx_edge_backward_dst": (c_i, [P, P, P, P, P, P, P, c_i64, c_i, c_i, c_i, c_f, c_u64, P, P,
                                      P, P, c_i64, P, P]),

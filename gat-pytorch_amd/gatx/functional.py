@@ -89,43 +89,163 @@ class LayerShape:
         self.out_cols = self.NH * self.F if self.concat else self.F
 
 
-def project(x: torch.Tensor, W: torch.Tensor, a, sh: LayerShape):
-    """Wh [N][Dp] and S [N][2NH] = x . W_aug^T in one MFMA GEMM (gat_layer.py:64 + :76-82)."""
-    N = x.size(0)
-    s = stream()
+_MAX_WS = {}
+
+
+def _max_ws(dev):
+    """Per-device scratch for the max pre-pass partials (reused: stream-ordered)."""
+    t = _MAX_WS.get(dev)
+    if t is None:
+        t = torch.empty(lib.gatx_attention_max_workspace_bytes(), dtype=torch.uint8, device=dev)
+        _MAX_WS[dev] = t
+    return t
+
+
+_WAUG_CACHE: "OrderedDict" = None
+
+
+def augmented_weight(W, a, sh: "LayerShape"):
+    """W_aug = [W padded per head; A_src W; A_dst W] (gatx_prepare_weights). Cached on the
+    parameters' identity and version counters, so inference reuses it across steps while any
+    in-place update (optimizer step, load_state_dict) rebuilds it."""
+    global _WAUG_CACHE
+    from collections import OrderedDict
+    if _WAUG_CACHE is None:
+        _WAUG_CACHE = OrderedDict()
+    key = (W.data_ptr(), W._version, tuple(W.shape), W.device,
+           a.data_ptr() if a is not None else 0, a._version if a is not None else -1,
+           sh.NH, sh.F)
+    hit = _WAUG_CACHE.get(key)
+    if hit is not None:
+        _WAUG_CACHE.move_to_end(key)
+        return hit[2]
     waug_floats = lib.gatx_prepare_weights_floats(sh.NH, sh.F, sh.F_in, int(a is not None))
-    W_aug = torch.empty(waug_floats, dtype=torch.float32, device=x.device)
+    W_aug = torch.empty(waug_floats, dtype=torch.float32, device=W.device)
     with _span("prepare_weights", (sh.NH, sh.F, sh.F_in)):
-        call("gatx_prepare_weights", ptr(W), ptr(a), sh.NH, sh.F, sh.F_in, ptr(W_aug), s)
-    Wh = torch.empty((N, sh.Dp), dtype=torch.float32, device=x.device)
-    S = torch.empty((N, max(sh.H2, 1)), dtype=torch.float32, device=x.device)
-    with _span("gemm", (N, sh.K_aug, sh.F_in, sh.NH, sh.F)):
-        call("gatx_gemm_f32", N, sh.K_aug, sh.F_in, ptr(x), sh.F_in, 1, ptr(W_aug), 1, sh.F_in,
-             ptr(Wh), sh.Dp, sh.Dp, ptr(S), max(sh.H2, 1), 0, s)
-    return W_aug, Wh, S
+        call("gatx_prepare_weights", ptr(W), ptr(a), sh.NH, sh.F, sh.F_in, ptr(W_aug), stream())
+    _WAUG_CACHE[key] = (W, a, W_aug)   # holding W / a pins their storage (no pointer reuse)
+    while len(_WAUG_CACHE) > 16:
+        _WAUG_CACHE.popitem(last=False)
+    return W_aug
 
 
-def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: int):
-    """Returns out, alpha (edge_index' order) and the saved state for the backward."""
+def _env_int(name: str, default: int) -> int:
+    import os
+    v = os.environ.get(name)
+    return int(v) if v not in (None, "") else default
+
+
+def edge_heads_per_item(sh: LayerShape) -> int:
+    """Heads per edge work item: one head per item when a head's row slice is >= 256 B (its
+    per-graph working set then fits one XCD's L2); otherwise the largest divisor of NH that is
+    <= 8 (the batch phase keeps the item's heads in registers). Head-mean layers need all heads
+    in one item (NH <= 8)."""
+    hs = _env_int("GATX_HEADS_PER_ITEM", 0)
+    if hs > 0 and sh.NH % hs == 0 and hs <= 8 and (sh.concat or hs == sh.NH):
+        return hs
+    if not sh.concat:
+        if sh.NH > 8:
+            raise RuntimeError("gatx: head-mean layers support at most 8 heads")
+        return sh.NH
+    # ~512 floats of row per item: one XCD's L2 still holds the sweep's slice while each edge
+    # step moves >= 1 KB per wave (measured on PPI layer 1: 2 heads of 256 beat 1 and 4)
+    return max(d for d in range(1, 9) if sh.NH % d == 0 and d * sh.Fp <= max(512, sh.Fp))
+
+
+def fold_scores_into_gemm(sh: LayerShape) -> bool:
+    """Compute S as 2NH extra GEMM columns only when they fit the last column tile for free;
+    otherwise (e.g. Dp = 1024: a whole extra 128-wide tile, +12% GEMM time) project Wh alone and
+    derive S from it with gatx_node_scores (one extra read of Wh)."""
+    if sh.H2 == 0:
+        return True
+    if 2 * sh.NH * sh.Dp * 4 > 64 * 1024:
+        return True
+    return -(-(sh.Dp + sh.H2) // 128) == -(-sh.Dp // 128)
+
+
+def use_reassociation(sh: LayerShape) -> bool:
+    """Aggregate x rows instead of Wh rows when x is much narrower (PPI layer 0: 50 vs 1024):
+    out_h = (sum alpha~ x[src]) W_h^T == sum alpha~ (x[src] W_h^T)."""
+    if _env_int("GATX_REASSOC", 1) == 0:
+        return False
+    return sh.concat and 2 * _round4(sh.F_in) <= sh.Dp
+
+
+def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: int,
+                  resid=None, elu=False):
+    """Returns out (= elu?(layer(x) + resid) when fused), alpha (edge_index' order) and the saved
+    state for the backward."""
     N = x.size(0)
     dev = x.device
     s = stream()
-    W_aug, Wh, S = project(x, W, a, sh)
-    M_ord = torch.zeros(1, dtype=torch.int32, device=dev)
     E2 = graph.num_edges
+    f32 = dict(dtype=torch.float32, device=dev)
+    chunk = _env_int("GATX_EDGE_CHUNK", 2048)
+    out = torch.empty((N, sh.out_cols), **f32)
+    alpha = torch.empty((E2, sh.NH), **f32)
+    den = torch.empty((N, sh.NH), **f32)
+    argmax = torch.zeros(ARGMAX_CAP + 2, dtype=torch.int64, device=dev)
+    M_ord = torch.zeros(1, dtype=torch.int32, device=dev)
+    resid_p = ptr(resid) if resid is not None else None
+    W_aug = augmented_weight(W, a, sh)
+    saved = dict(W_aug=W_aug, M_ord=M_ord, den=den, argmax=argmax, Wh=None)
+    if use_reassociation(sh):
+        Fin_p = _round4(sh.F_in)
+        if Fin_p != sh.F_in:
+            x_rows = torch.empty((N, Fin_p), **f32)
+            call("gatx_pad_rows", ptr(x), N, sh.F_in, sh.F_in, ptr(x_rows), Fin_p, s)
+        else:
+            x_rows = x
+        S = torch.empty((N, max(sh.H2, 1)), **f32)
+        if not sh.const:
+            with _span("gemm_scores", (N, sh.H2, sh.F_in)):
+                call("gatx_gemm_f32", N, sh.H2, sh.F_in, ptr(x), sh.F_in, 1,
+                     ptr(W_aug) + 4 * sh.Dp * sh.F_in, 1, sh.F_in, ptr(S), sh.H2, sh.H2, None,
+                     0, 0, s)
+            with _span("attention_max", (E2, sh.NH)):
+                call("gatx_attention_max", ptr(graph.col), ptr(graph.rowidx), E2, ptr(S),
+                     sh.NH, ptr(M_ord), ptr(_max_ws(dev)), s)
+        Z = torch.empty((N, sh.NH * Fin_p), **f32)
+        with _span("edge_forward", (N, E2, sh.NH, Fin_p, "x")):
+            hs_x = max(d for d in range(1, 9) if sh.NH % d == 0)   # heads sharing one x row
+            call("gatx_edge_forward_ex", ptr(x_rows), Fin_p, 0, ptr(S), ptr(M_ord),
+                 ptr(graph.rowptr), ptr(graph.col), ptr(graph.perm), N, sh.NH, Fin_p, hs_x, 1,
+                 int(sh.const), None, float(p), seed, ptr(Z), sh.NH * Fin_p, None, 0, 0,
+                 ptr(den), chunk, s)
+        with _span("attention_alpha", (E2, sh.NH)):
+            call("gatx_attention_alpha", ptr(graph.col), ptr(graph.rowidx), ptr(graph.perm), E2,
+                 ptr(S), ptr(M_ord), ptr(den), sh.NH, int(sh.const), ptr(alpha), ptr(argmax), s)
+        with _span("gemm_out", (N, sh.F, sh.F_in, sh.NH)):
+            call("gatx_gemm_f32_batched", sh.NH, N, sh.F, sh.F_in, ptr(Z), sh.NH * Fin_p, 1,
+                 Fin_p, ptr(W), 1, sh.F_in, sh.F * sh.F_in, ptr(out), sh.NH * sh.F, sh.F, 0,
+                 ptr(bias), sh.F, resid_p, sh.out_cols, sh.F, int(elu), s)
+        saved.update(S=S, reassoc=True)
+        return out, alpha, saved
+    Wh = torch.empty((N, sh.Dp), **f32)
+    S = torch.empty((N, max(sh.H2, 1)), **f32)
+    if fold_scores_into_gemm(sh):
+        with _span("gemm", (N, sh.K_aug, sh.F_in, sh.NH, sh.F)):
+            call("gatx_gemm_f32", N, sh.K_aug, sh.F_in, ptr(x), sh.F_in, 1, ptr(W_aug), 1,
+                 sh.F_in, ptr(Wh), sh.Dp, sh.Dp, ptr(S), max(sh.H2, 1), 0, s)
+    else:
+        with _span("gemm", (N, sh.Dp, sh.F_in, sh.NH, sh.F)):
+            call("gatx_gemm_f32", N, sh.Dp, sh.F_in, ptr(x), sh.F_in, 1, ptr(W_aug), 1,
+                 sh.F_in, ptr(Wh), sh.Dp, sh.Dp, None, 0, 0, s)
+        with _span("node_scores", (N, sh.NH, sh.F)):
+            call("gatx_node_scores", ptr(Wh), N, sh.NH, sh.F, ptr(a), ptr(S), s)
     if not sh.const:
         with _span("attention_max", (E2, sh.NH)):
             call("gatx_attention_max", ptr(graph.col), ptr(graph.rowidx), E2, ptr(S), sh.NH,
-                 ptr(M_ord), s)
-    out = torch.empty((N, sh.out_cols), dtype=torch.float32, device=dev)
-    alpha = torch.empty((E2, sh.NH), dtype=torch.float32, device=dev)
-    den = torch.empty((N, sh.NH), dtype=torch.float32, device=dev)
-    argmax = torch.zeros(ARGMAX_CAP + 2, dtype=torch.int64, device=dev)
+                 ptr(M_ord), ptr(_max_ws(dev)), s)
     with _span("edge_forward", (N, E2, sh.NH, sh.F, sh.concat)):
-        call("gatx_edge_forward", ptr(Wh), ptr(S), ptr(M_ord), ptr(graph.rowptr),
-             ptr(graph.col), ptr(graph.perm), N, sh.NH, sh.F, int(sh.concat), int(sh.const),
-             ptr(bias), float(p), seed, ptr(out), ptr(alpha), ptr(den), ptr(argmax), s)
-    saved = dict(W_aug=W_aug, Wh=Wh, S=S, M_ord=M_ord, den=den, argmax=argmax)
+        call("gatx_edge_forward_ex", ptr(Wh), sh.Dp, sh.Fp, ptr(S), ptr(M_ord),
+             ptr(graph.rowptr), ptr(graph.col), ptr(graph.perm), N, sh.NH, sh.F,
+             edge_heads_per_item(sh), int(sh.concat), int(sh.const), ptr(bias), float(p), seed,
+             ptr(out), sh.out_cols, resid_p, sh.out_cols, int(elu), ptr(den), chunk, s)
+    with _span("attention_alpha", (E2, sh.NH)):
+        call("gatx_attention_alpha", ptr(graph.col), ptr(graph.rowidx), ptr(graph.perm), E2,
+             ptr(S), ptr(M_ord), ptr(den), sh.NH, int(sh.const), ptr(alpha), ptr(argmax), s)
+    saved.update(Wh=Wh, S=S, reassoc=False)
     return out, alpha, saved
 
 
@@ -137,6 +257,11 @@ def layer_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShape, 
     g_out = g_out.contiguous()
     E2 = graph.num_edges
     graph.ensure_transpose()
+    if saved["Wh"] is None:   # reassociated forward never built Wh: project now
+        Wh = torch.empty((N, sh.Dp), dtype=torch.float32, device=dev)
+        call("gatx_gemm_f32", N, sh.Dp, sh.F_in, ptr(x), sh.F_in, 1, ptr(saved["W_aug"]), 1,
+             sh.F_in, ptr(Wh), sh.Dp, sh.Dp, None, 0, 0, s)
+        saved["Wh"] = Wh
     G_aug = torch.empty((N, sh.ldg), dtype=torch.float32, device=dev)
     if not sh.const:
         g_raw = torch.empty((max(E2, 1), sh.NH), dtype=torch.float32, device=dev)
@@ -165,8 +290,10 @@ def layer_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShape, 
              ptr(g_x), sh.F_in, sh.F_in, None, 0, 0, s)
     if need_W or need_a:
         gW_aug = torch.empty((sh.K_aug, sh.F_in), dtype=torch.float32, device=dev)
-        call("gatx_gemm_f32", sh.K_aug, sh.F_in, N, ptr(G_aug), 1, sh.ldg, ptr(x), sh.F_in, 1,
-             ptr(gW_aug), sh.F_in, sh.F_in, None, 0, 0, s)
+        ws_bytes = lib.gatx_gemm_splitk_workspace_bytes(sh.K_aug, sh.F_in, N)
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+        call("gatx_gemm_f32_splitk", sh.K_aug, sh.F_in, N, ptr(G_aug), 1, sh.ldg, ptr(x),
+             sh.F_in, 1, ptr(gW_aug), sh.F_in, 0, ptr(ws), ws_bytes, s)
         g_W = torch.empty_like(W)
         g_a = torch.empty_like(a) if a is not None else None
         call("gatx_weight_grads", ptr(gW_aug), ptr(W), ptr(a), sh.NH, sh.F, sh.F_in, ptr(g_W),
@@ -181,27 +308,34 @@ def layer_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShape, 
 
 class GATLayerFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, W, a, bias, graph, sh, p, seed):
-        out, alpha, saved = layer_forward(x, W, a, bias, graph, sh, p, seed)
-        ctx.graph, ctx.sh, ctx.p, ctx.seed, ctx.saved = graph, sh, p, seed, saved
-        ctx.save_for_backward(x, W, a, bias)
+    def forward(ctx, x, W, a, bias, resid, graph, sh, p, seed, elu):
+        out, alpha, saved = layer_forward(x, W, a, bias, graph, sh, p, seed, resid, elu)
+        ctx.graph, ctx.sh, ctx.p, ctx.seed, ctx.saved, ctx.elu = graph, sh, p, seed, saved, elu
+        ctx.has_resid = resid is not None
+        ctx.save_for_backward(x, W, a, bias, out if elu else None)
         return out, alpha
 
     @staticmethod
     def backward(ctx, g_out, g_alpha):
-        x, W, a, bias = ctx.saved_tensors
+        x, W, a, bias, out = ctx.saved_tensors
         if g_out is None:
             g_out = torch.zeros((x.size(0), ctx.sh.out_cols), dtype=torch.float32,
                                 device=x.device)
+        if ctx.elu:   # d elu(v) = 1 (v > 0) else elu(v) + 1, from the saved post-ELU output
+            g_out = g_out * torch.where(out > 0, torch.ones_like(out), out + 1.0)
+        g_resid = g_out if (ctx.has_resid and ctx.needs_input_grad[4]) else None
         nx, nW, na, nb = ctx.needs_input_grad[:4]
         g_x, g_W, g_a, g_b = layer_backward(g_out, g_alpha, x, W, a, bias, ctx.graph, ctx.sh,
                                             ctx.p, ctx.seed, ctx.saved, nx, nW, na, nb)
-        return g_x, g_W, g_a, g_b, None, None, None, None
+        return g_x, g_W, g_a, g_b, g_resid, None, None, None, None, None
 
 
 def gat_layer(x, edge_index, W, a, bias, num_heads, out_features, concat, add_self_loops,
-              const_attention=False, dropout_p=0.0, seed=0, graph: Graph | None = None):
-    """Functional form of GATLayer.forward: returns (out, edge_index', alpha)."""
+              const_attention=False, dropout_p=0.0, seed=0, graph: Graph | None = None,
+              resid=None, elu=False):
+    """Functional form of GATLayer.forward: returns (out, edge_index', alpha).
+    resid / elu fuse GATModel's skip-add and ELU into the layer's epilogue:
+    out = elu?(layer(x) + resid)."""
     from .graph import graph_cache
     _require(x, "x")
     _require(W, "W")
@@ -227,5 +361,11 @@ def gat_layer(x, edge_index, W, a, bias, num_heads, out_features, concat, add_se
         # output (N, F) += bias_param (NH*F,) cannot broadcast (models/gat_layer.py:134-135)
         raise RuntimeError(f"The size of tensor a ({out_features}) must match the size of tensor "
                            f"b ({num_heads * out_features}) at non-singleton dimension 1")
-    out, alpha = GATLayerFunction.apply(x, W, a, bias, graph, sh, float(dropout_p), int(seed))
+    if resid is not None:
+        _require(resid, "resid")
+        resid = resid.contiguous()
+        if resid.shape != (x.size(0), sh.out_cols):
+            raise RuntimeError(f"resid shape {tuple(resid.shape)} != {(x.size(0), sh.out_cols)}")
+    out, alpha = GATLayerFunction.apply(x, W, a, bias, resid, graph, sh, float(dropout_p),
+                                        int(seed), bool(elu))
     return out, graph.edge_index, alpha

@@ -46,7 +46,9 @@ class Graph:
                                "Specify the reduction dim with the 'dim' argument.")
         s = stream()
         stats = torch.empty(3, dtype=torch.int64, device=dev)
-        call("gatx_edge_stats", ptr(edge_index), is64, E, ld, ptr(stats), s)
+        sws = torch.empty(_lib.lib.gatx_edge_stats_workspace_bytes(), dtype=torch.uint8,
+                          device=dev)
+        call("gatx_edge_stats", ptr(edge_index), is64, E, ld, ptr(stats), ptr(sws), s)
         mn, mx, nloops = (int(v) for v in stats.cpu())   # the one host sync per new graph
         if E and mn < 0:
             raise RuntimeError(f"index {mn} is out of bounds: edge_index has negative node ids")

@@ -57,13 +57,18 @@ class GATLayer(nn.Module):
         # one 64-bit draw from torch's CPU generator per forward: follows torch.manual_seed
         return int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
 
-    def forward(self, x, edge_index, return_attention_weights=False, *, graph=None):
+    def forward(self, x, edge_index, return_attention_weights=False, *, graph=None, resid=None,
+                elu=False):
+        """Reference signature (`models/gat_layer.py:42`); keyword-only extras: `graph` (a
+        prebuilt gatx.Graph), `resid` / `elu` (GATModel's skip-add + ELU fused into the
+        epilogue: returns elu?(out + resid))."""
         p = float(self.dropout) if (self.dropout > 0 and self.training) else 0.0
         seed = self._dropout_seed() if p > 0 else 0
         out, edge_index_out, alpha = gat_layer(
             x, edge_index, self.W.weight, None if self.const_attention else self.a.weight,
             self.bias_param if self.bias else None, self.num_heads, self.out_features,
-            self.concat, self.add_self_loops, self.const_attention, p, seed, graph=graph)
+            self.concat, self.add_self_loops, self.const_attention, p, seed, graph=graph,
+            resid=resid, elu=elu)
         self.normalised_attention_coeffs = alpha
         if return_attention_weights:
             return out, (edge_index_out, alpha)

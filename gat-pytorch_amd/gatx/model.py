@@ -50,42 +50,43 @@ class GATModel(nn.Module):
         self.gat_layer_list = nn.ModuleList(gat_layers)
         self.skip_layer_list = nn.ModuleList(skip_layers)
 
-    def _skip(self, i, skip_count, layer_input, x):
+    def _resid(self, i, skip_count, layer_input):
+        """Skip connection of layer i (`models/GATModel.py:135-145`) in the layer's output shape,
+        to be added inside the layer's fused epilogue."""
         skip_output = self.skip_layer_list[skip_count](layer_input)
         if self.heads_concat_per_layer[i]:
-            return x + skip_output
-        skip_output = skip_output.view(-1, self.num_heads_per_layer[i + 1],
-                                       self.head_output_features_per_layer[i + 1])
-        return x + skip_output.mean(dim=1)
+            return skip_output
+        return skip_output.view(-1, self.num_heads_per_layer[i + 1],
+                                self.head_output_features_per_layer[i + 1]).mean(dim=1)
 
-    def forward(self, x, edge_index):
-        skip_count = 0
-        for i in range(len(self.gat_layer_list)):
-            layer_input = x
-            x = F.dropout(x, p=self.dropout, training=self.training)
-            x = self.gat_layer_list[i](x, edge_index)
-            if self.add_skip_connection[i]:
-                x = self._skip(i, skip_count, layer_input, x)
-                skip_count += 1
-            if i != len(self.gat_layer_list) - 1:
-                x = F.elu(x)
-        return x
-
-    def forward_and_return_attention(self, x, edge_index, return_attention_weights=True):
+    def _run(self, x, edge_index, with_attention):
         attention_weights_list = []
         skip_count = 0
-        for i in range(len(self.gat_layer_list)):
+        L = len(self.gat_layer_list)
+        for i in range(L):
             layer_input = x
             x = F.dropout(x, p=self.dropout, training=self.training)
-            x, (edge_index, att) = self.gat_layer_list[i](
-                x, edge_index, return_attention_weights=return_attention_weights)
-            attention_weights_list.append(att)
+            resid = None
             if self.add_skip_connection[i]:
-                x = self._skip(i, skip_count, layer_input, x)
+                resid = self._resid(i, skip_count, layer_input)
                 skip_count += 1
-            if i != len(self.gat_layer_list) - 1:
-                x = F.elu(x)
+            # layer -> (+ skip) -> ELU except after the last layer, fused in the layer epilogue
+            out = self.gat_layer_list[i](x, edge_index, return_attention_weights=with_attention,
+                                         resid=resid, elu=(i != L - 1))
+            if with_attention:
+                x, (edge_index, att) = out
+                attention_weights_list.append(att)
+            else:
+                x = out
         return x, edge_index, attention_weights_list
+
+    def forward(self, x, edge_index):
+        """`models/GATModel.py:120-151`: dropout -> layer -> skip -> ELU, per layer."""
+        return self._run(x, edge_index, False)[0]
+
+    def forward_and_return_attention(self, x, edge_index, return_attention_weights=True):
+        """`models/GATModel.py:153-187`: as forward, also returning edge_index' and the alphas."""
+        return self._run(x, edge_index, True)
 
     @staticmethod
     def calc_attention_norm(edge_index, attention_list):

@@ -43,8 +43,9 @@ int gatx_version(void);
  * int32; rows `ld` elements apart). stats: device int64[3] = {min, max, n_selfloops}.
  * Replaces the `index.max()` of maybe_num_nodes (models/utils.py:70-72) and the `row != col`
  * mask count of add_remaining_self_loops (models/utils.py:58-60). */
+size_t gatx_edge_stats_workspace_bytes(void);
 int gatx_edge_stats(const void* edge_index, int index_is_int64, int64_t E, int64_t ld,
-                    int64_t* stats, gatx_stream_t stream);
+                    int64_t* stats, void* workspace, gatx_stream_t stream);
 
 /* Self-loop rewrite + destination CSR, one pass of device kernels.
  * edge_index' = [edges with src != dst in input order | (i, i) for i < num_loops] when
@@ -88,28 +89,90 @@ int64_t gatx_prepare_weights_floats(int NH, int F, int64_t F_in, int has_a);
 int gatx_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t sam, int64_t sak,
                   const float* B, int64_t sbk, int64_t sbn, float* C0, int64_t ldc0,
                   int64_t n_split, float* C1, int64_t ldc1, int accumulate, gatx_stream_t stream);
+/* Split-K variant for reductions over many rows (g_W_aug = G_aug^T x, K = #nodes): slabs of
+ * partial products in `workspace` (gatx_gemm_splitk_workspace_bytes; 0 = no split needed)
+ * summed in a fixed order by a second kernel (deterministic). */
+size_t gatx_gemm_splitk_workspace_bytes(int64_t M, int64_t N, int64_t K);
+int gatx_gemm_f32_splitk(int64_t M, int64_t N, int64_t K, const float* A, int64_t sam,
+                         int64_t sak, const float* B, int64_t sbk, int64_t sbn, float* C,
+                         int64_t ldc, int accumulate, void* workspace, size_t workspace_bytes,
+                         gatx_stream_t stream);
+
+/* Tuning knob: block-tile rows of gatx_gemm_f32* (128 or 256; 0 = default / env GATX_GEMM_WM). */
+void gatx_set_gemm_rows(int rows);
+
+/* The same for `batch` independent products (batch b offsets A, B, C by b*a_bs, b*b_bs,
+ * b*c_bs floats) with a fused epilogue C = elu?(A*B (+C) + bias[b*bias_bs + n] +
+ * resid[b*resid_bs + m*resid_ld + n]) (bias / resid nullable): the per-head output projection
+ * of the reassociated first layer, with GATModel's skip-add + ELU folded in. */
+int gatx_gemm_f32_batched(int64_t batch, int64_t M, int64_t N, int64_t K, const float* A,
+                          int64_t sam, int64_t sak, int64_t a_bs, const float* B, int64_t sbk,
+                          int64_t sbn, int64_t b_bs, float* C, int64_t ldc, int64_t c_bs,
+                          int accumulate, const float* bias, int64_t bias_bs, const float* resid,
+                          int64_t resid_ld, int64_t resid_bs, int elu, gatx_stream_t stream);
 
 /* ---------------------------------------------------------------- attention + aggregation */
 
 /* Global max M = max_{e,h} s_src[col[e],h] + s_dst[rowidx[e],h]  (gat_layer.py:85), written as an
- * order-preserving uint32 into *M_ord (device). */
+ * order-preserving uint32 into *M_ord (device). workspace: gatx_attention_max_workspace_bytes(). */
+size_t gatx_attention_max_workspace_bytes(void);
 int gatx_attention_max(const int32_t* col, const int32_t* rowidx, int64_t E2, const float* S,
-                       int NH, uint32_t* M_ord, gatx_stream_t stream);
+                       int NH, uint32_t* M_ord, void* workspace, gatx_stream_t stream);
 
-/* Fused edge pass per destination segment (gat_layer.py:85-135):
+/* Fused edge pass per destination segment (gat_layer.py:85-135), then the attention output:
  *   ex = exp(0.01 * (s_src[src] + s_dst[dst] - M))   (LeakyReLU(0.01) of a non-positive value)
  *   den[n,h] = sum_{e->n} ex;  alpha = ex / (den[dst] + 1e-8)   (no per-segment max: :96-109)
  *   out[n,h,:] = sum_{e->n} alpha~ * Wh[src,h,:]   (alpha~ = dropout(alpha), :113-127)
  *   concat: out [N][NH*F]; else out [N][F] = head mean (:129-132); + bias (:134-135, nullable).
  * alpha is written in edge_index' order ([E2][NH], via perm); den [N][NH] is kept for the
  * backward; argmax = int64[GATX_ARGMAX_CAP + 2]: count, then (csr_slot*NH + h) of raw == M
- * entries, then one scratch slot for gatx_max_backward (zeroed by the caller). const_attention: ex = 1 (S, M, argmax unused).
- * dropout_p > 0 applies the counter-based keep mask dropout_keep(seed, e', h) (gatx_common.h). */
+ * entries, then one scratch slot for gatx_max_backward (zeroed by the caller).
+ * const_attention: ex = 1 (S, M, argmax unused). dropout_p > 0 applies the counter-based keep
+ * mask dropout_keep(seed, e', h) (gatx_common.h). = gatx_edge_forward_ex + gatx_attention_alpha. */
 int gatx_edge_forward(const float* Wh, const float* S, const uint32_t* M_ord,
-                      const int32_t* rowptr, const int32_t* col, const int32_t* perm,
-                      int64_t num_nodes, int NH, int F, int concat, int const_attention,
-                      const float* bias, float dropout_p, uint64_t seed, float* out, float* alpha,
-                      float* den, int64_t* argmax, gatx_stream_t stream);
+                      const int32_t* rowptr, const int32_t* col, const int32_t* rowidx,
+                      const int32_t* perm, int64_t num_nodes, int64_t E2, int NH, int F,
+                      int concat, int const_attention, const float* bias, float dropout_p,
+                      uint64_t seed, float* out, float* alpha, float* den, int64_t* argmax,
+                      gatx_stream_t stream);
+
+/* The aggregation half, generalised. Source rows are read at rows + src*row_stride +
+ * h*head_stride (+ f): row_stride = Dp, head_stride = Fp for Wh; for the reassociated first
+ * layer rows = x padded to Fp = round_up(F_in, 4) with head_stride = 0, so the pass aggregates
+ * Z[n,h,:] = sum alpha~ x[src,:] (F = that Fp). One work item is (node, group of heads_per_item
+ * heads) (<= 0: all heads; at most 8; head-mean needs all heads); items are swept in chunks of
+ * `chunk` nodes per head group (<= 0: 2048) so one XCD's L2 holds one head's slice of the rows.
+ * out rows are out_ld floats apart; fused epilogue out = elu?(agg + bias + resid) with resid
+ * [N][resid_ld] (nullable) and elu in {0, 1} (GATModel's skip-add + ELU). Writes den. */
+int gatx_edge_forward_ex(const float* rows, int64_t row_stride, int64_t head_stride,
+                         const float* S, const uint32_t* M_ord, const int32_t* rowptr,
+                         const int32_t* col, const int32_t* perm, int64_t num_nodes, int NH,
+                         int F, int heads_per_item, int concat, int const_attention,
+                         const float* bias, float dropout_p, uint64_t seed, float* out,
+                         int64_t out_ld, const float* resid, int64_t resid_ld, int elu,
+                         float* den, int64_t chunk, gatx_stream_t stream);
+
+/* alpha [E2][NH] in edge_index' order from S, M and den (one thread per CSR slot, all heads of
+ * an edge stored together), plus the argmax records (see gatx_edge_forward). */
+int gatx_attention_alpha(const int32_t* col, const int32_t* rowidx, const int32_t* perm,
+                         int64_t E2, const float* S, const uint32_t* M_ord, const float* den,
+                         int NH, int const_attention, float* alpha, int64_t* argmax,
+                         gatx_stream_t stream);
+
+/* S [N][2NH] = (Wh . A_src^T | Wh . A_dst^T) from Wh [N][Dp] and a.weight — the reference's own
+ * association of the logit GEMV (gat_layer.py:76-82), used when folding the scores into the
+ * projection GEMM would cost a whole extra column tile. */
+int gatx_node_scores(const float* Wh, int64_t num_nodes, int NH, int F, const float* a, float* S,
+                     gatx_stream_t stream);
+
+/* Diagnostic ablations of the edge pass for profiling only (results are WRONG when set):
+ * bit 1 skip exp (ex = 1). */
+void gatx_set_debug(int flags);
+
+/* Copy an [rows x cols] matrix (row stride ld_src) into [rows x ld_dst], zero-filling columns
+ * cols..ld_dst-1 (float4-aligned source rows for the gathers). */
+int gatx_pad_rows(const float* src, int64_t rows, int64_t cols, int64_t ld_src, float* dst,
+                  int64_t ld_dst, gatx_stream_t stream);
 
 /* ---------------------------------------------------------------- backward (autograd of above) */
 

@@ -233,3 +233,84 @@ def test_errors_mirror_reference(device):
         layer(x, torch.tensor([[0, 7], [1, 2]], device=device))
     with pytest.raises(RuntimeError):
         layer(x.cpu(), torch.tensor([[0, 1], [1, 2]]))
+
+
+@pytest.mark.parametrize("reassoc", ["0", "1"])
+@pytest.mark.parametrize("fin,NH,F", [(50, 4, 256), (3, 4, 12), (13, 2, 40)])
+def test_reassociation_paths(reassoc, fin, NH, F, device, monkeypatch):
+    """First-layer reassociation (aggregate x rows, then project per head) vs the direct path;
+    both against the oracle, forward and backward."""
+    monkeypatch.setenv("GATX_REASSOC", reassoc)
+    _layer_vs_oracle(device, 2, 150, 2500, fin, NH, F, True)
+
+
+@pytest.mark.parametrize("hs", ["1", "2", "4"])
+@pytest.mark.parametrize("chunk", ["0", "7"])
+def test_heads_per_item_and_chunking(hs, chunk, device, monkeypatch):
+    monkeypatch.setenv("GATX_HEADS_PER_ITEM", hs)
+    monkeypatch.setenv("GATX_EDGE_CHUNK", chunk)
+    _layer_vs_oracle(device, 3, 100, 2000, 300, 4, 64, True)
+
+
+@pytest.mark.parametrize("concat,fin", [(True, 16), (False, 16), (True, 512)])
+def test_fused_skip_elu_epilogue(concat, fin, device):
+    """layer(x, resid=r, elu=True) == elu(layer(x) + r), with gradients through both."""
+    gatx = _gatx()
+    from gatx import data as gd
+    NH, F = 4, 32
+    b = gd.uniform_graph_batch(2, 120, 1500, fin, feature_seed=9)
+    W = gd.xavier_uniform(10, NH * F, fin)
+    a = gd.xavier_uniform(11, NH, NH * 2 * F)
+    cols = NH * F if concat else F
+    r = gd.normal(12, b.num_nodes * cols).reshape(b.num_nodes, cols)
+    layer = gatx.GATLayer(fin, F, NH, concat, add_self_loops=True).to(device)
+    with torch.no_grad():
+        layer.W.weight.copy_(torch.from_numpy(W))
+        layer.a.weight.copy_(torch.from_numpy(a))
+    x = torch.from_numpy(b.x).to(device).requires_grad_(True)
+    rt = torch.from_numpy(r).to(device).requires_grad_(True)
+    ei = torch.from_numpy(b.edge_index).to(device)
+    out = layer(x, ei, resid=rt, elu=True)
+    g = gd.normal(13, out.numel()).reshape(tuple(out.shape))
+    (out * torch.from_numpy(g).to(device)).sum().backward()
+    o, _, _, cache = orc.gat_layer_forward(b.x, b.edge_index, W, a, NH, F, concat)
+    pre = o + r
+    post = orc.elu(pre)
+    assert np.abs(out.detach().cpu().numpy() - post).max() <= OUT_TOL
+    g_pre = g * np.where(pre > 0, 1.0, np.exp(pre)).astype(np.float32)
+    gr = orc.gat_layer_backward(cache, g_pre)
+    assert np.abs(rt.grad.cpu().numpy() - g_pre).max() <= GRAD_TOL * max(1, np.abs(g_pre).max())
+    for k, t in (("x", x.grad), ("W", layer.W.weight.grad), ("a", layer.a.weight.grad)):
+        ref = gr[k]
+        assert np.abs(t.cpu().numpy() - ref).max() <= GRAD_TOL * max(1.0, np.abs(ref).max()), k
+
+
+def test_gemm_splitk_and_node_scores(device):
+    from gatx._lib import call, lib, ptr, stream
+    torch.manual_seed(1)
+    for (M, N, K) in [(100, 70, 20000), (1032, 200, 5000), (33, 1024, 3000)]:
+        A = torch.randn(K, M, device=device)          # A(m,k) = A[k, m]  (G_aug^T layout)
+        B = torch.randn(K, N, device=device)
+        ref = (A.double().t() @ B.double()).float()
+        wsb = lib.gatx_gemm_splitk_workspace_bytes(M, N, K)
+        ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=device)
+        C = torch.full((M, N), float("nan"), device=device)
+        call("gatx_gemm_f32_splitk", M, N, K, ptr(A), 1, M, ptr(B), N, 1, ptr(C), N, 0, ptr(ws),
+             wsb, stream())
+        torch.cuda.synchronize()
+        assert (C - ref).abs().max().item() < 1e-4 * K ** 0.5, (M, N, K)
+    # node scores == Wh . A2^T (reference association of the logit GEMV)
+    from gatx import data as gd
+    NH, F, N = 4, 30, 333
+    Wh = torch.from_numpy(gd.normal(3, N * NH * 32).reshape(N, NH * 32)).to(device)
+    Wh.view(N, NH, 32)[:, :, F:] = 0
+    a = torch.from_numpy(gd.xavier_uniform(4, NH, NH * 2 * F)).to(device)
+    S = torch.empty(N, 2 * NH, device=device)
+    call("gatx_node_scores", ptr(Wh), N, NH, F, ptr(a), ptr(S), stream())
+    A = a.view(NH, NH, 2, F)
+    Whv = Wh.view(N, NH, 32)[:, :, :F].double()
+    ref_src = torch.einsum("nkf,hkf->nh", Whv, A[:, :, 0].double())
+    ref_dst = torch.einsum("nkf,hkf->nh", Whv, A[:, :, 1].double())
+    torch.cuda.synchronize()
+    assert (S[:, :NH].double() - ref_src).abs().max().item() < 1e-4
+    assert (S[:, NH:].double() - ref_dst).abs().max().item() < 1e-4
