@@ -137,7 +137,9 @@ __device__ inline void tile_of(int64_t b, int64_t T, int64_t tiles_n, int64_t& t
 // Block tile (64*WM) x 128 x 32, 2*WM waves as WM x 2; each wave owns a 64 x 64 sub-tile =
 // 2 x 2 MFMA blocks of 32 x 32. A_KC: A is k-contiguous (sak == 1, ld = sam) else m-contiguous;
 // B_NC: B is n-contiguous (sbn == 1, ld = sbk) else k-contiguous.
-template <bool A_KC, bool B_NC, int WM>
+// TAG only separates the symbol names of the call sites in profiles (0 = forward projection,
+// 1 = auxiliary products, 2 = split-K weight gradient); the code is identical.
+template <bool A_KC, bool B_NC, int WM, int TAG>
 __global__ void __launch_bounds__(128 * WM, 2) gemm_f32_kernel(GemmArgs g) {
   constexpr int BM = 64 * WM, BN = 128, THREADS = 128 * WM;
   using AL = typename std::conditional<A_KC, KContig<BM, THREADS>, RContig<BM, THREADS>>::type;
@@ -234,7 +236,7 @@ __global__ void __launch_bounds__(128 * WM, 2) gemm_f32_kernel(GemmArgs g) {
     }
 }
 
-template <int WM>
+template <int WM, int TAG>
 int launch_gemm(const GemmArgs& g0, bool a_kc, bool b_nc, int batch, hipStream_t stream) {
   GemmArgs g = g0;
   g.tiles_m = ceil_div(g.M, 64 * WM);
@@ -243,10 +245,10 @@ int launch_gemm(const GemmArgs& g0, bool a_kc, bool b_nc, int batch, hipStream_t
   GATX_REQUIRE(tiles < (1ll << 31) && batch < 65536, "gemm: too many tiles");
   dim3 grid((unsigned)tiles, (unsigned)batch, (unsigned)g.splits);
   constexpr int TH = 128 * WM;
-  if (a_kc && b_nc) gemm_f32_kernel<true, true, WM><<<grid, TH, 0, stream>>>(g);
-  else if (a_kc) gemm_f32_kernel<true, false, WM><<<grid, TH, 0, stream>>>(g);
-  else if (b_nc) gemm_f32_kernel<false, true, WM><<<grid, TH, 0, stream>>>(g);
-  else gemm_f32_kernel<false, false, WM><<<grid, TH, 0, stream>>>(g);
+  if (a_kc && b_nc) gemm_f32_kernel<true, true, WM, TAG><<<grid, TH, 0, stream>>>(g);
+  else if (a_kc) gemm_f32_kernel<true, false, WM, TAG><<<grid, TH, 0, stream>>>(g);
+  else if (b_nc) gemm_f32_kernel<false, true, WM, TAG><<<grid, TH, 0, stream>>>(g);
+  else gemm_f32_kernel<false, false, WM, TAG><<<grid, TH, 0, stream>>>(g);
   GATX_LAUNCH_CHECK("gemm_f32");
   if (g.splits > 1) {
     const int64_t total = g.M * g.N * batch;
@@ -277,7 +279,8 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
                      int64_t b_bs, float* C0, int64_t ldc0, int64_t c0_bs, int64_t n_split,
                      float* C1, int64_t ldc1, int64_t c1_bs, int accumulate, const float* bias,
                      int64_t bias_bs, const float* resid, int64_t resid_ld, int64_t resid_bs,
-                     int elu, void* workspace, size_t workspace_bytes, hipStream_t stream) {
+                     int elu, void* workspace, size_t workspace_bytes, int tag,
+                     hipStream_t stream) {
   GATX_REQUIRE(M >= 0 && N >= 0 && K >= 0 && batch >= 1, "gemm: negative size");
   if (M == 0 || N == 0) return 0;
   GATX_REQUIRE(sak == 1 || sam == 1, "gemm: A needs a unit stride");
@@ -320,8 +323,10 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
       g.partial = (float*)workspace;
     }
   }
-  if (wm == 2) return launch_gemm<2>(g, a_kc, b_nc, batch, stream);
-  return launch_gemm<4>(g, a_kc, b_nc, batch, stream);
+  if (wm == 4) return launch_gemm<4, 1>(g, a_kc, b_nc, batch, stream);   // tuning only
+  if (tag == 0) return launch_gemm<2, 0>(g, a_kc, b_nc, batch, stream);
+  if (tag == 2) return launch_gemm<2, 2>(g, a_kc, b_nc, batch, stream);
+  return launch_gemm<2, 1>(g, a_kc, b_nc, batch, stream);
 }
 
 extern "C" void gatx_set_gemm_rows(int rows) { g_gemm_wm = rows / 64; }
@@ -331,7 +336,15 @@ extern "C" int gatx_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, in
                              int64_t ldc0, int64_t n_split, float* C1, int64_t ldc1,
                              int accumulate, gatx_stream_t s) {
   return gemm_impl(M, N, K, 1, A, sam, sak, 0, B, sbk, sbn, 0, C0, ldc0, 0, n_split, C1, ldc1, 0,
-                   accumulate, nullptr, 0, nullptr, 0, 0, 0, nullptr, 0, (hipStream_t)s);
+                   accumulate, nullptr, 0, nullptr, 0, 0, 0, nullptr, 0, 1, (hipStream_t)s);
+}
+
+extern "C" int gatx_projection_gemm(int64_t M, int64_t N, int64_t K, const float* A, int64_t sam,
+                                    int64_t sak, const float* B, int64_t sbk, int64_t sbn,
+                                    float* C0, int64_t ldc0, int64_t n_split, float* C1,
+                                    int64_t ldc1, gatx_stream_t s) {
+  return gemm_impl(M, N, K, 1, A, sam, sak, 0, B, sbk, sbn, 0, C0, ldc0, 0, n_split, C1, ldc1, 0,
+                   0, nullptr, 0, nullptr, 0, 0, 0, nullptr, 0, 0, (hipStream_t)s);
 }
 
 extern "C" int gatx_gemm_f32_batched(int64_t batch, int64_t M, int64_t N, int64_t K,
@@ -343,7 +356,7 @@ extern "C" int gatx_gemm_f32_batched(int64_t batch, int64_t M, int64_t N, int64_
                                      gatx_stream_t s) {
   return gemm_impl(M, N, K, (int)batch, A, sam, sak, a_bs, B, sbk, sbn, b_bs, C, ldc, c_bs, N,
                    nullptr, 0, 0, accumulate, bias, bias_bs, resid, resid_ld, resid_bs, elu,
-                   nullptr, 0, (hipStream_t)s);
+                   nullptr, 0, 1, (hipStream_t)s);
 }
 
 extern "C" size_t gatx_gemm_splitk_workspace_bytes(int64_t M, int64_t N, int64_t K) {
@@ -357,6 +370,6 @@ extern "C" int gatx_gemm_f32_splitk(int64_t M, int64_t N, int64_t K, const float
                                     float* C, int64_t ldc, int accumulate, void* workspace,
                                     size_t workspace_bytes, gatx_stream_t s) {
   return gemm_impl(M, N, K, 1, A, sam, sak, 0, B, sbk, sbn, 0, C, ldc, 0, N, nullptr, 0, 0,
-                   accumulate, nullptr, 0, nullptr, 0, 0, 0, workspace, workspace_bytes,
+                   accumulate, nullptr, 0, nullptr, 0, 0, 0, workspace, workspace_bytes, 2,
                    (hipStream_t)s);
 }

@@ -45,6 +45,8 @@ SIGNATURES = {
     "gatx_edge_forward_ex": (c_i, [P, c_i64, c_i64, P, P, P, P, P, c_i64, c_i, c_i, c_i, c_i, c_i,
                                    P, c_f, c_u64, P, c_i64, P, c_i64, c_i, P, c_i64, P]),
     "gatx_pad_rows": (c_i, [P, c_i64, c_i64, c_i64, P, c_i64, P]),
+    "gatx_projection_gemm": (c_i, [c_i64, c_i64, c_i64, P, c_i64, c_i64, P, c_i64, c_i64, P,
+                                   c_i64, c_i64, P, c_i64, P]),
     "gatx_set_gemm_rows": (None, [c_i]),
     "gatx_set_debug": (None, [c_i]),
     "gatx_gemm_splitk_workspace_bytes": (c_sz, [c_i64, c_i64, c_i64]),

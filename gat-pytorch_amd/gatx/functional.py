@@ -225,12 +225,12 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
     S = torch.empty((N, max(sh.H2, 1)), **f32)
     if fold_scores_into_gemm(sh):
         with _span("gemm", (N, sh.K_aug, sh.F_in, sh.NH, sh.F)):
-            call("gatx_gemm_f32", N, sh.K_aug, sh.F_in, ptr(x), sh.F_in, 1, ptr(W_aug), 1,
-                 sh.F_in, ptr(Wh), sh.Dp, sh.Dp, ptr(S), max(sh.H2, 1), 0, s)
+            call("gatx_projection_gemm", N, sh.K_aug, sh.F_in, ptr(x), sh.F_in, 1, ptr(W_aug), 1,
+                 sh.F_in, ptr(Wh), sh.Dp, sh.Dp, ptr(S), max(sh.H2, 1), s)
     else:
         with _span("gemm", (N, sh.Dp, sh.F_in, sh.NH, sh.F)):
-            call("gatx_gemm_f32", N, sh.Dp, sh.F_in, ptr(x), sh.F_in, 1, ptr(W_aug), 1,
-                 sh.F_in, ptr(Wh), sh.Dp, sh.Dp, None, 0, 0, s)
+            call("gatx_projection_gemm", N, sh.Dp, sh.F_in, ptr(x), sh.F_in, 1, ptr(W_aug), 1,
+                 sh.F_in, ptr(Wh), sh.Dp, sh.Dp, None, 0, s)
         with _span("node_scores", (N, sh.NH, sh.F)):
             call("gatx_node_scores", ptr(Wh), N, sh.NH, sh.F, ptr(a), ptr(S), s)
     if not sh.const:

@@ -101,6 +101,13 @@ int gatx_gemm_f32_splitk(int64_t M, int64_t N, int64_t K, const float* A, int64_
 /* Tuning knob: block-tile rows of gatx_gemm_f32* (128 or 256; 0 = default / env GATX_GEMM_WM). */
 void gatx_set_gemm_rows(int rows);
 
+/* gatx_gemm_f32 for the forward projection x . W_aug^T (accumulate = 0); a separate entry point
+ * only so profiles can tell the projection launches from the auxiliary products. */
+int gatx_projection_gemm(int64_t M, int64_t N, int64_t K, const float* A, int64_t sam,
+                         int64_t sak, const float* B, int64_t sbk, int64_t sbn, float* C0,
+                         int64_t ldc0, int64_t n_split, float* C1, int64_t ldc1,
+                         gatx_stream_t stream);
+
 /* The same for `batch` independent products (batch b offsets A, B, C by b*a_bs, b*b_bs,
  * b*c_bs floats) with a fused epilogue C = elu?(A*B (+C) + bias[b*bias_bs + n] +
  * resid[b*resid_bs + m*resid_ld + n]) (bias / resid nullable): the per-head output projection

@@ -2,7 +2,7 @@
 dispatch and mean duration. FETCH_SIZE / WRITE_SIZE are in KB; on gfx950 FETCH_SIZE reports
 half the bytes of wide (16 B/lane) coalesced reads (MI355X_MICROARCH.md §HBM), so HBM read
 bytes = 2 x FETCH_SIZE x 1024 for such kernels.
-    python tools/pmc_summary.py gpurun_out/pmc1 [> profiles/rNN/pmc_summary.txt]"""
+    python tools/pmc_summary.py gpurun_out/pmc1 [profiles/pmc_latest.json] [> summary.txt]"""
 import csv
 import glob
 import os
@@ -29,6 +29,21 @@ for f in sorted(glob.glob(os.path.join(base + "_p*", "**", "*counter_collection.
         if key not in seen:
             seen.add(key)
             acc[name]["_dur_us"].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+import json
+out_json = {"source": "rocprofv3 --pmc, bench.py --steps 3 --cached-graph, round 1", "kernels": {}}
+for n, cs in acc.items():
+    d = {k: sum(v) / len(v) for k, v in cs.items()}
+    out_json["kernels"][n] = {
+        "launches": len(cs["_dur_us"]) // max(1, len([d for d in glob.glob(base + "_p*")
+                                                       if os.path.isdir(d)])),
+        "dur_us": d.get("_dur_us", 0.0),
+        # gfx950: FETCH_SIZE counts half the bytes of 16-B/lane coalesced reads -> x2
+        "hbm_read_bytes": 2 * d.get("FETCH_SIZE", 0.0) * 1024,
+        "hbm_write_bytes": d.get("WRITE_SIZE", 0.0) * 1024,
+        "l2_hit": (d.get("TCC_HIT_sum", 0) / (d.get("TCC_HIT_sum", 0) + d.get("TCC_MISS_sum", 0))
+                   if d.get("TCC_HIT_sum", 0) + d.get("TCC_MISS_sum", 0) else None)}
+if len(sys.argv) > 2:
+    json.dump(out_json, open(sys.argv[2], "w"), indent=1)
 rows = sorted(((n, {k: sum(v) / len(v) for k, v in cs.items()}) for n, cs in acc.items()),
               key=lambda x: -x[1].get("_dur_us", 0) * len(acc[x[0]]["_dur_us"]))
 print(f"{'kernel':60s} {'dur_us':>8s} {'FETCHx2_MB':>10s} {'WRITE_MB':>9s} {'HBM_GB/s':>9s} "
