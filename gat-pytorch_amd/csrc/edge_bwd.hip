@@ -1,18 +1,21 @@
 // Backward of the GATLayer attention + aggregation: the closed form of torch autograd through
 // models/gat_layer.py:64-135, as passes over the two CSR orders.
 //
-//   dst pass  (per destination n, one wave): g_alpha~ = <go[n,h,:], Wh[src,h,:]> per edge & head
-//             (go row held in registers, Wh[src] streamed), softmax backward
-//             c = sum g_alpha * alpha, g_raw' = 0.01 * ex * (g_alpha - c) / (den + 1e-8),
-//             g_s_dst = sum_e g_raw', and a per-workgroup partial of sum g_raw' for max()'s grad.
-//   max bwd   g_M = -sum g_raw' split evenly over the argmax entries recorded by the forward.
-//   src pass  (per source s, one wave): the message gradient sum alpha~ * go[dst] (go rows
-//             streamed) and g_s_src = sum_e g_raw' + the max() correction, written as one row of
-//             G_aug = [g_Wh | g_s_src | g_s_dst], the gradient of the augmented projection.
+//   prepare_go  go = g_out * elu'(out) (fused-epilogue layers), scaled 1/NH for head-mean layers,
+//               written head-padded [N][NH][Fp] (or [N][Fp] for head-mean) so every later gather is
+//               an aligned float4; optionally also the residual's gradient.
+//   dst pass    one wave per (destination n, head h): g_alpha~[e] = <go[n,h,:], Wh[src_e,h,:]>
+//               (go in registers, Wh rows gathered with a wave-uniform scalar address, the dot
+//               reduced with DPP + permlane swaps), then softmax backward:
+//               c = sum_e g_alpha alpha, g_raw'[e] = 0.01 ex (g_alpha - c) / (den + 1e-8),
+//               g_s_dst[n,h] = sum_e g_raw'  (g_raw' stored head-major [NH][E2] in CSR order).
+//   max bwd     g_M = -sum g_raw' (= -sum g_s_dst), split evenly over the argmax entries.
+//   src pass    one wave per (source s, head h): the message gradient sum alpha~ go[dst] (go rows
+//               gathered like the forward gathers Wh rows) and g_s_src = sum g_raw' + max share,
+//               written as one row of G_aug = [g_Wh | g_s_src | g_s_dst].
 // The weight/input gradients then come from two MFMA GEMMs on G_aug (gemm.hip) and
-// gatx_weight_grads, which maps g_W_aug back onto W.weight and a.weight.
-// No float atomics on the data path: every sum has a fixed order (bitwise reproducible), except
-// the tie-split of max()'s gradient when several argmax entries share a node.
+// gatx_weight_grads. No float atomics on the data path: every sum has a fixed order (bitwise
+// reproducible), except the tie-split of max()'s gradient when several argmax entries share a node.
 #include "gatx_common.h"
 
 namespace gatx {
@@ -23,127 +26,218 @@ inline unsigned grid_for(int64_t n, int block = 256, int64_t cap = 16384) {
   return (unsigned)(g < cap ? g : cap);
 }
 
-// Load chunk q (4 features of head h) of the upstream gradient row of node n, in the padded
-// [NH][Fp] layout; f >= F reads as 0. Head-mean layers broadcast g_out[n, :F] / NH to all heads.
-__device__ inline float4 load_go(const float* __restrict__ g_out, int64_t n, int q, int NH, int F,
-                                 int Fp, int concat, float inv_nh) {
-  const int h = (q * 4) / Fp, f0 = q * 4 - h * Fp;
-  const float* row = concat ? g_out + n * (int64_t)(NH * F) + h * F : g_out + n * (int64_t)F;
-  float4 v;
-  if ((F & 3) == 0) {
-    v = *(const float4*)(row + f0);
-  } else {
-    v.x = (f0 + 0 < F) ? row[f0 + 0] : 0.f;
-    v.y = (f0 + 1 < F) ? row[f0 + 1] : 0.f;
-    v.z = (f0 + 2 < F) ? row[f0 + 2] : 0.f;
-    v.w = (f0 + 3 < F) ? row[f0 + 3] : 0.f;
+__device__ inline int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ inline float lane_f(float v, int j) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+}
+template <int CTRL>
+__device__ inline float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+// Sum over aligned groups of L lanes (L = 1..64); every lane of a group gets the group's total.
+// xor 1/2 via quad_perm, 4/8 via row half-mirror / mirror (valid once the smaller groups agree),
+// 16/32 via the gfx950 permlane swaps (r[0] + r[1] = own + partner).
+template <int L>
+__device__ inline float group_sum(float v) {
+  if (L >= 2) v += dpp<0xB1>(v);
+  if (L >= 4) v += dpp<0x4E>(v);
+  if (L >= 8) v += dpp<0x141>(v);
+  if (L >= 16) v += dpp<0x140>(v);
+  if (L >= 32) {
+    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
   }
-  return concat ? v : v * inv_nh;
+  if (L >= 64) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  return v;
 }
 
-template <int LPE, int CPL>
-__global__ void __launch_bounds__(256)
-edge_bwd_dst_kernel(const float* __restrict__ Wh, const float* __restrict__ S,
-                    const uint32_t* __restrict__ M_ord, const float* __restrict__ den,
-                    const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
-                    const int32_t* __restrict__ perm, int64_t N, int NH, int F, int Fp,
-                    int concat, float p_drop, uint64_t seed, const float* __restrict__ g_out,
-                    const float* __restrict__ g_alpha_ret, float* __restrict__ g_raw,
-                    float* __restrict__ G_aug, int64_t ldg, float* __restrict__ partials) {
-  __shared__ float part_lds[4];
-  constexpr int EPW = 64 / LPE;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int grp = lane / LPE, li = lane % LPE;
-  const int D4 = NH * Fp / 4, F4 = Fp / 4, S2 = 2 * NH;
-  const int64_t Dp = (int64_t)NH * Fp;
-  const float M = ord_to_float(*M_ord);
-  const bool drop = p_drop > 0.f;
-  const float drop_scale = drop ? 1.f / (1.f - p_drop) : 1.f;
-  const float inv_nh = 1.f / (float)NH;
-  const float4* __restrict__ Wh4 = (const float4*)Wh;
-  // lane li < NH of every edge group owns head li for the per-(edge, head) scalars
-  const bool owner = li < NH;
-  const int hl = owner ? li : 0;
+__device__ inline int64_t xcd_contiguous(int64_t b, int64_t nb) {
+  const int64_t q = nb / 8, r = nb % 8, xcd = b % 8, j = b / 8;
+  return (xcd < r) ? xcd * (q + 1) + j : r * (q + 1) + (xcd - r) * q + j;
+}
 
-  int q[CPL], hc[CPL];
+// (node, head) work item -> n, h with chunked sweeps (one head over `chunk` nodes at a time).
+__device__ inline bool decode_item(int64_t item, int64_t N, int NH, int64_t chunk, int64_t& n,
+                                   int& h) {
+  const int64_t per_chunk = chunk * NH;
+  const int64_t ck = item / per_chunk, rem = item - ck * per_chunk;
+  h = (int)(rem / chunk);
+  n = ck * chunk + (rem - (int64_t)h * chunk);
+  return n < N;
+}
+
+// go [N][GW] (GW = NH*Fp concat, Fp head-mean): elu-gated, 1/NH-scaled, head-padded g_out.
+__global__ void __launch_bounds__(256) prepare_go_kernel(const float* __restrict__ g_out,
+                                                         const float* __restrict__ out,
+                                                         int64_t N, int NH, int F, int Fp,
+                                                         int concat, int elu,
+                                                         float* __restrict__ go,
+                                                         float* __restrict__ g_pre) {
+  const int OC = concat ? NH * F : F, GW = concat ? NH * Fp : Fp;
+  const float scale = concat ? 1.f : 1.f / (float)NH;
+  const int64_t total = N * GW;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t n = t / GW;
+    const int c = (int)(t - n * GW), h = c / Fp, f = c - h * Fp;
+    float v = 0.f;
+    if (f < F) {
+      const int64_t src = n * OC + (concat ? h * F + f : f);
+      v = g_out[src];
+      if (elu) {
+        const float o = out[src];
+        v = o > 0.f ? v : v * (o + 1.f);   // d elu(x) = elu(x) + 1 for x <= 0
+      }
+      if (g_pre) g_pre[src] = v;
+    }
+    go[t] = v * scale;
+  }
+}
+
+struct BwdArgs {
+  const float* Wh;      // [N][Dp]
+  const float* go;      // prepared upstream gradient rows
+  int64_t go_stride4;   // float4s per go row
+  int go_head4;         // float4s between heads in a go row (0 for head-mean)
+  const float* S;
+  const uint32_t* M_ord;
+  const float* den;
+  const int32_t* rowptr;   // dst CSR (dst pass) / src CSR (src pass)
+  const int32_t* col;      // src of each dst-CSR slot / dst of each src-CSR slot
+  const int32_t* seid;     // src pass: dst-CSR slot of each src-CSR slot
+  const int32_t* perm;
+  int64_t N, E2;
+  int NH, F, Fp, const_att;
+  float p_drop;
+  uint64_t seed;
+  const float* g_alpha_ret;
+  float* g_raw;            // [NH][E2] head-major, dst-CSR order
+  float* gsd;              // [N][NH] compact copy of g_s_dst (for max()'s gradient)
+  const float* g_corr;     // [N][NH] max() share for the src pass
+  float* G_aug;
+  int64_t ldg, chunk, n_items;
+};
+
+// dst pass: one wave per (destination n, head h); LPE lanes per edge over the head's Fp/4
+// chunks (CPL per lane), 64/LPE edges per step.
+template <int LPE, int CPL>
+__global__ void __launch_bounds__(256) edge_bwd_dst_kernel(BwdArgs g) {
+  constexpr int EPW = 64 / LPE;
+  const int lane = threadIdx.x & 63;
+  const int wave = uni(threadIdx.x >> 6);
+  const int grp = lane / LPE, li = lane % LPE;
+  const int64_t item = xcd_contiguous(blockIdx.x, gridDim.x) * 4 + wave;
+  if (item >= g.n_items) return;
+  int64_t n;
+  int h;
+  if (!decode_item(item, g.N, g.NH, g.chunk, n, h)) return;
+  const int NH = g.NH, Fp = g.Fp, F4 = Fp / 4, S2 = 2 * NH;
+  const int64_t Dp = (int64_t)NH * Fp, E2 = g.E2;
+  const float M = ord_to_float(*g.M_ord);
+  const bool drop = g.p_drop > 0.f;
+  const float drop_scale = drop ? 1.f / (1.f - g.p_drop) : 1.f;
+  const float4* __restrict__ Wh4 = (const float4*)g.Wh;
+  const float4* __restrict__ go4 = (const float4*)g.go;
+
+  int off4[CPL];
   bool vq[CPL];
+  float4 gv[CPL];
 #pragma unroll
   for (int c = 0; c < CPL; ++c) {
-    q[c] = c * LPE + li;
-    vq[c] = q[c] < D4;
-    hc[c] = vq[c] ? q[c] / F4 : -1;
+    const int q = c * LPE + li;
+    vq[c] = q < F4;
+    off4[c] = h * F4 + (vq[c] ? q : 0);
+    gv[c] = vq[c] ? go4[n * g.go_stride4 + h * g.go_head4 + q] : make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  float wave_part = 0.f;
+  const float sdst = g.S[n * S2 + NH + h];
+  const float dinv = 1.f / (g.den[n * NH + h] + kSoftmaxEps);
+  float* __restrict__ graw = g.g_raw + (int64_t)h * E2;
+  __shared__ int src_sh[4][64];
+  __shared__ float dot_sh[4][64];
+  int* src_lds = src_sh[wave];
+  float* dot_lds = dot_sh[wave];
 
-  for (int64_t n = blockIdx.x * 4ll + wave; n < N; n += gridDim.x * 4ll) {
-    const int beg = rowptr[n], end = rowptr[n + 1];
-    float4 go[CPL];
-#pragma unroll
-    for (int c = 0; c < CPL; ++c)
-      go[c] = vq[c] ? load_go(g_out, n, q[c], NH, F, Fp, concat, inv_nh)
-                    : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float sdst = S[n * S2 + NH + hl];
-    const float dinv = 1.f / (den[n * NH + hl] + kSoftmaxEps);
-    // loop 1: g_alpha per (edge, head) and c = sum g_alpha * alpha
-    float c_acc = 0.f;
-    for (int e = beg + grp; e < end; e += EPW) {
-      const int64_t s = col[e];
-      float pc[CPL];
+  const int beg = uni(g.rowptr[n]), end = uni(g.rowptr[n + 1]);
+  // sweep 1: g_alpha per edge (stored), c = sum g_alpha * alpha
+  float c_acc = 0.f;
+  for (int base = beg; base < end; base += 64) {
+    const int cnt = min(64, end - base);
+    const bool valid = lane < cnt;
+    const int e = base + min(lane, cnt - 1);
+    const int my_src = g.col[e];
+    const float ex = att_exp(g.S[(int64_t)my_src * S2 + h] + sdst, M);
+    if (EPW > 1) src_lds[lane] = my_src;
+    if (EPW > 1) wave_lds_sync();
+    float my_dot = 0.f;
+    for (int j0 = grp; j0 < cnt; j0 += EPW) {
+      const int sj = (EPW == 1) ? __builtin_amdgcn_readlane(my_src, j0) : src_lds[j0];
+      const float4* rp = Wh4 + (int64_t)sj * (Dp / 4);
+      float p = 0.f;
 #pragma unroll
       for (int c = 0; c < CPL; ++c) {
-        pc[c] = 0.f;
-        if (!vq[c]) continue;
-        const float4 v = Wh4[s * D4 + q[c]];
-        pc[c] = go[c].x * v.x + go[c].y * v.y + go[c].z * v.z + go[c].w * v.w;
+        const float4 v = rp[off4[c]];
+        p += gv[c].x * v.x + gv[c].y * v.y + gv[c].z * v.z + gv[c].w * v.w;
       }
-      float mine = 0.f;
-      for (int h = 0; h < NH; ++h) {   // per-head sum over the group's lanes
-        float t = 0.f;
-#pragma unroll
-        for (int c = 0; c < CPL; ++c) t += (hc[c] == h) ? pc[c] : 0.f;
-#pragma unroll
-        for (int off = 1; off < LPE; off <<= 1) t += __shfl_xor(t, off);
-        if (li == h) mine = t;
-      }
-      if (owner) {
-        const float alpha = att_exp(S[s * S2 + hl] + sdst, M) * dinv;
-        float ga = mine;
-        if (drop) ga = dropout_keep(seed, (int64_t)perm[e] * NH + hl, p_drop) ? ga * drop_scale : 0.f;
-        if (g_alpha_ret) ga += g_alpha_ret[(int64_t)perm[e] * NH + hl];
-        g_raw[(int64_t)e * NH + hl] = ga;   // g_alpha for now; the same lane rewrites it below
-        c_acc += ga * alpha;
+      p = group_sum<LPE>(p);
+      if (EPW == 1) {
+        if (lane == j0) my_dot = p;
+      } else if (li == 0) {
+        dot_lds[j0] = p;
       }
     }
-#pragma unroll
-    for (int off = LPE; off < 64; off <<= 1) c_acc += __shfl_xor(c_acc, off);
-    // loop 2 (same lane <-> (edge, head) map as loop 1): g_raw' and g_s_dst = sum_e g_raw'
-    float gsum = 0.f;
-    if (owner) {
-      for (int e = beg + grp; e < end; e += EPW) {
-        const float ex = att_exp(S[(int64_t)col[e] * S2 + hl] + sdst, M);
-        const float ga = g_raw[(int64_t)e * NH + hl];
-        const float gr = kLeakySlope * ex * (ga - c_acc) * dinv;
-        g_raw[(int64_t)e * NH + hl] = gr;
-        gsum += gr;
-      }
+    if (EPW > 1) {
+      wave_lds_sync();
+      my_dot = dot_lds[lane];
+      wave_lds_sync();
     }
-#pragma unroll
-    for (int off = LPE; off < 64; off <<= 1) gsum += __shfl_xor(gsum, off);
-    if (grp == 0 && owner) G_aug[n * ldg + Dp + NH + hl] = gsum;
-    // wave-level partial of sum g_raw' (for max()'s gradient), fixed order
-    float hs = (grp == 0 && owner) ? gsum : 0.f;
-    for (int off = 1; off < 64; off <<= 1) hs += __shfl_xor(hs, off);
-    wave_part += hs;
+    if (valid) {
+      float ga = my_dot;
+      if (drop) ga = dropout_keep(g.seed, (int64_t)g.perm[e] * NH + h, g.p_drop) ? ga * drop_scale : 0.f;
+      if (g.g_alpha_ret) ga += g.g_alpha_ret[(int64_t)g.perm[e] * NH + h];
+      graw[e] = ga;
+      c_acc += ga * ex * dinv;
+    }
   }
-  if (lane == 0) part_lds[wave] = wave_part;
-  __syncthreads();
-  if (threadIdx.x == 0)
-    partials[blockIdx.x] = (part_lds[0] + part_lds[1]) + (part_lds[2] + part_lds[3]);
+  const float cc = group_sum<64>(c_acc);
+  // sweep 2 (same lane <-> edge map, so each lane re-reads only its own stores)
+  float gsum = 0.f;
+  for (int base = beg; base < end; base += 64) {
+    const int e = base + lane;
+    if (e < end) {
+      const float ex = att_exp(g.S[(int64_t)g.col[e] * S2 + h] + sdst, M);
+      const float gr = kLeakySlope * ex * (graw[e] - cc) * dinv;
+      graw[e] = gr;
+      gsum += gr;
+    }
+  }
+  gsum = group_sum<64>(gsum);
+  if (lane == 0) {
+    g.G_aug[n * g.ldg + Dp + NH + h] = gsum;
+    g.gsd[n * NH + h] = gsum;
+  }
 }
 
-// max() backward: g_M = -sum(g_raw'), split evenly over the k tied argmax entries.
-__global__ void __launch_bounds__(256) max_bwd_kernel(const float* __restrict__ partials,
-                                                      int64_t n_part,
+// max() backward: g_M = -sum_{n,h} g_s_dst[n,h] (two-stage fixed-order reduction of the compact
+// g_s_dst copy), split evenly over the k tied argmax entries recorded by the forward.
+constexpr int kSumBlocks = 1024;
+
+__global__ void __launch_bounds__(256) sum_partial_kernel(const float* __restrict__ x, int64_t n,
+                                                          float* __restrict__ part) {
+  float s = 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    s += x[i];
+  s = group_sum<64>(s);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ void __launch_bounds__(256) max_bwd_kernel(const float* __restrict__ part, int nb,
                                                       const long long* __restrict__ argmax,
                                                       const int32_t* __restrict__ col,
                                                       const int32_t* __restrict__ rowidx, int NH,
@@ -152,8 +246,8 @@ __global__ void __launch_bounds__(256) max_bwd_kernel(const float* __restrict__ 
                                                       int64_t Dp, float* __restrict__ gm_out) {
   __shared__ float red[4];
   float s = 0.f;
-  for (int64_t i = threadIdx.x; i < n_part; i += blockDim.x) s += partials[i];
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) s += part[b];
+  s = group_sum<64>(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
   if (threadIdx.x != 0) return;
@@ -198,73 +292,112 @@ __global__ void __launch_bounds__(256) max_bwd_scan_kernel(const float* __restri
   }
 }
 
+// src pass: one wave per (source s, head h); gathers go rows of the destinations with weights
+// alpha~ = keep * exp(0.01 (s_src[s] + s_dst[d] - M)) / (den[d] + 1e-8) computed lane-parallel
+// per 64-edge batch (the forward's structure with the roles of src and dst swapped).
 template <int LPE, int CPL>
-__global__ void __launch_bounds__(256)
-edge_bwd_src_kernel(const float* __restrict__ S, const uint32_t* __restrict__ M_ord,
-                    const float* __restrict__ den, const int32_t* __restrict__ srowptr,
-                    const int32_t* __restrict__ scol, const int32_t* __restrict__ seid,
-                    const int32_t* __restrict__ perm, int64_t N, int NH, int F, int Fp,
-                    int concat, int const_att, float p_drop, uint64_t seed,
-                    const float* __restrict__ g_out, const float* __restrict__ g_raw,
-                    const float* __restrict__ g_corr_src, float* __restrict__ G_aug,
-                    int64_t ldg) {
+__global__ void __launch_bounds__(256) edge_bwd_src_kernel(BwdArgs g) {
   constexpr int EPW = 64 / LPE;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr int U = CPL <= 1 ? 8 : (CPL <= 2 ? 4 : 2);
+  const int lane = threadIdx.x & 63;
+  const int wave = uni(threadIdx.x >> 6);
   const int grp = lane / LPE, li = lane % LPE;
-  const int D4 = NH * Fp / 4, F4 = Fp / 4, S2 = 2 * NH;
-  const int64_t Dp = (int64_t)NH * Fp;
-  const float M = const_att ? 0.f : ord_to_float(*M_ord);
-  const bool drop = p_drop > 0.f;
-  const float drop_scale = drop ? 1.f / (1.f - p_drop) : 1.f;
-  const float inv_nh = 1.f / (float)NH;
+  const int64_t item = xcd_contiguous(blockIdx.x, gridDim.x) * 4 + wave;
+  if (item >= g.n_items) return;
+  int64_t s;
+  int h;
+  if (!decode_item(item, g.N, g.NH, g.chunk, s, h)) return;
+  const int NH = g.NH, Fp = g.Fp, F4 = Fp / 4, S2 = 2 * NH;
+  const int64_t Dp = (int64_t)NH * Fp, E2 = g.E2;
+  const float M = g.const_att ? 0.f : ord_to_float(*g.M_ord);
+  const bool drop = g.p_drop > 0.f;
+  const float drop_scale = drop ? 1.f / (1.f - g.p_drop) : 1.f;
+  const float4* __restrict__ go4 = (const float4*)g.go;
+  __shared__ int src_sh[4][64];
+  __shared__ float w_sh[4][64];
+  int* src_lds = src_sh[wave];
+  float* w_lds = w_sh[wave];
 
-  int q[CPL], hc[CPL];
+  int off4[CPL];
   bool vq[CPL];
 #pragma unroll
   for (int c = 0; c < CPL; ++c) {
-    q[c] = c * LPE + li;
-    vq[c] = q[c] < D4;
-    hc[c] = vq[c] ? q[c] / F4 : 0;
+    const int q = c * LPE + li;
+    vq[c] = q < F4;
+    off4[c] = h * g.go_head4 + (vq[c] ? q : 0);
   }
+  const float ssrc = g.const_att ? 0.f : g.S[s * S2 + h];
+  float4 acc[CPL];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) acc[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+  float gs = 0.f;
+  const float* __restrict__ graw = g.g_raw ? g.g_raw + (int64_t)h * E2 : nullptr;
 
-  for (int64_t s = blockIdx.x * 4ll + wave; s < N; s += gridDim.x * 4ll) {
-    const int beg = srowptr[s], end = srowptr[s + 1];
-    float ssrc[CPL];
-    float4 acc[CPL];
+  const int beg = uni(g.rowptr[s]), end = uni(g.rowptr[s + 1]);
+  for (int base = beg; base < end; base += 64) {
+    const int cnt = min(64, end - base);
+    const bool valid = lane < cnt;
+    const int j = base + min(lane, cnt - 1);
+    const int d = g.col[j];
+    const int e = g.seid[j];
+    float w = 0.f;
+    if (valid) {
+      const float ex = g.const_att ? 1.f : att_exp(ssrc + g.S[(int64_t)d * S2 + NH + h], M);
+      w = ex / (g.den[(int64_t)d * NH + h] + kSoftmaxEps);
+      if (drop) w = dropout_keep(g.seed, (int64_t)g.perm[e] * NH + h, g.p_drop) ? w * drop_scale : 0.f;
+      if (graw) gs += graw[e];
+    }
+    if (EPW > 1) {
+      src_lds[lane] = d;
+      w_lds[lane] = w;
+      wave_lds_sync();
+    }
+    if constexpr (EPW == 1) {
+      for (int j0 = 0; j0 < cnt; j0 += U) {
+        const float4* rp[U];
+        float wsc[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int jj = min(j0 + u, cnt - 1);
+          rp[u] = go4 + (int64_t)__builtin_amdgcn_readlane(d, jj) * g.go_stride4;
+          wsc[u] = (j0 + u < cnt) ? lane_f(w, jj) : 0.f;
+        }
+        float4 v[U][CPL];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) v[u][c] = rp[u][off4[c]];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) acc[c] = fma4(wsc[u], v[u][c], acc[c]);
+      }
+    } else {
+      for (int j0 = grp; j0 < cnt; j0 += EPW) {
+        const float4* rp = go4 + (int64_t)src_lds[j0] * g.go_stride4;
+        const float wj = w_lds[j0];
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) acc[c] = fma4(wj, rp[off4[c]], acc[c]);
+      }
+      wave_lds_sync();
+    }
+  }
+#pragma unroll
+  for (int off = LPE; off < 64; off <<= 1) {
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) acc[c] = add4(acc[c], shfl_xor4(acc[c], off));
+  }
+  float* row = g.G_aug + s * g.ldg;
+  if (grp == 0) {
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
-      ssrc[c] = const_att ? 0.f : S[s * S2 + hc[c]];
-      acc[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+      const int q = c * LPE + li;
+      if (q < F4) *(float4*)(row + (int64_t)h * Fp + 4 * q) = acc[c];
     }
-    float gs = 0.f;
-    for (int j = beg + grp; j < end; j += EPW) {
-      const int64_t d = scol[j];
-      const int64_t e = seid[j];
-      const int64_t ep = drop ? (int64_t)perm[e] : 0;
-#pragma unroll
-      for (int c = 0; c < CPL; ++c) {
-        if (!vq[c]) continue;
-        const float4 g = load_go(g_out, d, q[c], NH, F, Fp, concat, inv_nh);
-        const float ex = const_att ? 1.f : att_exp(ssrc[c] + S[d * S2 + NH + hc[c]], M);
-        float w = ex / (den[d * NH + hc[c]] + kSoftmaxEps);
-        if (drop) w = dropout_keep(seed, ep * NH + hc[c], p_drop) ? w * drop_scale : 0.f;
-        acc[c] = fma4(w, g, acc[c]);
-      }
-      if (!const_att && li < NH) gs += g_raw[e * NH + li];
-    }
-#pragma unroll
-    for (int off = LPE; off < 64; off <<= 1) {
-#pragma unroll
-      for (int c = 0; c < CPL; ++c) acc[c] = add4(acc[c], shfl_xor4(acc[c], off));
-      gs += __shfl_xor(gs, off);
-    }
-    if (grp == 0) {
-      float* row = G_aug + s * ldg;
-#pragma unroll
-      for (int c = 0; c < CPL; ++c)
-        if (vq[c]) *(float4*)(row + q[c] * 4) = acc[c];
-      if (!const_att && li < NH) row[Dp + li] = gs + g_corr_src[s * NH + li];
-    }
+  }
+  if (!g.const_att) {
+    gs = group_sum<64>(gs);
+    if (lane == 0) row[Dp + h] = gs + g.g_corr[s * NH + h];
   }
 }
 
@@ -313,8 +446,7 @@ __global__ void __launch_bounds__(256) ga_kernel(const float* __restrict__ gW_au
 #pragma unroll
   for (int h = 0; h < 32; ++h) {
     if (h >= 2 * NH) break;
-    float v = acc[h];
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    const float v = group_sum<64>(acc[h]);
     if (lane == 0) {
       const int hh = h < NH ? h : h - NH;
       g_a[(int64_t)hh * 2 * D + k * 2 * F + (h < NH ? 0 : F) + f] = v;
@@ -336,92 +468,101 @@ __global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ X
   if (ty == 0 && j < ncols) out[j] = (red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]);
 }
 
-template <int LPE, int CPL>
-int launch_bwd_dst(unsigned grid, hipStream_t st, const float* Wh, const float* S,
-                   const uint32_t* M_ord, const float* den, const int32_t* rowptr,
-                   const int32_t* col, const int32_t* perm, int64_t N, int NH, int F, int Fp,
-                   int concat, float p, uint64_t seed, const float* g_out, const float* g_alpha,
-                   float* g_raw, float* G_aug, int64_t ldg, float* partials) {
-  edge_bwd_dst_kernel<LPE, CPL><<<grid, 256, 0, st>>>(Wh, S, M_ord, den, rowptr, col, perm, N, NH,
-                                                      F, Fp, concat, p, seed, g_out, g_alpha,
-                                                      g_raw, G_aug, ldg, partials);
-  GATX_LAUNCH_CHECK("edge_bwd_dst");
-  return 0;
+struct Geom {
+  int lpe, cpl;
+};
+// lanes per edge for one head's Fp/4 chunks (power of two <= 64), chunks per lane
+inline Geom head_geom(int F4) {
+  if (F4 >= 64) return {64, (int)ceil_div(F4, 64)};
+  int l = 1;
+  while (l < F4) l <<= 1;
+  return {l, 1};
 }
 
-template <int LPE, int CPL>
-int launch_bwd_src(unsigned grid, hipStream_t st, const float* S, const uint32_t* M_ord,
-                   const float* den, const int32_t* srowptr, const int32_t* scol,
-                   const int32_t* seid, const int32_t* perm, int64_t N, int NH, int F, int Fp,
-                   int concat, int const_att, float p, uint64_t seed, const float* g_out,
-                   const float* g_raw, const float* g_corr, float* G_aug, int64_t ldg) {
-  edge_bwd_src_kernel<LPE, CPL><<<grid, 256, 0, st>>>(S, M_ord, den, srowptr, scol, seid, perm,
-                                                      N, NH, F, Fp, concat, const_att, p, seed,
-                                                      g_out, g_raw, g_corr, G_aug, ldg);
-  GATX_LAUNCH_CHECK("edge_bwd_src");
-  return 0;
-}
-
-constexpr int64_t kDstGridCap = 8192;
+constexpr int64_t kChunk = 2048;
 
 }  // namespace
 }  // namespace gatx
 
 using namespace gatx;
 
-#define GATX_DISPATCH_GEOM(g, MACRO)                                                           \
+#define GATX_DISPATCH_HEAD(gm, KERNEL, grid, args)                                             \
   do {                                                                                         \
-    if ((g).lpe == 64) {                                                                       \
-      switch ((g).cpl) {                                                                       \
-        case 1: MACRO(64, 1); case 2: MACRO(64, 2); case 3: MACRO(64, 3);                      \
-        case 4: MACRO(64, 4); case 5: MACRO(64, 5); case 6: MACRO(64, 6);                      \
-        case 7: MACRO(64, 7); default: MACRO(64, 8);                                           \
+    if ((gm).lpe == 64) {                                                                      \
+      switch ((gm).cpl) {                                                                      \
+        case 1: KERNEL<64, 1><<<grid, 256, 0, st>>>(args); break;                              \
+        case 2: KERNEL<64, 2><<<grid, 256, 0, st>>>(args); break;                              \
+        case 3: KERNEL<64, 3><<<grid, 256, 0, st>>>(args); break;                              \
+        default: KERNEL<64, 4><<<grid, 256, 0, st>>>(args); break;                             \
       }                                                                                        \
-    }                                                                                          \
-    switch ((g).lpe) {                                                                         \
-      case 1: MACRO(1, 1); case 2: MACRO(2, 1); case 4: MACRO(4, 1);                           \
-      case 8: MACRO(8, 1); case 16: MACRO(16, 1); default: MACRO(32, 1);                       \
+    } else {                                                                                   \
+      switch ((gm).lpe) {                                                                      \
+        case 1: KERNEL<1, 1><<<grid, 256, 0, st>>>(args); break;                               \
+        case 2: KERNEL<2, 1><<<grid, 256, 0, st>>>(args); break;                               \
+        case 4: KERNEL<4, 1><<<grid, 256, 0, st>>>(args); break;                               \
+        case 8: KERNEL<8, 1><<<grid, 256, 0, st>>>(args); break;                               \
+        case 16: KERNEL<16, 1><<<grid, 256, 0, st>>>(args); break;                             \
+        default: KERNEL<32, 1><<<grid, 256, 0, st>>>(args); break;                             \
+      }                                                                                        \
     }                                                                                          \
   } while (0)
 
-extern "C" int64_t gatx_edge_backward_dst_partials(int64_t N) {
-  return std::max<int64_t>(1, std::min<int64_t>(ceil_div(N, 4), kDstGridCap));
+extern "C" int gatx_prepare_go(const float* g_out, const float* out, int64_t N, int NH, int F,
+                               int concat, int elu, float* go, float* g_pre, gatx_stream_t s) {
+  if (N == 0) return 0;
+  const int Fp = (int)round_up(F, 4);
+  const int64_t GW = concat ? (int64_t)NH * Fp : Fp;
+  GATX_REQUIRE(!elu || out, "prepare_go: elu needs the forward output");
+  prepare_go_kernel<<<grid_for(N * GW), 256, 0, (hipStream_t)s>>>(g_out, out, N, NH, F, Fp,
+                                                                  concat, elu, go, g_pre);
+  GATX_LAUNCH_CHECK("prepare_go");
+  return 0;
 }
 
 extern "C" int gatx_edge_backward_dst(const float* Wh, const float* S, const uint32_t* M_ord,
                                       const float* den, const int32_t* rowptr,
-                                      const int32_t* col, const int32_t* perm, int64_t N, int NH,
-                                      int F, int concat, float p, uint64_t seed,
-                                      const float* g_out, const float* g_alpha, float* g_raw,
-                                      float* G_aug, int64_t ldg, float* partials,
+                                      const int32_t* col, const int32_t* perm, int64_t N,
+                                      int64_t E2, int NH, int F, int concat, float p,
+                                      uint64_t seed, const float* go, const float* g_alpha,
+                                      float* g_raw, float* gsd, float* G_aug, int64_t ldg,
                                       gatx_stream_t s) {
   hipStream_t st = (hipStream_t)s;
+  if (N == 0) return 0;
   const int Fp = (int)round_up(F, 4);
-  const RowGeom g = row_geom((int64_t)NH * Fp / 4);
-  GATX_REQUIRE(g.cpl <= 8, "edge_backward: num_heads*out_features > 2048 unsupported");
-  GATX_REQUIRE(NH <= 64 && NH <= g.lpe, "edge_backward: num_heads too large");
-  const unsigned grid = (unsigned)gatx_edge_backward_dst_partials(N);
-  if (N == 0) {
-    hipError_t r = hipMemsetAsync(partials, 0, sizeof(float), st);
-    return (int)r;
-  }
-#define GATX_BD(L, C)                                                                          \
-  return launch_bwd_dst<L, C>(grid, st, Wh, S, M_ord, den, rowptr, col, perm, N, NH, F, Fp,    \
-                              concat, p, seed, g_out, g_alpha, g_raw, G_aug, ldg, partials)
-  GATX_DISPATCH_GEOM(g, GATX_BD);
-#undef GATX_BD
+  const Geom gm = head_geom(Fp / 4);
+  GATX_REQUIRE(gm.cpl <= 4, "edge_backward: out_features > 1024 unsupported");
+  BwdArgs a{};
+  a.Wh = Wh; a.go = go;
+  a.go_stride4 = concat ? (int64_t)NH * Fp / 4 : Fp / 4;
+  a.go_head4 = concat ? Fp / 4 : 0;
+  a.S = S; a.M_ord = M_ord; a.den = den; a.rowptr = rowptr; a.col = col; a.perm = perm;
+  a.N = N; a.E2 = E2; a.NH = NH; a.F = F; a.Fp = Fp; a.p_drop = p; a.seed = seed;
+  a.g_alpha_ret = g_alpha; a.g_raw = g_raw; a.gsd = gsd; a.G_aug = G_aug; a.ldg = ldg;
+  a.chunk = kChunk;
+  a.n_items = ceil_div(N, kChunk) * kChunk * NH;
+  const unsigned grid = (unsigned)ceil_div(a.n_items, 4);
+  GATX_DISPATCH_HEAD(gm, edge_bwd_dst_kernel, grid, a);
+  GATX_LAUNCH_CHECK("edge_bwd_dst");
+  return 0;
 }
 
-extern "C" int gatx_max_backward(const float* partials, int64_t n_partials,
-                                 const int64_t* argmax, const float* S, const uint32_t* M_ord,
-                                 const int32_t* col, const int32_t* rowidx, int64_t E2, int NH,
-                                 float* g_corr_src, float* G_aug, int64_t ldg, int64_t Dp,
-                                 gatx_stream_t s) {
+extern "C" size_t gatx_max_backward_workspace_bytes(void) {
+  return sizeof(float) * kSumBlocks;
+}
+
+extern "C" int gatx_max_backward(const int64_t* argmax, const float* gsd, const float* S,
+                                 const uint32_t* M_ord, const int32_t* col, const int32_t* rowidx,
+                                 int64_t N, int64_t E2, int NH, float* g_corr_src, float* G_aug,
+                                 int64_t ldg, int64_t Dp, void* workspace, gatx_stream_t s) {
   hipStream_t st = (hipStream_t)s;
   // the g_M share is parked right after the argmax records (the buffer holds CAP + 2 int64s)
   float* gm = (float*)(argmax + 1 + GATX_ARGMAX_CAP);
-  max_bwd_kernel<<<1, 256, 0, st>>>(partials, n_partials, (const long long*)argmax, col, rowidx,
-                                    NH, g_corr_src, G_aug, ldg, Dp, gm);
+  float* part = (float*)workspace;
+  const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(N * NH, 256), kSumBlocks));
+  sum_partial_kernel<<<nb, 256, 0, st>>>(gsd, N * NH, part);
+  GATX_LAUNCH_CHECK("gsd_sum");
+  max_bwd_kernel<<<1, 256, 0, st>>>(part, nb, (const long long*)argmax, col, rowidx, NH,
+                                    g_corr_src, G_aug, ldg, Dp, gm);
   GATX_LAUNCH_CHECK("max_bwd");
   max_bwd_scan_kernel<<<grid_for(E2 * NH, 256, 4096), 256, 0, st>>>(
       S, M_ord, col, rowidx, E2, NH, (const long long*)argmax, gm, g_corr_src, G_aug, ldg, Dp);
@@ -431,24 +572,31 @@ extern "C" int gatx_max_backward(const float* partials, int64_t n_partials,
 
 extern "C" int gatx_edge_backward_src(const float* S, const uint32_t* M_ord, const float* den,
                                       const int32_t* srowptr, const int32_t* scol,
-                                      const int32_t* seid, const int32_t* perm, int64_t N, int NH,
-                                      int F, int concat, int const_att, float p, uint64_t seed,
-                                      const float* g_out, const float* g_raw,
-                                      const float* g_corr_src, float* G_aug, int64_t ldg,
-                                      gatx_stream_t s) {
+                                      const int32_t* seid, const int32_t* perm, int64_t N,
+                                      int64_t E2, int NH, int F, int concat, int const_att,
+                                      float p, uint64_t seed, const float* go,
+                                      const float* g_raw, const float* g_corr_src, float* G_aug,
+                                      int64_t ldg, gatx_stream_t s) {
   hipStream_t st = (hipStream_t)s;
   if (N == 0) return 0;
   const int Fp = (int)round_up(F, 4);
-  const RowGeom g = row_geom((int64_t)NH * Fp / 4);
-  GATX_REQUIRE(g.cpl <= 8, "edge_backward: num_heads*out_features > 2048 unsupported");
+  const Geom gm = head_geom(Fp / 4);
+  GATX_REQUIRE(gm.cpl <= 4, "edge_backward: out_features > 1024 unsupported");
   GATX_REQUIRE(ldg % 4 == 0, "edge_backward: G_aug row stride must be a multiple of 4");
-  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(N, 4), 65536);
-#define GATX_BS(L, C)                                                                          \
-  return launch_bwd_src<L, C>(grid, st, S, M_ord, den, srowptr, scol, seid, perm, N, NH, F,    \
-                              Fp, concat, const_att, p, seed, g_out, g_raw, g_corr_src, G_aug, \
-                              ldg)
-  GATX_DISPATCH_GEOM(g, GATX_BS);
-#undef GATX_BS
+  BwdArgs a{};
+  a.go = go;
+  a.go_stride4 = concat ? (int64_t)NH * Fp / 4 : Fp / 4;
+  a.go_head4 = concat ? Fp / 4 : 0;
+  a.S = S; a.M_ord = M_ord; a.den = den; a.rowptr = srowptr; a.col = scol; a.seid = seid;
+  a.perm = perm; a.N = N; a.E2 = E2; a.NH = NH; a.F = F; a.Fp = Fp; a.const_att = const_att;
+  a.p_drop = p; a.seed = seed; a.g_raw = const_att ? nullptr : (float*)g_raw;
+  a.g_corr = g_corr_src; a.G_aug = G_aug; a.ldg = ldg;
+  a.chunk = kChunk;
+  a.n_items = ceil_div(N, kChunk) * kChunk * NH;
+  const unsigned grid = (unsigned)ceil_div(a.n_items, 4);
+  GATX_DISPATCH_HEAD(gm, edge_bwd_src_kernel, grid, a);
+  GATX_LAUNCH_CHECK("edge_bwd_src");
+  return 0;
 }
 
 extern "C" int gatx_weight_grads(const float* gW_aug, const float* W, const float* a, int NH,

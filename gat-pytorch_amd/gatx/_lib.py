@@ -58,12 +58,13 @@ SIGNATURES = {
     "gatx_edge_forward": (c_i, [P, P, P, P, P, P, P, c_i64, c_i64, c_i, c_i, c_i, c_i, P, c_f,
                                 c_u64, P, P, P, P, P]),
     "gatx_attention_alpha": (c_i, [P, P, P, c_i64, P, P, P, c_i, c_i, P, P, P]),
-    "gatx_edge_backward_dst_partials": (c_i64, [c_i64]),
-    "gatx_edge_backward_dst": (c_i, [P, P, P, P, P, P, P, c_i64, c_i, c_i, c_i, c_f, c_u64, P, P,
-                                     P, P, c_i64, P, P]),
-    "gatx_max_backward": (c_i, [P, c_i64, P, P, P, P, P, c_i64, c_i, P, P, c_i64, c_i64, P]),
-    "gatx_edge_backward_src": (c_i, [P, P, P, P, P, P, P, c_i64, c_i, c_i, c_i, c_i, c_f, c_u64,
-                                     P, P, P, P, c_i64, P]),
+    "gatx_prepare_go": (c_i, [P, P, c_i64, c_i, c_i, c_i, c_i, P, P, P]),
+    "gatx_edge_backward_dst": (c_i, [P, P, P, P, P, P, P, c_i64, c_i64, c_i, c_i, c_i, c_f, c_u64,
+                                     P, P, P, P, P, c_i64, P]),
+    "gatx_max_backward_workspace_bytes": (c_sz, []),
+    "gatx_max_backward": (c_i, [P, P, P, P, P, P, c_i64, c_i64, c_i, P, P, c_i64, c_i64, P, P]),
+    "gatx_edge_backward_src": (c_i, [P, P, P, P, P, P, P, c_i64, c_i64, c_i, c_i, c_i, c_i, c_f,
+                                     c_u64, P, P, P, P, c_i64, P]),
     "gatx_weight_grads": (c_i, [P, P, P, c_i, c_i, c_i64, P, P, P]),
     "gatx_colsum": (c_i, [P, c_i64, c_i64, c_i64, P, P]),
 }

@@ -147,9 +147,9 @@ def edge_heads_per_item(sh: LayerShape) -> int:
         if sh.NH > 8:
             raise RuntimeError("gatx: head-mean layers support at most 8 heads")
         return sh.NH
-    # ~512 floats of row per item: one XCD's L2 still holds the sweep's slice while each edge
-    # step moves >= 1 KB per wave (measured on PPI layer 1: 2 heads of 256 beat 1 and 4)
-    return max(d for d in range(1, 9) if sh.NH % d == 0 and d * sh.Fp <= max(512, sh.Fp))
+    # ~256+ floats of row per item: one XCD's L2 holds the sweep's slice of the rows (measured
+    # inside the PPI forward: 1 head of 256 per item beats 2 and 4)
+    return max(d for d in range(1, 9) if sh.NH % d == 0 and d * sh.Fp <= max(256, sh.Fp))
 
 
 def fold_scores_into_gemm(sh: LayerShape) -> bool:
@@ -250,46 +250,52 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
 
 
 def layer_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShape, p: float,
-                   seed: int, saved, need_x: bool, need_W: bool, need_a: bool, need_bias: bool):
+                   seed: int, saved, need_x: bool, need_W: bool, need_a: bool, need_bias: bool,
+                   out=None, elu=False, need_resid=False):
+    """Gradients of layer_forward; returns (g_x, g_W, g_a, g_bias, g_resid)."""
     N = x.size(0)
     dev = x.device
     s = stream()
+    f32 = dict(dtype=torch.float32, device=dev)
     g_out = g_out.contiguous()
     E2 = graph.num_edges
     graph.ensure_transpose()
     if saved["Wh"] is None:   # reassociated forward never built Wh: project now
-        Wh = torch.empty((N, sh.Dp), dtype=torch.float32, device=dev)
+        Wh = torch.empty((N, sh.Dp), **f32)
         call("gatx_gemm_f32", N, sh.Dp, sh.F_in, ptr(x), sh.F_in, 1, ptr(saved["W_aug"]), 1,
              sh.F_in, ptr(Wh), sh.Dp, sh.Dp, None, 0, 0, s)
         saved["Wh"] = Wh
-    G_aug = torch.empty((N, sh.ldg), dtype=torch.float32, device=dev)
+    go = torch.empty((N, sh.Dp if sh.concat else sh.Fp), **f32)
+    g_pre = torch.empty((N, sh.out_cols), **f32) if (need_resid or (need_bias and elu)) else None
+    call("gatx_prepare_go", ptr(g_out), ptr(out) if elu else None, N, sh.NH, sh.F,
+         int(sh.concat), int(elu), ptr(go), ptr(g_pre), s)
+    G_aug = torch.empty((N, sh.ldg), **f32)
+    g_raw = g_corr = None
     if not sh.const:
-        g_raw = torch.empty((max(E2, 1), sh.NH), dtype=torch.float32, device=dev)
-        n_part = lib.gatx_edge_backward_dst_partials(N)
-        partials = torch.empty(n_part, dtype=torch.float32, device=dev)
+        g_raw = torch.empty((sh.NH, max(E2, 1)), **f32)
+        gsd = torch.empty((N, sh.NH), **f32)
         call("gatx_edge_backward_dst", ptr(saved["Wh"]), ptr(saved["S"]), ptr(saved["M_ord"]),
-             ptr(saved["den"]), ptr(graph.rowptr), ptr(graph.col), ptr(graph.perm), N, sh.NH,
-             sh.F, int(sh.concat), float(p), seed, ptr(g_out),
-             ptr(g_alpha.contiguous()) if g_alpha is not None else None, ptr(g_raw), ptr(G_aug),
-             sh.ldg, ptr(partials), s)
-        g_corr = torch.zeros((N, sh.NH), dtype=torch.float32, device=dev)
-        call("gatx_max_backward", ptr(partials), n_part, ptr(saved["argmax"]), ptr(saved["S"]),
-             ptr(saved["M_ord"]), ptr(graph.col), ptr(graph.rowidx), E2, sh.NH, ptr(g_corr),
-             ptr(G_aug), sh.ldg, sh.Dp, s)
-    else:
-        g_raw = g_corr = None
+             ptr(saved["den"]), ptr(graph.rowptr), ptr(graph.col), ptr(graph.perm), N, E2,
+             sh.NH, sh.F, int(sh.concat), float(p), seed, ptr(go),
+             ptr(g_alpha.contiguous()) if g_alpha is not None else None, ptr(g_raw), ptr(gsd),
+             ptr(G_aug), sh.ldg, s)
+        g_corr = torch.zeros((N, sh.NH), **f32)
+        mws = torch.empty(lib.gatx_max_backward_workspace_bytes(), dtype=torch.uint8, device=dev)
+        call("gatx_max_backward", ptr(saved["argmax"]), ptr(gsd), ptr(saved["S"]),
+             ptr(saved["M_ord"]), ptr(graph.col), ptr(graph.rowidx), N, E2, sh.NH, ptr(g_corr),
+             ptr(G_aug), sh.ldg, sh.Dp, ptr(mws), s)
     call("gatx_edge_backward_src", ptr(saved["S"]), ptr(saved["M_ord"]), ptr(saved["den"]),
-         ptr(graph.srowptr), ptr(graph.scol), ptr(graph.seid), ptr(graph.perm), N, sh.NH, sh.F,
-         int(sh.concat), int(sh.const), float(p), seed, ptr(g_out), ptr(g_raw), ptr(g_corr),
+         ptr(graph.srowptr), ptr(graph.scol), ptr(graph.seid), ptr(graph.perm), N, E2, sh.NH,
+         sh.F, int(sh.concat), int(sh.const), float(p), seed, ptr(go), ptr(g_raw), ptr(g_corr),
          ptr(G_aug), sh.ldg, s)
     g_x = g_W = g_a = g_bias = None
     W_aug = saved["W_aug"]
     if need_x:
-        g_x = torch.empty((N, sh.F_in), dtype=torch.float32, device=dev)
+        g_x = torch.empty((N, sh.F_in), **f32)
         call("gatx_gemm_f32", N, sh.F_in, sh.K_aug, ptr(G_aug), sh.ldg, 1, ptr(W_aug), sh.F_in, 1,
              ptr(g_x), sh.F_in, sh.F_in, None, 0, 0, s)
     if need_W or need_a:
-        gW_aug = torch.empty((sh.K_aug, sh.F_in), dtype=torch.float32, device=dev)
+        gW_aug = torch.empty((sh.K_aug, sh.F_in), **f32)
         ws_bytes = lib.gatx_gemm_splitk_workspace_bytes(sh.K_aug, sh.F_in, N)
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
         call("gatx_gemm_f32_splitk", sh.K_aug, sh.F_in, N, ptr(G_aug), 1, sh.ldg, ptr(x),
@@ -300,10 +306,12 @@ def layer_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShape, 
              ptr(g_a), s)
     if need_bias and bias is not None:
         g_bias = torch.empty_like(bias)
-        call("gatx_colsum", ptr(g_out), N, sh.out_cols, sh.out_cols, ptr(g_bias), s)
-        if not sh.concat and bias.numel() != sh.out_cols:
-            raise RuntimeError("bias with head-mean needs num_heads == 1")
-    return g_x, (g_W if need_W else None), (g_a if need_a else None), g_bias
+        src = g_pre if elu else g_out
+        call("gatx_colsum", ptr(src), N, sh.out_cols, sh.out_cols, ptr(g_bias), s)
+    g_resid = None
+    if need_resid:
+        g_resid = g_pre
+    return (g_x, (g_W if need_W else None), (g_a if need_a else None), g_bias, g_resid)
 
 
 class GATLayerFunction(torch.autograd.Function):
@@ -321,13 +329,11 @@ class GATLayerFunction(torch.autograd.Function):
         if g_out is None:
             g_out = torch.zeros((x.size(0), ctx.sh.out_cols), dtype=torch.float32,
                                 device=x.device)
-        if ctx.elu:   # d elu(v) = 1 (v > 0) else elu(v) + 1, from the saved post-ELU output
-            g_out = g_out * torch.where(out > 0, torch.ones_like(out), out + 1.0)
-        g_resid = g_out if (ctx.has_resid and ctx.needs_input_grad[4]) else None
-        nx, nW, na, nb = ctx.needs_input_grad[:4]
-        g_x, g_W, g_a, g_b = layer_backward(g_out, g_alpha, x, W, a, bias, ctx.graph, ctx.sh,
-                                            ctx.p, ctx.seed, ctx.saved, nx, nW, na, nb)
-        return g_x, g_W, g_a, g_b, g_resid, None, None, None, None, None
+        nx, nW, na, nb, nr = ctx.needs_input_grad[:5]
+        g_x, g_W, g_a, g_b, g_r = layer_backward(
+            g_out, g_alpha, x, W, a, bias, ctx.graph, ctx.sh, ctx.p, ctx.seed, ctx.saved, nx, nW,
+            na, nb, out=out, elu=ctx.elu, need_resid=bool(ctx.has_resid and nr))
+        return g_x, g_W, g_a, g_b, g_r, None, None, None, None, None
 
 
 def gat_layer(x, edge_index, W, a, bias, num_heads, out_features, concat, add_self_loops,

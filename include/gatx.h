@@ -183,36 +183,43 @@ int gatx_pad_rows(const float* src, int64_t rows, int64_t cols, int64_t ld_src, 
 
 /* ---------------------------------------------------------------- backward (autograd of above) */
 
-/* Destination pass. go = g_out (concat [N][NH*F]; mean [N][F], scaled by 1/NH inside).
- *   g_alpha~[e,h] = <go[dst,h,:], Wh[src,h,:]>; g_alpha = g_alpha~ * keep/(1-p) + g_alpha_ret
+/* go [N][NH*Fp] (concat) or [N][Fp] (head mean, scaled by 1/NH): the upstream gradient, gated by
+ * elu'(out) when the layer's epilogue applied ELU (out = the saved post-ELU output), zero-padded
+ * per head. g_pre (nullable) receives the unpadded elu-gated gradient (the residual's gradient). */
+int gatx_prepare_go(const float* g_out, const float* out, int64_t num_nodes, int NH, int F,
+                    int concat, int elu, float* go, float* g_pre, gatx_stream_t stream);
+
+/* Destination pass, one wave per (node n, head h):
+ *   g_alpha~[e,h] = <go[n,h,:], Wh[src,h,:]>; g_alpha = g_alpha~ * keep/(1-p) + g_alpha_ret
  *   c[n,h] = sum_{e->n} g_alpha * alpha; g_raw'[e,h] = 0.01 * ex * (g_alpha - c) / (den + 1e-8)
- * Writes g_raw' [E2][NH] in CSR order, g_s_dst into G_aug[n][Dp+NH+h] and one partial sum of
- * g_raw' per workgroup into partials [gatx_edge_backward_dst_partials(num_nodes)].
- * g_alpha_ret (the returned alpha's gradient, edge_index' order) may be NULL. */
-int64_t gatx_edge_backward_dst_partials(int64_t num_nodes);
+ * Writes g_raw' head-major [NH][E2] in CSR order and g_s_dst = sum_e g_raw' into
+ * G_aug[n][Dp+NH+h] and gsd [N][NH]. g_alpha_ret (the returned alpha's gradient, edge_index'
+ * order) may be NULL. */
 int gatx_edge_backward_dst(const float* Wh, const float* S, const uint32_t* M_ord,
                            const float* den, const int32_t* rowptr, const int32_t* col,
-                           const int32_t* perm, int64_t num_nodes, int NH, int F, int concat,
-                           float dropout_p, uint64_t seed, const float* g_out,
-                           const float* g_alpha_ret, float* g_raw, float* G_aug, int64_t ldg,
-                           float* partials, gatx_stream_t stream);
+                           const int32_t* perm, int64_t num_nodes, int64_t E2, int NH, int F,
+                           int concat, float dropout_p, uint64_t seed, const float* go,
+                           const float* g_alpha_ret, float* g_raw, float* gsd, float* G_aug,
+                           int64_t ldg, gatx_stream_t stream);
 
-/* max() backward (torch splits the gradient evenly over ties): g_M = -sum(partials);
- * g_corr_src[src,h] += g_M/k and G_aug[dst][Dp+NH+h] += g_M/k for each recorded argmax entry.
- * g_corr_src [N][NH] must be zeroed by the caller. Falls back to a full scan of the edges when
- * more than GATX_ARGMAX_CAP entries tie. */
-int gatx_max_backward(const float* partials, int64_t n_partials, const int64_t* argmax,
-                      const float* S, const uint32_t* M_ord, const int32_t* col,
-                      const int32_t* rowidx, int64_t E2, int NH, float* g_corr_src, float* G_aug,
-                      int64_t ldg, int64_t Dp, gatx_stream_t stream);
+/* max() backward (torch splits the gradient evenly over ties): g_M = -sum gsd (two-stage
+ * fixed-order reduction); g_corr_src[src,h] += g_M/k and G_aug[dst][Dp+NH+h] += g_M/k for each
+ * recorded argmax entry. g_corr_src [N][NH] must be zeroed by the caller. Falls back to a full
+ * scan of the edges when more than GATX_ARGMAX_CAP entries tie. */
+size_t gatx_max_backward_workspace_bytes(void);
+int gatx_max_backward(const int64_t* argmax, const float* gsd, const float* S,
+                      const uint32_t* M_ord, const int32_t* col, const int32_t* rowidx,
+                      int64_t num_nodes, int64_t E2, int NH, float* g_corr_src, float* G_aug,
+                      int64_t ldg, int64_t Dp, void* workspace, gatx_stream_t stream);
 
-/* Source pass: G_aug[s][0:Dp] = sum_{e: src=s} alpha~[e,h] * go[dst_e,h,:] (the message
- * gradient), G_aug[s][Dp+h] = sum_{e: src=s} g_raw'[e,h] + g_corr_src[s,h] (g_s_src). */
+/* Source pass, one wave per (node s, head h): G_aug[s][h*Fp:] = sum_{e: src=s} alpha~[e,h] *
+ * go[dst_e,h,:] (the message gradient), G_aug[s][Dp+h] = sum_{e: src=s} g_raw'[e,h] +
+ * g_corr_src[s,h] (g_s_src; skipped for const_attention). */
 int gatx_edge_backward_src(const float* S, const uint32_t* M_ord, const float* den,
                            const int32_t* srowptr, const int32_t* scol, const int32_t* seid,
-                           const int32_t* perm, int64_t num_nodes, int NH, int F, int concat,
-                           int const_attention, float dropout_p, uint64_t seed,
-                           const float* g_out, const float* g_raw, const float* g_corr_src,
+                           const int32_t* perm, int64_t num_nodes, int64_t E2, int NH, int F,
+                           int concat, int const_attention, float dropout_p, uint64_t seed,
+                           const float* go, const float* g_raw, const float* g_corr_src,
                            float* G_aug, int64_t ldg, gatx_stream_t stream);
 
 /* From g_W_aug [(Dp+2NH) x F_in] (= G_aug^T x): g_W [NH*F x F_in] and g_a [NH x NH*2F]
