@@ -30,30 +30,6 @@ __device__ inline int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ inline float lane_f(float v, int j) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
 }
-template <int CTRL>
-__device__ inline float dpp(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
-}
-// Sum over aligned groups of L lanes (L = 1..64); every lane of a group gets the group's total.
-// xor 1/2 via quad_perm, 4/8 via row half-mirror / mirror (valid once the smaller groups agree),
-// 16/32 via the gfx950 permlane swaps (r[0] + r[1] = own + partner).
-template <int L>
-__device__ inline float group_sum(float v) {
-  if (L >= 2) v += dpp<0xB1>(v);
-  if (L >= 4) v += dpp<0x4E>(v);
-  if (L >= 8) v += dpp<0x141>(v);
-  if (L >= 16) v += dpp<0x140>(v);
-  if (L >= 32) {
-    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-  }
-  if (L >= 64) {
-    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-  }
-  return v;
-}
-
 __device__ inline int64_t xcd_contiguous(int64_t b, int64_t nb) {
   const int64_t q = nb / 8, r = nb % 8, xcd = b % 8, j = b / 8;
   return (xcd < r) ? xcd * (q + 1) + j : r * (q + 1) + (xcd - r) * q + j;

@@ -430,6 +430,64 @@ __global__ void __launch_bounds__(256) node_scores_kernel(const float* __restric
   }
 }
 
+// S from Wh rows with the attention matrix held in registers: one wave per row, lane l owns
+// float4 columns q = l + 64c (c < CPL) and the matching slice of every one of the H (= 2NH
+// rounded up to a power of two) rows of A2 [2NH][Dp] (a rearranged per column of Wh). The next
+// row's loads are issued before the current row's reduce-scatter (reduce_scatter64).
+template <int CPL, int H>
+__global__ void __launch_bounds__(256) node_scores_reg_kernel(const float* __restrict__ Wh,
+                                                              int64_t N, int NH, int F, int Fp,
+                                                              const float* __restrict__ a,
+                                                              float* __restrict__ S) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave0 = blockIdx.x * 4ll + (threadIdx.x >> 6), nw = gridDim.x * 4ll;
+  const int Dp = NH * Fp, D4 = Dp / 4, D = NH * F, H2 = 2 * NH;
+  float4 w[CPL][H];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int q = lane + 64 * c;
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      float e[4] = {0.f, 0.f, 0.f, 0.f};
+      if (q < D4 && h < H2) {
+        const int hh = h < NH ? h : h - NH;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int col = 4 * q + j, k = col / Fp, f = col - k * Fp;
+          if (f < F) e[j] = a[(int64_t)hh * 2 * D + k * 2 * F + (h < NH ? 0 : F) + f];
+        }
+      }
+      w[c][h] = make_float4(e[0], e[1], e[2], e[3]);
+    }
+  }
+  const float4* __restrict__ W4 = (const float4*)Wh;
+  float4 cur[CPL];
+  auto load = [&](int64_t n, float4 (&v)[CPL]) {
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const int q = lane + 64 * c;
+      v[c] = (n < N && q < D4) ? W4[n * D4 + q] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  load(wave0, cur);
+  for (int64_t n = wave0; n < N; n += nw) {
+    float acc[H];
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      float t = 0.f;
+#pragma unroll
+      for (int c = 0; c < CPL; ++c)
+        t += cur[c].x * w[c][h].x + cur[c].y * w[c][h].y + cur[c].z * w[c][h].z +
+             cur[c].w * w[c][h].w;
+      acc[h] = t;
+    }
+    load(n + nw, cur);
+    int h;
+    const float tot = reduce_scatter64<H>(acc, lane, h);
+    if ((lane & (64 / H - 1)) == 0 && h < H2) S[n * H2 + h] = tot;
+  }
+}
+
 // alpha in edge_index' order (pre-dropout, as the reference returns and stores it,
 // models/gat_layer.py:109-110): alpha[e', h] = ex / (den[dst] + 1e-8), one thread per CSR slot,
 // all heads of an edge written together (one random 4*NH-byte store per edge instead of NH
@@ -565,11 +623,29 @@ extern "C" int gatx_node_scores(const float* Wh, int64_t N, int NH, int F, const
                                 float* S, gatx_stream_t s) {
   const int Fp = (int)round_up(F, 4);
   GATX_REQUIRE(2 * NH <= kMaxH2, "node_scores: num_heads > %d unsupported", kMaxH2 / 2);
+  if (N == 0) return 0;
+  hipStream_t st = (hipStream_t)s;
+  const int cpl = (int)ceil_div((int64_t)NH * Fp / 4, 64);
+  int H = 2;
+  while (H < 2 * NH) H *= 2;
+  if (cpl <= 4 && cpl * H <= 32) {
+    const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(N, 4), 512);
+#define GATX_NS(C, HH)                                                                         \
+  if (cpl == C && H == HH) {                                                                   \
+    node_scores_reg_kernel<C, HH><<<grid, 256, 0, st>>>(Wh, N, NH, F, Fp, a, S);               \
+    GATX_LAUNCH_CHECK("node_scores");                                                          \
+    return 0;                                                                                  \
+  }
+    GATX_NS(1, 2) GATX_NS(1, 4) GATX_NS(1, 8) GATX_NS(1, 16) GATX_NS(1, 32)
+    GATX_NS(2, 2) GATX_NS(2, 4) GATX_NS(2, 8) GATX_NS(2, 16)
+    GATX_NS(3, 2) GATX_NS(3, 4) GATX_NS(3, 8)
+    GATX_NS(4, 2) GATX_NS(4, 4) GATX_NS(4, 8)
+#undef GATX_NS
+  }
   const size_t lds = (size_t)2 * NH * NH * Fp * sizeof(float);
   GATX_REQUIRE(lds <= 64 * 1024, "node_scores: attention vector too large for LDS");
-  if (N == 0) return 0;
-  node_scores_kernel<<<(unsigned)std::min<int64_t>(ceil_div(N, 4), 1024), 256, lds,
-                       (hipStream_t)s>>>(Wh, N, NH, F, Fp, a, S);
+  node_scores_kernel<<<(unsigned)std::min<int64_t>(ceil_div(N, 4), 1024), 256, lds, st>>>(
+      Wh, N, NH, F, Fp, a, S);
   GATX_LAUNCH_CHECK("node_scores");
   return 0;
 }

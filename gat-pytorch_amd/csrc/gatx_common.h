@@ -104,4 +104,83 @@ inline RowGeom row_geom(int64_t D4) {
   return {l, 1};
 }
 
+template <int CTRL>
+__device__ inline float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+// Sum over aligned groups of L lanes (L = 1..64); every lane of a group gets the group's total.
+// xor 1/2 via quad_perm, 4/8 via row half-mirror / mirror (valid once the smaller groups agree),
+// 16/32 via the gfx950 permlane swaps (r[0] + r[1] = own + partner).
+template <int L>
+__device__ inline float group_sum(float v) {
+  if (L >= 2) v += dpp<0xB1>(v);
+  if (L >= 4) v += dpp<0x4E>(v);
+  if (L >= 8) v += dpp<0x141>(v);
+  if (L >= 16) v += dpp<0x140>(v);
+  if (L >= 32) {
+    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  if (L >= 64) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  return v;
+}
+
+// Reduce-scatter of H values (H a power of two <= 64) over the 64 lanes: returns, in every
+// lane, the wave-wide sum of v[h] for h = h_of_lane (h = the top log2(H) lane bits read as
+// 32->H/2, 16->H/4, ...; lanes sharing those bits hold the same total). log2(H) exchange steps
+// (each halves the values a lane keeps) + 6 - log2(H) plain butterfly steps: H/2 + ... + 1
+// cross-lane moves plus the plain ones, instead of 6 per value. Partners at each level differ
+// exactly in that level's lane bit (permlane swaps for 32/16, mirrors for 8/4, quad perms).
+template <int H>
+__device__ inline float reduce_scatter64(float (&v)[H], int lane, int& h) {
+  int cnt = H;
+  h = 0;
+#pragma unroll
+  for (int lev = 0; lev < 6; ++lev) {
+    const int bit = 5 - lev;
+    const bool up = (lane >> bit) & 1;
+    if (cnt > 1) {
+      const int half = cnt / 2;
+#pragma unroll
+      for (int j = 0; j < half; ++j) {
+        const float x0 = v[j], x1 = v[half + j];
+        if (lev < 2) {
+          auto r = lev == 0 ? __builtin_amdgcn_permlane32_swap(__float_as_uint(x0),
+                                                               __float_as_uint(x1), false, false)
+                            : __builtin_amdgcn_permlane16_swap(__float_as_uint(x0),
+                                                               __float_as_uint(x1), false, false);
+          v[j] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+        } else {
+          const float send = up ? x0 : x1;
+          float recv;
+          if (lev == 2) recv = dpp<0x140>(send);
+          else if (lev == 3) recv = dpp<0x141>(send);
+          else if (lev == 4) recv = dpp<0x4E>(send);
+          else recv = dpp<0xB1>(send);
+          v[j] = (up ? x1 : x0) + recv;
+        }
+      }
+      if (up) h += half;
+      cnt = half;
+    } else {
+      float x = v[0];
+      if (lev < 2) {
+        auto r = lev == 0 ? __builtin_amdgcn_permlane32_swap(__float_as_uint(x),
+                                                             __float_as_uint(x), false, false)
+                          : __builtin_amdgcn_permlane16_swap(__float_as_uint(x),
+                                                             __float_as_uint(x), false, false);
+        x = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+      } else if (lev == 2) x += dpp<0x140>(x);
+      else if (lev == 3) x += dpp<0x141>(x);
+      else if (lev == 4) x += dpp<0x4E>(x);
+      else x += dpp<0xB1>(x);
+      v[0] = x;
+    }
+  }
+  return v[0];
+}
+
 }  // namespace gatx

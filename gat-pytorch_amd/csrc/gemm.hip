@@ -6,11 +6,17 @@
 // also produces the per-node logit factors s_src / s_dst that stand in for the per-edge
 // (E, NH*2F) x a^T GEMV of :76-82 — and the two backward products g_x and g_W.
 //
-// Tile: 128 x 128 x 16 per 256-thread workgroup, 4 waves as 2 x 2, each wave 64 x 64 = 2 x 2
-// MFMA blocks of 32 x 32 (16 accumulators each). Operands are staged global -> registers ->
-// LDS ([k][m] and [k][n] images, so each MFMA operand read is 32 consecutive floats per lane
-// half: conflict-free ds_read_b32); the next K-tile's global loads are issued before the
-// current tile's MFMAs so their latency hides under 32 MFMAs per wave.
+// Tile 128 x 128 x 16 per 256-thread workgroup, 4 waves as 2 x 2, each wave 64 x 64 = 2 x 2 MFMA
+// blocks of 32 x 32. Two LDS stages (one barrier per K-tile): tile kt+1 is fetched into
+// registers before tile kt's MFMAs and stored into the other stage after them. An operand whose
+// K index is contiguous in memory is staged as a [row][k] image (float4 copies, 36-float rows:
+// conflict-free ds_read_b128); a row-contiguous one as a [k][row] image. Within each group of 8
+// k, lane half h feeds k = 8g + 4h + j to MFMA step j, so one 16-byte read gives a lane its
+// operands for 4 MFMAs; the next group's fragments are read while the current group's MFMAs run.
+// Occupancy 4 workgroups per CU (40 KB LDS, <= 128 VGPRs each); the last partial wave of tiles
+// can be split along K (tail split) so it does not leave most of the chip idle. A barrier-free
+// variant streaming each wave's fragments from L1/L2 into registers (no LDS) reached only 74 TF
+// on the same shapes (TA-bound), so operands are shared through LDS.
 #include "gatx_common.h"
 
 namespace gatx {
@@ -18,68 +24,71 @@ namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
-constexpr int BK = 32, PAD = 4;
+constexpr int BM = 128, BN = 128, THREADS = 256;
+constexpr int KSTEP = 32;   // split-K / tail slice granularity
 
-// Stage a (ROWS x BK) tile whose K index is contiguous in memory into img[k][row] (transposed).
-// THREADS threads, EPT = ROWS*BK/THREADS consecutive k per thread.
-template <int ROWS, int THREADS>
-struct KContig {
-  static constexpr int EPT = ROWS * BK / THREADS, TPR = BK / EPT, LD = ROWS + PAD;
+// One operand tile of ROWS rows x BK k. KC: k-contiguous in memory (row stride ld).
+template <bool KC, int ROWS, int BK>
+struct Tile {
+  static constexpr int LD = KC ? BK + 4 : ROWS + 4;
+  static constexpr int SIZE = KC ? ROWS * LD : BK * LD;   // floats per stage
+  static constexpr int NV = ROWS * BK / 4 / THREADS;      // float4 per thread
+  // VEC (16-byte aligned rows, ld % 4 == 0): every thread issues NV float4 loads from clamped
+  // in-bounds addresses and zeroes the components outside the matrix; otherwise scalar loads.
+  template <bool VEC>
   static __device__ inline void load(const float* __restrict__ P, int64_t ld, int64_t r0,
-                                     int64_t rmax, int64_t k0, int64_t K, bool vec,
-                                     float (&v)[EPT]) {
-    const int t = threadIdx.x;
-    const int64_t r = r0 + t / TPR;
-    const int64_t k = k0 + (t % TPR) * EPT;
-    const float* p = P + r * ld + k;
-    if (r < rmax && vec && k + EPT <= K) {
+                                     int64_t rmax, int64_t k0, int64_t kmax, float4 (&v)[NV]) {
 #pragma unroll
-      for (int j = 0; j < EPT / 4; ++j) {
-        const float4 a = *(const float4*)(p + 4 * j);
-        v[4 * j] = a.x; v[4 * j + 1] = a.y; v[4 * j + 2] = a.z; v[4 * j + 3] = a.w;
+    for (int c = 0; c < NV; ++c) {
+      const int idx = threadIdx.x + THREADS * c;
+      int64_t r, k;
+      if (KC) { r = r0 + idx / (BK / 4); k = k0 + 4 * (idx % (BK / 4)); }
+      else { k = k0 + idx / (ROWS / 4); r = r0 + 4 * (idx % (ROWS / 4)); }
+      if (VEC) {
+        // KC: lanes j run along k (valid while k + j < kmax); RC: along rows
+        const bool rok = r < rmax, kok = k < kmax;
+        const int64_t rc = rok ? r : (KC ? rmax - 1 : 0);
+        const int64_t kc = kok ? k : (KC ? 0 : kmax - 1);
+        v[c] = *(const float4*)(KC ? P + rc * ld + kc : P + kc * ld + rc);   // masked in store
+      } else {
+        float e[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const bool ok = KC ? (r < rmax && k + j < kmax) : (k < kmax && r + j < rmax);
+          e[j] = ok ? (KC ? P[r * ld + k + j] : P[k * ld + r + j]) : 0.f;
+        }
+        v[c] = make_float4(e[0], e[1], e[2], e[3]);
       }
-    } else {
-#pragma unroll
-      for (int j = 0; j < EPT; ++j) v[j] = (r < rmax && k + j < K) ? p[j] : 0.f;
     }
   }
-  static __device__ inline void store(float* img, const float (&v)[EPT]) {
-    const int t = threadIdx.x;
-    const int r = t / TPR, kb = (t % TPR) * EPT;
+  // Components outside the matrix are zeroed here, after the MFMAs of the current tile, so the
+  // loads' latency stays hidden (a select right after the load would wait for it).
+  template <bool VEC>
+  static __device__ inline void store(float* img, float4 (&v)[NV], int64_t r0, int64_t rmax,
+                                      int64_t k0, int64_t kmax) {
 #pragma unroll
-    for (int j = 0; j < EPT; ++j) img[(kb + j) * LD + r] = v[j];
-  }
-};
-
-// Stage a tile whose row (M or N) index is contiguous straight into img[k][row].
-template <int ROWS, int THREADS>
-struct RContig {
-  static constexpr int EPT = ROWS * BK / THREADS, TPK = ROWS / EPT, LD = ROWS + PAD;
-  static __device__ inline void load(const float* __restrict__ P, int64_t ld, int64_t r0,
-                                     int64_t rmax, int64_t k0, int64_t K, bool vec,
-                                     float (&v)[EPT]) {
-    const int t = threadIdx.x;
-    const int64_t k = k0 + t / TPK;
-    const int64_t r = r0 + (t % TPK) * EPT;
-    const float* p = P + k * ld + r;
-    if (k < K && vec && r + EPT <= rmax) {
-#pragma unroll
-      for (int j = 0; j < EPT / 4; ++j) {
-        const float4 a = *(const float4*)(p + 4 * j);
-        v[4 * j] = a.x; v[4 * j + 1] = a.y; v[4 * j + 2] = a.z; v[4 * j + 3] = a.w;
+    for (int c = 0; c < NV; ++c) {
+      const int idx = threadIdx.x + THREADS * c;
+      const int row = KC ? idx / (BK / 4) : 4 * (idx % (ROWS / 4));
+      const int kk = KC ? 4 * (idx % (BK / 4)) : idx / (ROWS / 4);
+      if (VEC) {
+        const int64_t r = r0 + row, k = k0 + kk;
+        const bool ok = r < rmax && k < kmax;
+        const int64_t lim = KC ? kmax - k : rmax - r;
+        v[c].x = ok ? v[c].x : 0.f;
+        v[c].y = ok && lim > 1 ? v[c].y : 0.f;
+        v[c].z = ok && lim > 2 ? v[c].z : 0.f;
+        v[c].w = ok && lim > 3 ? v[c].w : 0.f;
       }
-    } else {
-#pragma unroll
-      for (int j = 0; j < EPT; ++j) v[j] = (k < K && r + j < rmax) ? p[j] : 0.f;
+      const int off = KC ? row * LD + kk : kk * LD + row;
+      *(float4*)&img[off] = v[c];
     }
   }
-  static __device__ inline void store(float* img, const float (&v)[EPT]) {
-    const int t = threadIdx.x;
-    const int k = t / TPK, r = (t % TPK) * EPT;
-#pragma unroll
-    for (int j = 0; j < EPT / 4; ++j)
-      *(float4*)&img[k * LD + r + 4 * j] = make_float4(v[4 * j], v[4 * j + 1], v[4 * j + 2],
-                                                        v[4 * j + 3]);
+  // k = kb .. kb+3 of row `row`
+  static __device__ inline float4 frag(const float* img, int row, int kb) {
+    if (KC) return *(const float4*)&img[row * LD + kb];
+    return make_float4(img[kb * LD + row], img[(kb + 1) * LD + row], img[(kb + 2) * LD + row],
+                       img[(kb + 3) * LD + row]);
   }
 };
 
@@ -97,7 +106,27 @@ struct GemmArgs {
   const float* resid; int64_t resid_ld, resid_bs;
   int elu;
   int64_t k_per_split; int splits; float* partial;
+  // tail split (splits == 1): blocks >= dp_blocks each take K-slice z of one of the last
+  // tail_rem tiles and write a BM x BN partial; tail_fixup_kernel sums the slices in z order
+  int64_t dp_blocks, tail_rem; int tail_s, bm; float* tail_partial;
 };
+
+// C = elu?(v (+C) + bias + resid) for one output element (columns >= n_split go to C1 raw)
+__device__ inline void store_out(const GemmArgs& g, int64_t b, int64_t row, int64_t col, float v) {
+  float* Cb;
+  int64_t ldc, c;
+  const bool first = col < g.n_split;
+  if (first) { Cb = g.C0 + b * g.c0_bs; ldc = g.ldc0; c = col; }
+  else { Cb = g.C1 + b * g.c1_bs; ldc = g.ldc1; c = col - g.n_split; }
+  float* p = Cb + row * ldc + c;
+  if (g.accumulate) v += *p;
+  if (first) {
+    if (g.bias) v += g.bias[b * g.bias_bs + c];
+    if (g.resid) v += g.resid[b * g.resid_bs + row * g.resid_ld + c];
+    if (g.elu) v = v > 0.f ? v : expm1f(v);
+  }
+  *p = v;
+}
 
 // Deterministic split-K combine: C = epilogue(sum over slabs in slab order), one pass.
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(GemmArgs g, int batch) {
@@ -107,19 +136,22 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(GemmArgs g, int batc
     const int64_t b = t / MN, mn = t - b * MN, row = mn / g.N, col = mn - row * g.N;
     float v = 0.f;
     for (int z = 0; z < g.splits; ++z) v += g.partial[((int64_t)z * batch + b) * MN + mn];
-    float* Cb;
-    int64_t ldc, c;
-    const bool first = col < g.n_split;
-    if (first) { Cb = g.C0 + b * g.c0_bs; ldc = g.ldc0; c = col; }
-    else { Cb = g.C1 + b * g.c1_bs; ldc = g.ldc1; c = col - g.n_split; }
-    float* p = Cb + row * ldc + c;
-    if (g.accumulate) v += *p;
-    if (first) {
-      if (g.bias) v += g.bias[b * g.bias_bs + c];
-      if (g.resid) v += g.resid[b * g.resid_bs + row * g.resid_ld + c];
-      if (g.elu) v = v > 0.f ? v : expm1f(v);
-    }
-    *p = v;
+    store_out(g, b, row, col, v);
+  }
+}
+
+// Tail fix-up: the last tail_rem tiles, each the sum of tail_s K-slices in slice order.
+__global__ void __launch_bounds__(256) tail_fixup_kernel(GemmArgs g) {
+  const int64_t BN = 128, TS = (int64_t)g.bm * BN, total = g.tail_rem * TS;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t ti = t / TS, rc = t - ti * TS, rl = rc / BN, cl = rc - rl * BN;
+    const int64_t lin = g.dp_blocks + ti, tm = lin / g.tiles_n, tn = lin - tm * g.tiles_n;
+    const int64_t row = tm * g.bm + rl, col = tn * BN + cl;
+    if (row >= g.M || col >= g.N) continue;
+    float v = 0.f;
+    for (int z = 0; z < g.tail_s; ++z) v += g.tail_partial[((int64_t)z * g.tail_rem + ti) * TS + rc];
+    store_out(g, 0, row, col, v);
   }
 }
 
@@ -134,78 +166,31 @@ __device__ inline void tile_of(int64_t b, int64_t T, int64_t tiles_n, int64_t& t
   tn = t % tiles_n;
 }
 
-// Block tile (64*WM) x 128 x 32, 2*WM waves as WM x 2; each wave owns a 64 x 64 sub-tile =
-// 2 x 2 MFMA blocks of 32 x 32. A_KC: A is k-contiguous (sak == 1, ld = sam) else m-contiguous;
-// B_NC: B is n-contiguous (sbn == 1, ld = sbk) else k-contiguous.
-// TAG only separates the symbol names of the call sites in profiles (0 = forward projection,
-// 1 = auxiliary products, 2 = split-K weight gradient); the code is identical.
-template <bool A_KC, bool B_NC, int WM, int TAG>
-__global__ void __launch_bounds__(128 * WM, 2) gemm_f32_kernel(GemmArgs g) {
-  constexpr int BM = 64 * WM, BN = 128, THREADS = 128 * WM;
-  using AL = typename std::conditional<A_KC, KContig<BM, THREADS>, RContig<BM, THREADS>>::type;
-  using BL = typename std::conditional<B_NC, RContig<BN, THREADS>, KContig<BN, THREADS>>::type;
-  constexpr int LDA = BM + PAD, LDB = BN + PAD;
-  __shared__ __attribute__((aligned(16))) float As[BK * LDA];
-  __shared__ __attribute__((aligned(16))) float Bs[BK * LDB];
-
-  const int64_t T = g.tiles_m * g.tiles_n;
-  int64_t tm, tn;
-  tile_of(blockIdx.x, T, g.tiles_n, tm, tn);
-  const int64_t m0 = tm * BM, n0 = tn * BN;
-  const float* __restrict__ A = g.A + blockIdx.y * g.a_bs;
-  const float* __restrict__ B = g.B + blockIdx.y * g.b_bs;
+// Epilogue shared by both kernels. C/D map of a 32x32 f32 MFMA block: col = lane&31,
+// row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+__device__ inline void write_tile(const GemmArgs& g, floatx16 (&acc)[2][2], int tail_z,
+                                  int64_t tail_ti, int64_t m0, int64_t n0, int wm, int wn,
+                                  int lane) {
   const int64_t M = g.M, N = g.N;
-  // split-K: slice blockIdx.z covers k in [kb, ke) and writes its own partial slab
-  const int64_t kb = blockIdx.z * g.k_per_split;
-  const int64_t K = min(g.K, kb + g.k_per_split);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-
-  floatx16 acc[2][2];
+  if (tail_z >= 0) {   // tail slice: tile-local partial, summed by tail_fixup_kernel
+    float* P = g.tail_partial + ((int64_t)tail_z * g.tail_rem + tail_ti) * (BM * BN);
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+    for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+      for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  float va[AL::EPT], vb[BL::EPT];
-  const int64_t nk = ceil_div(K - kb, BK);
-  AL::load(A, g.lda, m0, M, kb, K, g.a_vec, va);
-  BL::load(B, g.ldb, n0, N, kb, K, g.b_vec, vb);
-  for (int64_t kt = 0; kt < nk; ++kt) {
-    __syncthreads();
-    AL::store(As, va);
-    BL::store(Bs, vb);
-    __syncthreads();
-    if (kt + 1 < nk) {
-      AL::load(A, g.lda, m0, M, kb + (kt + 1) * BK, K, g.a_vec, va);
-      BL::load(B, g.ldb, n0, N, kb + (kt + 1) * BK, K, g.b_vec, vb);
-    }
-    const int kl = lane >> 5, il = lane & 31;
-#pragma unroll
-    for (int kk = 0; kk < BK; kk += 2) {
-      const float a0 = As[(kk + kl) * LDA + wm * 64 + il];
-      const float a1 = As[(kk + kl) * LDA + wm * 64 + 32 + il];
-      const float b0 = Bs[(kk + kl) * LDB + wn * 64 + il];
-      const float b1 = Bs[(kk + kl) * LDB + wn * 64 + 32 + il];
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
-    }
+        for (int r = 0; r < 16; ++r) {
+          const int rl = wm * 64 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          P[rl * BN + wn * 64 + ni * 32 + (lane & 31)] = acc[mi][ni][r];
+        }
+    return;
   }
-
-  // C/D map of a 32x32 f32 MFMA block: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
     for (int ni = 0; ni < 2; ++ni) {
       const int64_t col = n0 + wn * 64 + ni * 32 + (lane & 31);
       if (col >= N) continue;
-      float* Cb;
-      int64_t ldc, c;
-      const bool first = col < g.n_split;
       if (g.splits > 1) {   // partial slab z: plain [M][N] store, reduced by splitk_reduce_kernel
         float* P = g.partial + ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * M * N;
 #pragma unroll
@@ -215,40 +200,160 @@ __global__ void __launch_bounds__(128 * WM, 2) gemm_f32_kernel(GemmArgs g) {
         }
         continue;
       }
-      if (first) { Cb = g.C0 + blockIdx.y * g.c0_bs; ldc = g.ldc0; c = col; }
-      else { Cb = g.C1 + blockIdx.y * g.c1_bs; ldc = g.ldc1; c = col - g.n_split; }
-      const float bcol = (first && g.bias) ? g.bias[blockIdx.y * g.bias_bs + c] : 0.f;
-      const float* rs = (first && g.resid) ? g.resid + blockIdx.y * g.resid_bs + c : nullptr;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int64_t row = m0 + wm * 64 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (row < M) {
-          float* p = Cb + row * ldc + c;
-          float v = g.accumulate ? *p + acc[mi][ni][r] : acc[mi][ni][r];
-          if (first) {
-            v += bcol;
-            if (rs) v += rs[row * g.resid_ld];
-            if (g.elu) v = v > 0.f ? v : expm1f(v);
-          }
-          *p = v;
-        }
+        if (row < M) store_out(g, blockIdx.y, row, col, acc[mi][ni][r]);
       }
     }
 }
 
-template <int WM, int TAG>
-int launch_gemm(const GemmArgs& g0, bool a_kc, bool b_nc, int batch, hipStream_t stream) {
+// A_KC: A is k-contiguous (sak == 1, ld = sam) else m-contiguous; B_KC: B is k-contiguous
+// (sbk == 1, ld = sbn) else n-contiguous. TAG only separates the symbol names of the call sites
+// in profiles (0 = forward projection, 1 = auxiliary products, 2 = split-K weight gradient).
+template <bool A_KC, bool B_KC, bool VEC, int TAG, int BK, int MINB>
+__global__ void __launch_bounds__(THREADS, MINB) gemm_f32_kernel(GemmArgs g) {
+  using TA = Tile<A_KC, BM, BK>;
+  using TB = Tile<B_KC, BN, BK>;
+  constexpr int STAGE = TA::SIZE + TB::SIZE;
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+
+  const int64_t T = g.tiles_m * g.tiles_n;
+  int64_t tm, tn, kb, K;
+  int tail_z = -1;
+  int64_t tail_ti = 0;
+  if (g.tail_s > 1 && (int64_t)blockIdx.x >= g.dp_blocks) {
+    const int64_t j = blockIdx.x - g.dp_blocks;
+    tail_ti = j % g.tail_rem;
+    tail_z = (int)(j / g.tail_rem);
+    const int64_t lin = g.dp_blocks + tail_ti;
+    tm = lin / g.tiles_n;
+    tn = lin - tm * g.tiles_n;
+    kb = tail_z * g.k_per_split;
+    K = min(g.K, kb + g.k_per_split);
+  } else if (g.tail_s > 1) {   // data-parallel part of a tail-split launch: whole K
+    tile_of(blockIdx.x, g.dp_blocks, g.tiles_n, tm, tn);
+    kb = 0;
+    K = g.K;
+  } else {
+    tile_of(blockIdx.x, T, g.tiles_n, tm, tn);
+    // split-K: slice blockIdx.z covers k in [kb, ke) and writes its own partial slab
+    kb = blockIdx.z * g.k_per_split;
+    K = min(g.K, kb + g.k_per_split);
+  }
+  const int64_t m0 = tm * BM, n0 = tn * BN;
+  const float* __restrict__ A = g.A + blockIdx.y * g.a_bs;
+  const float* __restrict__ B = g.B + blockIdx.y * g.b_bs;
+  const int64_t M = g.M, N = g.N;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int il = lane & 31, h4 = 4 * (lane >> 5);
+
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  float4 va[TA::NV], vb[TB::NV];
+  const int64_t nk = K > kb ? ceil_div(K - kb, BK) : 0;
+  if (nk > 0) {
+    TA::template load<VEC>(A, g.lda, m0, M, kb, K, va);
+    TB::template load<VEC>(B, g.ldb, n0, N, kb, K, vb);
+    TA::template store<VEC>(smem, va, m0, M, kb, K);
+    TB::template store<VEC>(smem + TA::SIZE, vb, n0, N, kb, K);
+  }
+  __syncthreads();
+  for (int64_t kt = 0; kt < nk; ++kt) {
+    float* cur = smem + (kt & 1) * STAGE;
+    float* nxt = smem + ((kt & 1) ^ 1) * STAGE;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      TA::template load<VEC>(A, g.lda, m0, M, kb + (kt + 1) * BK, K, va);
+      TB::template load<VEC>(B, g.ldb, n0, N, kb + (kt + 1) * BK, K, vb);
+    }
+    const float* ai = cur;
+    const float* bi = cur + TA::SIZE;
+    float4 fa[2], fb[2];
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+      fa[x] = TA::frag(ai, wm * 64 + x * 32 + il, h4);
+      fb[x] = TB::frag(bi, wn * 64 + x * 32 + il, h4);
+    }
+#pragma unroll
+    for (int grp = 0; grp < BK / 8; ++grp) {
+      float4 na[2], nb[2];
+      if (grp + 1 < BK / 8) {
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+          na[x] = TA::frag(ai, wm * 64 + x * 32 + il, 8 * (grp + 1) + h4);
+          nb[x] = TB::frag(bi, wn * 64 + x * 32 + il, 8 * (grp + 1) + h4);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float a0 = get4(fa[0], j), a1 = get4(fa[1], j);
+        const float b0 = get4(fb[0], j), b1 = get4(fb[1], j);
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+      }
+      if (grp + 1 < BK / 8) {
+        fa[0] = na[0]; fa[1] = na[1]; fb[0] = nb[0]; fb[1] = nb[1];
+      }
+    }
+    if (more) {
+      TA::template store<VEC>(nxt, va, m0, M, kb + (kt + 1) * BK, K);
+      TB::template store<VEC>(nxt + TA::SIZE, vb, n0, N, kb + (kt + 1) * BK, K);
+    }
+    __syncthreads();
+  }
+
+  write_tile(g, acc, tail_z, tail_ti, m0, n0, wm, wn, lane);
+}
+
+// K-tile depth / occupancy of the GEMM kernel, env GATX_GEMM_BK (tuning only): 17 (default) =
+// BK 16 at 4 workgroups per CU (LDS 4 x 40 KB, <= 128 VGPRs), 16 = BK 16 at 3, 32 = BK 32 at 2,
+// 64 = BK 64 at 1. Measured on the PPI shapes: 118 / 115 / 111 / 93 TF (occupancy hides the
+// barrier and LDS latency that one K-tile of MFMAs cannot).
+int gemm_variant() {
+  static const int v = [] {
+    const char* e = getenv("GATX_GEMM_BK");
+    const int x = e ? atoi(e) : 17;
+    return (x == 16 || x == 32 || x == 64) ? x : 17;
+  }();
+  return v;
+}
+
+template <int TAG>
+int launch_gemm(const GemmArgs& g0, bool a_kc, bool b_kc, int batch, hipStream_t stream) {
   GemmArgs g = g0;
-  g.tiles_m = ceil_div(g.M, 64 * WM);
-  g.tiles_n = ceil_div(g.N, 128);
   const int64_t tiles = g.tiles_m * g.tiles_n;
   GATX_REQUIRE(tiles < (1ll << 31) && batch < 65536, "gemm: too many tiles");
-  dim3 grid((unsigned)tiles, (unsigned)batch, (unsigned)g.splits);
-  constexpr int TH = 128 * WM;
-  if (a_kc && b_nc) gemm_f32_kernel<true, true, WM, TAG><<<grid, TH, 0, stream>>>(g);
-  else if (a_kc) gemm_f32_kernel<true, false, WM, TAG><<<grid, TH, 0, stream>>>(g);
-  else if (b_nc) gemm_f32_kernel<false, true, WM, TAG><<<grid, TH, 0, stream>>>(g);
-  else gemm_f32_kernel<false, false, WM, TAG><<<grid, TH, 0, stream>>>(g);
+  const int64_t gx = g.tail_s > 1 ? g.dp_blocks + g.tail_rem * g.tail_s : tiles;
+  dim3 grid((unsigned)gx, (unsigned)batch, (unsigned)g.splits);
+  const int var = gemm_variant();
+#define GATX_GEMM_V(AK, BKC, V)                                                                 \
+  do {                                                                                         \
+    if (var == 16) gemm_f32_kernel<AK, BKC, V, TAG, 16, 3><<<grid, THREADS, 0, stream>>>(g);   \
+    else if (var == 17) gemm_f32_kernel<AK, BKC, V, TAG, 16, 4><<<grid, THREADS, 0, stream>>>(g); \
+    else if (var == 64) gemm_f32_kernel<AK, BKC, V, TAG, 64, 1><<<grid, THREADS, 0, stream>>>(g); \
+    else gemm_f32_kernel<AK, BKC, V, TAG, 32, 2><<<grid, THREADS, 0, stream>>>(g);             \
+  } while (0)
+#define GATX_GEMM_GO(AK, BKC)                                                                  \
+  do {                                                                                        \
+    if (g.a_vec && g.b_vec) GATX_GEMM_V(AK, BKC, true);                                       \
+    else GATX_GEMM_V(AK, BKC, false);                                                         \
+  } while (0)
+  if (a_kc && b_kc) GATX_GEMM_GO(true, true);
+  else if (a_kc) GATX_GEMM_GO(true, false);
+  else if (b_kc) GATX_GEMM_GO(false, true);
+  else GATX_GEMM_GO(false, false);
+#undef GATX_GEMM_GO
+#undef GATX_GEMM_V
   GATX_LAUNCH_CHECK("gemm_f32");
   if (g.splits > 1) {
     const int64_t total = g.M * g.N * batch;
@@ -256,18 +361,60 @@ int launch_gemm(const GemmArgs& g0, bool a_kc, bool b_nc, int batch, hipStream_t
     splitk_reduce_kernel<<<rg, 256, 0, stream>>>(g, batch);
     GATX_LAUNCH_CHECK("splitk_reduce");
   }
+  if (g.tail_s > 1) {
+    const int64_t total = g.tail_rem * BM * BN;
+    tail_fixup_kernel<<<(unsigned)std::min<int64_t>(ceil_div(total, 256), 8192), 256, 0, stream>>>(g);
+    GATX_LAUNCH_CHECK("tail_fixup");
+  }
   return 0;
 }
 
+// Workgroups of one gemm_f32_kernel instance resident on the whole device at once.
+int64_t resident_blocks() {
+  static int64_t cached = 0;
+  if (cached) return cached;
+  int dev = 0, cus = 0, per_cu = 0;
+  const int var = gemm_variant();
+  const void* fn = var == 17 ? reinterpret_cast<const void*>(&gemm_f32_kernel<true, true, true, 0, 16, 4>)
+                 : var == 16 ? reinterpret_cast<const void*>(&gemm_f32_kernel<true, true, true, 0, 16, 3>)
+                 : var == 64 ? reinterpret_cast<const void*>(&gemm_f32_kernel<true, true, true, 0, 64, 1>)
+                             : reinterpret_cast<const void*>(&gemm_f32_kernel<true, true, true, 0, 32, 2>);
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, THREADS, 0) != hipSuccess ||
+      cus <= 0 || per_cu <= 0) {
+    (void)hipGetLastError();
+    return cached = 512;
+  }
+  return cached = (int64_t)cus * per_cu;
+}
+
 // Split K when the output alone cannot fill the chip (g_W = G^T x: ~70 tiles, K = #nodes):
-// aim for >= 512 workgroups with >= 1024 k per slice.
-int choose_splits(int64_t tiles, int64_t K) {
+// the most slices (<= 64, >= 512 k each) with tiles * slices still within one resident wave.
+int choose_splits(int64_t tiles, int64_t K, int64_t slots) {
   int s = 1;
-  while (tiles * s < 512 && K / (s * 2) >= 1024 && s < 32) s *= 2;
+  while ((s + 1) * tiles <= slots && K / (s + 1) >= 512 && s < 64) ++s;
   return s;
 }
 
-int g_gemm_wm = 0;   // 0: choose by shape; 2 or 4 forces the 128- or 256-row tile
+// Tail split of a data-parallel GEMM: the last `rem` tiles (the partial wave) are each cut into
+// s K-slices; s minimises the tail's length in waves, ceil(rem*s/slots)/s, plus the fix-up's
+// partial-tile traffic (~5 TB/s) measured in waves of 128x128xK tiles at ~157 TF.
+int choose_tail_split(int64_t tiles, int64_t K, int64_t slots, int64_t& rem) {
+  rem = tiles % slots;
+  if (rem == 0 || tiles < 1) return 1;
+  const double wave_s = 2.0 * BM * BN * (double)K / (157e12 / (double)slots);
+  int best = 1;
+  double best_c = 0.75 / 0.95;   // only clear wins: wave boundaries are soft in practice
+  for (int s = 2; s <= 16; ++s) {
+    if (ceil_div(K, s) < 2 * KSTEP) break;
+    const double waves = (double)ceil_div(rem * s, slots) / s;
+    const double fix = (double)rem * (s + 1) * BM * BN * 4.0 / 5e12 / wave_s;
+    if (waves + fix < best_c * 0.95) { best = s; best_c = waves + fix; }
+  }
+  return best;
+}
+
 
 }  // namespace
 }  // namespace gatx
@@ -290,10 +437,10 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
   if (K == 0) return 0;
   GemmArgs g;
   const bool a_kc = (sak == 1);
-  const bool b_nc = (sbn == 1);
+  const bool b_kc = (sbk == 1);
   g.M = M; g.N = N; g.K = K;
   g.A = A; g.lda = a_kc ? sam : sak; g.a_bs = a_bs;
-  g.B = B; g.ldb = b_nc ? sbk : sbn; g.b_bs = b_bs;
+  g.B = B; g.ldb = b_kc ? sbn : sbk; g.b_bs = b_bs;
   g.C0 = C0; g.ldc0 = ldc0; g.c0_bs = c0_bs; g.n_split = n_split;
   g.C1 = C1; g.ldc1 = ldc1; g.c1_bs = c1_bs;
   g.accumulate = accumulate;
@@ -306,45 +453,66 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
   };
   g.a_vec = aligned(A, g.lda, a_bs);
   g.b_vec = aligned(B, g.ldb, b_bs);
-  static const int env_wm = [] {
-    const char* e = getenv("GATX_GEMM_WM");
-    return e ? atoi(e) : 0;
-  }();
-  int wm = g_gemm_wm ? g_gemm_wm : env_wm;
-  if (wm == 0) wm = 2;
-  if (workspace) {
-    const int64_t tiles = ceil_div(M, 64 * wm) * ceil_div(N, 128) * batch;
-    int sp = choose_splits(tiles, K);
-    while (sp > 1 && (size_t)sp * batch * M * N * sizeof(float) > workspace_bytes) sp /= 2;
+  g.tiles_m = ceil_div(M, BM);
+  g.tiles_n = ceil_div(N, BN);
+  g.dp_blocks = 0; g.tail_rem = 0; g.tail_s = 1; g.bm = BM; g.tail_partial = nullptr;
+  const int64_t tiles = g.tiles_m * g.tiles_n * batch;
+  const int64_t slots = resident_blocks();
+  if (workspace && tag == 2) {   // explicit split-K into [M][N] slabs
+    int sp = choose_splits(tiles, K, slots);
+    while (sp > 1 && (size_t)sp * batch * M * N * sizeof(float) > workspace_bytes) --sp;
     if (sp > 1) {
-      g.splits = sp;
-      g.k_per_split = round_up(ceil_div(K, sp), BK);
+      g.k_per_split = round_up(ceil_div(K, sp), KSTEP);
       g.splits = (int)ceil_div(K, g.k_per_split);
       g.partial = (float*)workspace;
     }
+  } else if (workspace && batch == 1) {   // tail split of the last partial wave
+    int64_t rem = 0;
+    int ts = choose_tail_split(tiles, K, slots, rem);
+    while (ts > 1 && (size_t)ts * rem * BM * BN * sizeof(float) > workspace_bytes) --ts;
+    if (ts > 1) {
+      g.k_per_split = round_up(ceil_div(K, ts), KSTEP);
+      g.tail_s = (int)ceil_div(K, g.k_per_split);
+      if (g.tail_s >= 2) {
+        g.tail_rem = rem;
+        g.dp_blocks = tiles - rem;
+        g.tail_partial = (float*)workspace;
+      } else {
+        g.tail_s = 1;
+        g.k_per_split = K;
+      }
+    }
   }
-  if (wm == 4) return launch_gemm<4, 1>(g, a_kc, b_nc, batch, stream);   // tuning only
-  if (tag == 0) return launch_gemm<2, 0>(g, a_kc, b_nc, batch, stream);
-  if (tag == 2) return launch_gemm<2, 2>(g, a_kc, b_nc, batch, stream);
-  return launch_gemm<2, 1>(g, a_kc, b_nc, batch, stream);
+  if (tag == 0) return launch_gemm<0>(g, a_kc, b_kc, batch, stream);
+  if (tag == 2) return launch_gemm<2>(g, a_kc, b_kc, batch, stream);
+  return launch_gemm<1>(g, a_kc, b_kc, batch, stream);
 }
 
-extern "C" void gatx_set_gemm_rows(int rows) { g_gemm_wm = rows / 64; }
+extern "C" size_t gatx_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K) {
+  int64_t rem = 0;
+  const int ts = choose_tail_split(ceil_div(M, BM) * ceil_div(N, BN), K,
+                                   resident_blocks(), rem);
+  return ts > 1 ? (size_t)ts * rem * 128 * 128 * sizeof(float) : 0;
+}
 
 extern "C" int gatx_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t sam,
                              int64_t sak, const float* B, int64_t sbk, int64_t sbn, float* C0,
                              int64_t ldc0, int64_t n_split, float* C1, int64_t ldc1,
-                             int accumulate, gatx_stream_t s) {
+                             int accumulate, void* workspace, size_t workspace_bytes,
+                             gatx_stream_t s) {
   return gemm_impl(M, N, K, 1, A, sam, sak, 0, B, sbk, sbn, 0, C0, ldc0, 0, n_split, C1, ldc1, 0,
-                   accumulate, nullptr, 0, nullptr, 0, 0, 0, nullptr, 0, 1, (hipStream_t)s);
+                   accumulate, nullptr, 0, nullptr, 0, 0, 0, workspace, workspace_bytes, 1,
+                   (hipStream_t)s);
 }
 
 extern "C" int gatx_projection_gemm(int64_t M, int64_t N, int64_t K, const float* A, int64_t sam,
                                     int64_t sak, const float* B, int64_t sbk, int64_t sbn,
                                     float* C0, int64_t ldc0, int64_t n_split, float* C1,
-                                    int64_t ldc1, gatx_stream_t s) {
+                                    int64_t ldc1, void* workspace, size_t workspace_bytes,
+                                    gatx_stream_t s) {
   return gemm_impl(M, N, K, 1, A, sam, sak, 0, B, sbk, sbn, 0, C0, ldc0, 0, n_split, C1, ldc1, 0,
-                   0, nullptr, 0, nullptr, 0, 0, 0, nullptr, 0, 0, (hipStream_t)s);
+                   0, nullptr, 0, nullptr, 0, 0, 0, workspace, workspace_bytes, 0,
+                   (hipStream_t)s);
 }
 
 extern "C" int gatx_gemm_f32_batched(int64_t batch, int64_t M, int64_t N, int64_t K,
@@ -361,7 +529,7 @@ extern "C" int gatx_gemm_f32_batched(int64_t batch, int64_t M, int64_t N, int64_
 
 extern "C" size_t gatx_gemm_splitk_workspace_bytes(int64_t M, int64_t N, int64_t K) {
   const int64_t tiles = ceil_div(M, 128) * ceil_div(N, 128);
-  const int sp = choose_splits(tiles, K);
+  const int sp = choose_splits(tiles, K, resident_blocks());
   return sp > 1 ? (size_t)sp * M * N * sizeof(float) : 0;
 }
 

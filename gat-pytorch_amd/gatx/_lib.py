@@ -38,7 +38,8 @@ SIGNATURES = {
     "gatx_prepare_weights": (c_i, [P, P, c_i, c_i, c_i64, P, P]),
     "gatx_prepare_weights_floats": (c_i64, [c_i, c_i, c_i64, c_i]),
     "gatx_gemm_f32": (c_i, [c_i64, c_i64, c_i64, P, c_i64, c_i64, P, c_i64, c_i64, P, c_i64,
-                            c_i64, P, c_i64, c_i, P]),
+                            c_i64, P, c_i64, c_i, P, c_sz, P]),
+    "gatx_gemm_workspace_bytes": (c_sz, [c_i64, c_i64, c_i64]),
     "gatx_gemm_f32_batched": (c_i, [c_i64, c_i64, c_i64, c_i64, P, c_i64, c_i64, c_i64, P,
                                     c_i64, c_i64, c_i64, P, c_i64, c_i64, c_i, P, c_i64, P, c_i64,
                                     c_i64, c_i, P]),
@@ -46,8 +47,7 @@ SIGNATURES = {
                                    P, c_f, c_u64, P, c_i64, P, c_i64, c_i, P, c_i64, P]),
     "gatx_pad_rows": (c_i, [P, c_i64, c_i64, c_i64, P, c_i64, P]),
     "gatx_projection_gemm": (c_i, [c_i64, c_i64, c_i64, P, c_i64, c_i64, P, c_i64, c_i64, P,
-                                   c_i64, c_i64, P, c_i64, P]),
-    "gatx_set_gemm_rows": (None, [c_i]),
+                                   c_i64, c_i64, P, c_i64, P, c_sz, P]),
     "gatx_set_debug": (None, [c_i]),
     "gatx_gemm_splitk_workspace_bytes": (c_sz, [c_i64, c_i64, c_i64]),
     "gatx_gemm_f32_splitk": (c_i, [c_i64, c_i64, c_i64, P, c_i64, c_i64, P, c_i64, c_i64, P, c_i64,

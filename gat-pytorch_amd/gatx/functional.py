@@ -104,6 +104,15 @@ def _max_ws(dev):
 _WAUG_CACHE: "OrderedDict" = None
 
 
+def gemm_workspace(M: int, N: int, K: int, dev):
+    """(pointer, bytes) of the tail-split workspace gatx_gemm_f32 / gatx_projection_gemm may
+    use for an (M x K) . (K x N) product (cached allocator; None when this shape needs none)."""
+    nb = lib.gatx_gemm_workspace_bytes(M, N, K)
+    if nb == 0:
+        return None, 0
+    return ptr(torch.empty(nb, dtype=torch.uint8, device=dev)), nb
+
+
 def augmented_weight(W, a, sh: "LayerShape"):
     """W_aug = [W padded per head; A_src W; A_dst W] (gatx_prepare_weights). Cached on the
     parameters' identity and version counters, so inference reuses it across steps while any
@@ -201,7 +210,7 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
             with _span("gemm_scores", (N, sh.H2, sh.F_in)):
                 call("gatx_gemm_f32", N, sh.H2, sh.F_in, ptr(x), sh.F_in, 1,
                      ptr(W_aug) + 4 * sh.Dp * sh.F_in, 1, sh.F_in, ptr(S), sh.H2, sh.H2, None,
-                     0, 0, s)
+                     0, 0, *gemm_workspace(N, sh.H2, sh.F_in, dev), s)
             with _span("attention_max", (E2, sh.NH)):
                 call("gatx_attention_max", ptr(graph.col), ptr(graph.rowidx), E2, ptr(S),
                      sh.NH, ptr(M_ord), ptr(_max_ws(dev)), s)
@@ -226,11 +235,13 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
     if fold_scores_into_gemm(sh):
         with _span("gemm", (N, sh.K_aug, sh.F_in, sh.NH, sh.F)):
             call("gatx_projection_gemm", N, sh.K_aug, sh.F_in, ptr(x), sh.F_in, 1, ptr(W_aug), 1,
-                 sh.F_in, ptr(Wh), sh.Dp, sh.Dp, ptr(S), max(sh.H2, 1), s)
+                 sh.F_in, ptr(Wh), sh.Dp, sh.Dp, ptr(S), max(sh.H2, 1),
+                 *gemm_workspace(N, sh.K_aug, sh.F_in, dev), s)
     else:
         with _span("gemm", (N, sh.Dp, sh.F_in, sh.NH, sh.F)):
             call("gatx_projection_gemm", N, sh.Dp, sh.F_in, ptr(x), sh.F_in, 1, ptr(W_aug), 1,
-                 sh.F_in, ptr(Wh), sh.Dp, sh.Dp, None, 0, s)
+                 sh.F_in, ptr(Wh), sh.Dp, sh.Dp, None, 0, *gemm_workspace(N, sh.Dp, sh.F_in, dev),
+                 s)
         with _span("node_scores", (N, sh.NH, sh.F)):
             call("gatx_node_scores", ptr(Wh), N, sh.NH, sh.F, ptr(a), ptr(S), s)
     if not sh.const:
@@ -263,7 +274,8 @@ def layer_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShape, 
     if saved["Wh"] is None:   # reassociated forward never built Wh: project now
         Wh = torch.empty((N, sh.Dp), **f32)
         call("gatx_gemm_f32", N, sh.Dp, sh.F_in, ptr(x), sh.F_in, 1, ptr(saved["W_aug"]), 1,
-             sh.F_in, ptr(Wh), sh.Dp, sh.Dp, None, 0, 0, s)
+             sh.F_in, ptr(Wh), sh.Dp, sh.Dp, None, 0, 0, *gemm_workspace(N, sh.Dp, sh.F_in, dev),
+             s)
         saved["Wh"] = Wh
     go = torch.empty((N, sh.Dp if sh.concat else sh.Fp), **f32)
     g_pre = torch.empty((N, sh.out_cols), **f32) if (need_resid or (need_bias and elu)) else None
@@ -293,7 +305,7 @@ def layer_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShape, 
     if need_x:
         g_x = torch.empty((N, sh.F_in), **f32)
         call("gatx_gemm_f32", N, sh.F_in, sh.K_aug, ptr(G_aug), sh.ldg, 1, ptr(W_aug), sh.F_in, 1,
-             ptr(g_x), sh.F_in, sh.F_in, None, 0, 0, s)
+             ptr(g_x), sh.F_in, sh.F_in, None, 0, 0, *gemm_workspace(N, sh.F_in, sh.K_aug, dev), s)
     if need_W or need_a:
         gW_aug = torch.empty((sh.K_aug, sh.F_in), **f32)
         ws_bytes = lib.gatx_gemm_splitk_workspace_bytes(sh.K_aug, sh.F_in, N)

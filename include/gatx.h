@@ -88,7 +88,12 @@ int64_t gatx_prepare_weights_floats(int NH, int F, int64_t F_in, int has_a);
  * scores), and for the backward's g_x = G_aug * W_aug and g_W_aug = G_aug^T * x. */
 int gatx_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t sam, int64_t sak,
                   const float* B, int64_t sbk, int64_t sbn, float* C0, int64_t ldc0,
-                  int64_t n_split, float* C1, int64_t ldc1, int accumulate, gatx_stream_t stream);
+                  int64_t n_split, float* C1, int64_t ldc1, int accumulate, void* workspace,
+                  size_t workspace_bytes, gatx_stream_t stream);
+/* Workspace that lets gatx_gemm_f32 / gatx_projection_gemm split the K range of the tiles in
+ * their last, partially filled wave (0 = no split for this shape; NULL workspace = never split).
+ * The slices are summed in a fixed order by a fix-up kernel, so results stay deterministic. */
+size_t gatx_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K);
 /* Split-K variant for reductions over many rows (g_W_aug = G_aug^T x, K = #nodes): slabs of
  * partial products in `workspace` (gatx_gemm_splitk_workspace_bytes; 0 = no split needed)
  * summed in a fixed order by a second kernel (deterministic). */
@@ -98,15 +103,13 @@ int gatx_gemm_f32_splitk(int64_t M, int64_t N, int64_t K, const float* A, int64_
                          int64_t ldc, int accumulate, void* workspace, size_t workspace_bytes,
                          gatx_stream_t stream);
 
-/* Tuning knob: block-tile rows of gatx_gemm_f32* (128 or 256; 0 = default / env GATX_GEMM_WM). */
-void gatx_set_gemm_rows(int rows);
 
 /* gatx_gemm_f32 for the forward projection x . W_aug^T (accumulate = 0); a separate entry point
  * only so profiles can tell the projection launches from the auxiliary products. */
 int gatx_projection_gemm(int64_t M, int64_t N, int64_t K, const float* A, int64_t sam,
                          int64_t sak, const float* B, int64_t sbk, int64_t sbn, float* C0,
                          int64_t ldc0, int64_t n_split, float* C1, int64_t ldc1,
-                         gatx_stream_t stream);
+                         void* workspace, size_t workspace_bytes, gatx_stream_t stream);
 
 /* The same for `batch` independent products (batch b offsets A, B, C by b*a_bs, b*b_bs,
  * b*c_bs floats) with a fused epilogue C = elu?(A*B (+C) + bias[b*bias_bs + n] +

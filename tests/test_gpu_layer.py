@@ -125,7 +125,7 @@ def test_gemm_mfma_layout(device):
                 sbk, sbn = (1, K) if b_t else (N, 1)
                 C = torch.full((M, N), float("nan"), device=device)
                 call("gatx_gemm_f32", M, N, K, ptr(Am), sam, sak, ptr(Bm), sbk, sbn, ptr(C), N,
-                     N, None, 0, 0, stream())
+                     N, None, 0, 0, None, 0, stream())
                 torch.cuda.synchronize()
                 err = (C - ref).abs().max().item()
                 assert err < 1e-4 * max(1.0, K ** 0.5), (M, N, K, a_t, b_t, err)
@@ -136,9 +136,39 @@ def test_gemm_mfma_layout(device):
     C0 = torch.zeros(M, 64, device=device)
     C1 = torch.zeros(M, N - 64, device=device)
     call("gatx_gemm_f32", M, N, K, ptr(I), K, 1, ptr(B), N, 1, ptr(C0), 64, 64, ptr(C1), N - 64,
-         0, stream())
+         0, None, 0, stream())
     torch.cuda.synchronize()
     assert torch.equal(torch.cat([C0, C1], 1), B)
+
+
+@pytest.mark.gpu
+def test_gemm_tail_split(device):
+    """Shapes whose last wave of tiles is split along K (fix-up kernel sums the slices):
+    same result as the unsplit GEMM to fp32 rounding, bitwise run to run, split output kept."""
+    _gatx()
+    from gatx._lib import lib, call, ptr, stream
+    torch.manual_seed(3)
+    for (M, N, K, n_split) in [(2000, 1032, 1024, 1024), (44900, 756, 1024, 756),
+                               (3000, 200, 96, 200)]:
+        A = torch.randn(M, K, device=device)
+        Bt = torch.randn(N, K, device=device)            # W_aug layout: [N][K]
+        ref = (A.double() @ Bt.double().t()).float()
+        nb = lib.gatx_gemm_workspace_bytes(M, N, K)
+        ws = torch.empty(max(nb, 1), dtype=torch.uint8, device=device)
+        outs = []
+        for use_ws in (True, True, False):
+            C0 = torch.full((M, n_split), float("nan"), device=device)
+            C1 = torch.full((M, max(N - n_split, 1)), float("nan"), device=device)
+            call("gatx_projection_gemm", M, N, K, ptr(A), K, 1, ptr(Bt), 1, K, ptr(C0), n_split,
+                 n_split, ptr(C1), max(N - n_split, 1), ptr(ws) if use_ws else None,
+                 nb if use_ws else 0, stream())
+            torch.cuda.synchronize()
+            C = torch.cat([C0, C1[:, :N - n_split]], 1)
+            assert (C - ref).abs().max().item() < 2e-4 * K ** 0.5, (M, N, K)
+            outs.append(C)
+        assert torch.equal(outs[0], outs[1])
+        if nb:
+            assert (outs[0] - outs[2]).abs().max().item() < 2e-4 * K ** 0.5
 
 
 def test_graph_build_matches_oracle(device):
@@ -299,18 +329,22 @@ def test_gemm_splitk_and_node_scores(device):
              wsb, stream())
         torch.cuda.synchronize()
         assert (C - ref).abs().max().item() < 1e-4 * K ** 0.5, (M, N, K)
-    # node scores == Wh . A2^T (reference association of the logit GEMV)
+    # node scores == Wh . A2^T (reference association of the logit GEMV); covers the
+    # register-resident reduce-scatter kernel (all CPL x H instances) and the LDS fallback
     from gatx import data as gd
-    NH, F, N = 4, 30, 333
-    Wh = torch.from_numpy(gd.normal(3, N * NH * 32).reshape(N, NH * 32)).to(device)
-    Wh.view(N, NH, 32)[:, :, F:] = 0
-    a = torch.from_numpy(gd.xavier_uniform(4, NH, NH * 2 * F)).to(device)
-    S = torch.empty(N, 2 * NH, device=device)
-    call("gatx_node_scores", ptr(Wh), N, NH, F, ptr(a), ptr(S), stream())
-    A = a.view(NH, NH, 2, F)
-    Whv = Wh.view(N, NH, 32)[:, :, :F].double()
-    ref_src = torch.einsum("nkf,hkf->nh", Whv, A[:, :, 0].double())
-    ref_dst = torch.einsum("nkf,hkf->nh", Whv, A[:, :, 1].double())
-    torch.cuda.synchronize()
-    assert (S[:, :NH].double() - ref_src).abs().max().item() < 1e-4
-    assert (S[:, NH:].double() - ref_dst).abs().max().item() < 1e-4
+    for (NH, F, N) in [(4, 30, 333), (4, 256, 5001), (1, 7, 70), (6, 121, 900), (8, 8, 1000),
+                       (2, 100, 257), (3, 64, 130), (8, 30, 64), (1, 256, 300)]:
+        Fp = -(-F // 4) * 4
+        Wh = torch.from_numpy(gd.normal(3, N * NH * Fp).reshape(N, NH * Fp)).to(device)
+        Wh.view(N, NH, Fp)[:, :, F:] = 0
+        a = torch.from_numpy(gd.xavier_uniform(4, NH, NH * 2 * F)).to(device)
+        S = torch.full((N, 2 * NH), float("nan"), device=device)
+        call("gatx_node_scores", ptr(Wh), N, NH, F, ptr(a), ptr(S), stream())
+        A = a.view(NH, NH, 2, F)
+        Whv = Wh.view(N, NH, Fp)[:, :, :F].double()
+        ref_src = torch.einsum("nkf,hkf->nh", Whv, A[:, :, 0].double())
+        ref_dst = torch.einsum("nkf,hkf->nh", Whv, A[:, :, 1].double())
+        torch.cuda.synchronize()
+        tol = 1e-5 * max(1.0, (NH * F) ** 0.5) * 10
+        assert (S[:, :NH].double() - ref_src).abs().max().item() < tol, (NH, F)
+        assert (S[:, NH:].double() - ref_dst).abs().max().item() < tol, (NH, F)

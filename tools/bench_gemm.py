@@ -44,12 +44,14 @@ for name, M, Nc, K, lay in shapes:
         args = (M, Nc, K, ptr(A), 1, M, ptr(B), Nc, 1)
         ref = lambda: torch.mm(A.t(), B)
     res = []
-    for wm in (2, 4):
-        _lib.lib.gatx_set_gemm_rows(64 * wm)
-        f = lambda: call("gatx_gemm_f32", *args, ptr(C), Nc, Nc, None, 0, 0, stream())
+    for mode in ("tail", "plain"):
+        wb = _lib.lib.gatx_gemm_workspace_bytes(M, Nc, K) if mode == "tail" else 0
+        wt = torch.empty(max(wb, 1), dtype=torch.uint8, device=dev)
+        wp = ptr(wt) if wb else None
+        f = lambda: call("gatx_gemm_f32", *args, ptr(C), Nc, Nc, None, 0, 0, wp, wb, stream())
         t = timeit(f)
         err = (C - ref()).abs().max().item()
-        res.append(f"wm{wm} {t*1e3:8.1f}us {flops/t/1e9:6.1f}TF err={err:.1e}")
+        res.append(f"{mode} {t*1e3:8.1f}us {flops/t/1e9:6.1f}TF err={err:.1e}")
     if lay == "tn":
         wsb = _lib.lib.gatx_gemm_splitk_workspace_bytes(M, Nc, K)
         ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
