@@ -83,6 +83,7 @@ struct EdgeFwdArgs {
   int lds_row;
   int64_t chunk;           // destination nodes per (chunk, head-group) sweep
   int64_t n_items;
+  int vec_out;             // concat output / resid rows float4-aligned (F % 4 == 0)
   int dbg;                 // diagnostic ablations (gatx_set_debug); 0 in production
 };
 
@@ -102,7 +103,8 @@ __device__ inline float epilogue(float v, const EdgeFwdArgs& g, int64_t n, int64
   return v;
 }
 
-constexpr int kMaxHS = 8;   // heads per work item held in registers by the batch phase
+constexpr int kMaxHS = 8;
+typedef float f4v __attribute__((ext_vector_type(4)));   // heads per work item held in registers by the batch phase
 
 __device__ inline int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ inline float lane_f(float v, int j) {
@@ -289,9 +291,22 @@ __global__ void __launch_bounds__(256) edge_forward_kernel(EdgeFwdArgs g) {
       if (g.concat) {
         float* orow = g.out + n * g.out_ld;
         const int64_t cb = (int64_t)h * F + f0;
-        if ((F & 3) == 0 && !g.resid && !g.elu) {
-          const float4 b = g.bias ? *(const float4*)(g.bias + cb) : make_float4(0.f, 0.f, 0.f, 0.f);
-          *(float4*)(orow + cb) = add4(o, b);
+        if (g.vec_out) {
+          // out / resid are streamed once: non-temporal, so they do not evict the gathered rows
+          float4 r = g.bias ? *(const float4*)(g.bias + cb) : make_float4(0.f, 0.f, 0.f, 0.f);
+          r = add4(o, r);
+          if (g.resid) {
+            const f4v rv = __builtin_nontemporal_load((const f4v*)(g.resid + n * g.resid_ld + cb));
+            r.x += rv[0]; r.y += rv[1]; r.z += rv[2]; r.w += rv[3];
+          }
+          if (g.elu) {
+            r.x = r.x > 0.f ? r.x : expm1f(r.x);
+            r.y = r.y > 0.f ? r.y : expm1f(r.y);
+            r.z = r.z > 0.f ? r.z : expm1f(r.z);
+            r.w = r.w > 0.f ? r.w : expm1f(r.w);
+          }
+          const f4v ov = {r.x, r.y, r.z, r.w};
+          __builtin_nontemporal_store(ov, (f4v*)(orow + cb));
         } else {
 #pragma unroll
           for (int j = 0; j < 4; ++j)
@@ -713,8 +728,6 @@ extern "C" int gatx_edge_forward_ex(
   GATX_REQUIRE(p >= 0.f && p < 1.f, "edge_forward: dropout must be in [0, 1)");
   if (N == 0) return 0;
   const int Fp = (int)round_up(F, 4);
-  GATX_REQUIRE(!(concat && (F & 3) == 0 && !resid && !elu) || out_ld % 4 == 0,
-               "edge_forward: out row stride must be a multiple of 4");
   const int64_t D4 = (int64_t)HS * Fp / 4;
   const RowGeom rg = row_geom(D4);
   GATX_REQUIRE(rg.cpl <= 8, "edge_forward: heads_per_item*out_features > 2048 unsupported");
@@ -725,6 +738,9 @@ extern "C" int gatx_edge_forward_ex(
   g.bias = bias; g.p_drop = p; g.seed = seed; g.out = out; g.out_ld = out_ld;
   g.resid = resid; g.resid_ld = resid_ld; g.elu = elu;
   g.den = den;
+  g.vec_out = concat && (F & 3) == 0 && out_ld % 4 == 0 && ((uintptr_t)out % 16) == 0 &&
+              (!resid || (resid_ld % 4 == 0 && ((uintptr_t)resid % 16) == 0)) &&
+              (!bias || ((uintptr_t)bias % 16) == 0);
   GATX_REQUIRE(HS <= kMaxHS, "edge_forward: more than %d heads per work item", kMaxHS);
   g.lds_row = (int)round_up((int64_t)HS * Fp + HS + 64 + (int64_t)HS * 64, 4);
   g.chunk = chunk > 0 ? chunk : 2048;

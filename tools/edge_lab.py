@@ -28,7 +28,7 @@ def timeit(fn, reps=10):
     return s.elapsed_time(e) / reps * 1e3
 
 
-for (NH, F, concat) in [(4, 256, 1), (6, 121, 0)]:
+for (NH, F, concat) in [(4, 256, 1), (6, 121, 0), (6, 121, 1)]:
     Fp = (F + 3) // 4 * 4
     Wh = torch.randn(N, NH * Fp, device=dev)
     S = torch.randn(N, 2 * NH, device=dev)
@@ -40,9 +40,9 @@ for (NH, F, concat) in [(4, 256, 1), (6, 121, 0)]:
     den = torch.empty(N, NH, device=dev)
     am = torch.zeros(ARGMAX_CAP + 2, dtype=torch.int64, device=dev)
     alg = 4.0 * E2 * NH * F
-    for hs in ([1, 2, 4] if concat else [6]):
-        for chunk in ([512, 2048, 8192] if hs == 1 else [2048]):
-            for dbg in (0, 2):
+    for hs in ([d for d in (1, 2, 3, 4, 6) if NH % d == 0] if concat else [NH]):
+        for chunk in ([1024, 2048, 4096] if hs <= 2 else [2048]):
+            for dbg in (0,):
                 lib.gatx_set_debug(dbg)
                 f = lambda: call("gatx_edge_forward_ex", ptr(Wh), NH * Fp, Fp, ptr(S), ptr(M),
                                  ptr(g.rowptr), ptr(g.col), ptr(g.perm), N, NH, F, hs, concat, 0,
