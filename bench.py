@@ -94,6 +94,140 @@ def cpu_baseline(model_np, cfg, budget_s=20.0):
                       f"(N={b.num_nodes}, sum E'={e_tot}), best of {len(times)}: {best:.2f} s"}
 
 
+def cpu_baseline_rmat(W, a, NH, F, budget_s=20.0):
+    """The numpy oracle on a scaled RMAT (1e5 nodes / 1.6e6 edges, SURVEY.md §8d 'RMAT on CPU'),
+    one GATLayer forward (F_in 512 -> 8 x 64 concat)."""
+    from oracle import gat_oracle as orc
+    from gatx import data as gd
+    try:
+        from threadpoolctl import threadpool_limits
+    except Exception:  # pragma: no cover
+        threadpool_limits = None
+    cores = min(16, len(os.sched_getaffinity(0)))
+    n, e = 100_000, 1_600_000
+    ei = gd.rmat_edges(n, e, seed=4242)
+    x = gd.normal(7, n * W.shape[1]).reshape(n, W.shape[1])
+    ctx = threadpool_limits(limits=cores) if threadpool_limits else None
+    times, E2 = [], 0
+    try:
+        t_start = time.perf_counter()
+        while True:
+            t0 = time.perf_counter()
+            out, ei2, alpha, _ = orc.gat_layer_forward(x, ei, W, a, NH, F, True)
+            times.append(time.perf_counter() - t0)
+            E2 = alpha.shape[0]
+            if time.perf_counter() - t_start > budget_s or len(times) >= 3:
+                break
+    finally:
+        if ctx is not None:
+            ctx.__exit__(None, None, None)
+    best = min(times)
+    return {"value": E2 / best, "unit": "layer-edges/s", "cores": cores, "kind": "port",
+            "sample": f"numpy oracle (reference dataflow), 1 GATLayer fwd on a SCALED RMAT "
+                      f"(N={n}, E'={E2}; the full 1e7/1.6e8 graph is infeasible on CPU), best of "
+                      f"{len(times)}: {best:.2f} s"}
+
+
+def run_rmat(args, world, rank, dev):
+    """BASELINE config 5: one GATLayer (F_in 512 -> 8 heads x 64, concat, self-loops) forward on
+    a synthetic R-MAT graph (1e7 nodes, 1.6e8 edges), eval mode, CSR built per step. One graph,
+    no sharding: with --gpus N each rank runs an independent replica (value sums them)."""
+    from gatx import GATLayer, clear_graph_cache
+    from gatx import data as gd
+    from gatx.functional import KernelTimer, set_kernel_timer
+    NH, F, FIN = 8, 64, 512
+    N, E = args.rmat_nodes, args.rmat_edges
+    torch.manual_seed(0)
+    layer = GATLayer(FIN, F, NH, True, add_self_loops=True).to(dev).eval()
+    ei = gd.rmat_edges_device(N, E, seed=42 + rank, device=dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(1 + rank)
+    x = torch.randn(N, FIN, device=dev, generator=g)
+
+    def step():
+        clear_graph_cache()
+        with torch.no_grad():
+            return layer(x, ei)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    from gatx.graph import graph_cache
+    E2 = graph_cache.get(ei, N, True).num_edges
+    timer = KernelTimer()
+    set_kernel_timer(timer)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    set_kernel_timer(None)
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms = elapsed / args.steps * 1e3
+    alg = algorithmic(N, E2, FIN, NH, F, True)
+    summ = timer.summary()
+    kern = {}
+    for phase, recs in summ.items():
+        tot = sum(t for _, t in recs)
+        kern[phase] = {"launches": len(recs), "avg_ms": tot / len(recs),
+                       "total_ms_per_step": tot / args.steps}
+    roofs = []
+    edg = summ.get("edge_forward", [])
+    if edg:
+        by = alg["b_edge_fwd"] - 4.0 * E2 * NH     # alpha is written by attention_alpha
+        ms_ = sum(t for _, t in edg) / len(edg)
+        gbs = by / (ms_ * 1e-3) / 1e9
+        roofs.append({"bound": "hbm", "kernel": "edge_forward_kernel (Wh[src] row gathers)",
+                      "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                      "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                      "bytes_per_launch": by, "avg_launch_ms": ms_, "_ms": ms_})
+    gem = summ.get("gemm", [])
+    if gem:
+        fl = 2.0 * N * FIN * NH * F
+        ms_ = sum(t for _, t in gem) / len(gem)
+        tfs = fl / (ms_ * 1e-3) / 1e12
+        roofs.append({"bound": "mfma", "kernel": "gemm_f32_kernel (projection x.W^T)",
+                      "achieved": round(tfs, 2), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                      "frac": round(tfs / FP32_MFMA_PEAK_TFS, 4), "traffic": None,
+                      "flops_per_launch": fl, "avg_launch_ms": ms_, "_ms": ms_})
+    roofs.sort(key=lambda r: -r["_ms"])
+    for r in roofs:
+        r.pop("_ms")
+    result = {
+        "metric": "GAT-layer edges/sec + achieved HBM GB/s, RMAT 1-layer fwd",
+        "value": round(E2 * world / (elapsed / args.steps), 1), "unit": "layer-edges/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic R-MAT (a,b,c,d)=(0.57,0.19,0.19,0.05), ids permuted, x ~ N(0,1), "
+                "xavier weights",
+        "config": {"workload": f"RMAT {N} nodes / {E} edges, GATLayer 512 -> 8x64 concat, "
+                               "self-loops, eval, CSR built per step",
+                   "nodes": N, "edges_in": int(ei.size(1)), "edges_per_layer": E2,
+                   "parallelism": "replicas" if world > 1 else "single GPU"},
+        "achieved_GBps_algorithmic_per_gpu": round((alg["b_gemm"] + alg["b_edge"])
+                                                   / (elapsed / args.steps) / 1e9, 1),
+        "roofline_time_frac": round(max((alg["b_gemm"] + alg["b_edge"]) / (HBM_PEAK_GBS * 1e9),
+                                        alg["f_gemm"] / (FP32_MFMA_PEAK_TFS * 1e12))
+                                    / (ms * 1e-3), 4),
+        "roofline": roofs[0] if roofs else None,
+        "roofline_other": roofs[1] if len(roofs) > 1 else None,
+        "kernels": kern,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline_rmat(layer.W.weight.detach().cpu().numpy(),
+                                                   layer.a.weight.detach().cpu().numpy(), NH, F)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -102,6 +236,11 @@ def main():
     ap.add_argument("--graphs", type=int, default=20, help="PPI graphs per rank")
     ap.add_argument("--mode", choices=["fwd", "train"], default="fwd")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--attention-penalty", type=float, default=0.0,
+                    help="PPI_GAT attention_penalty (train mode)")
+    ap.add_argument("--workload", choices=["ppi", "rmat"], default="ppi")
+    ap.add_argument("--rmat-nodes", type=int, default=10_000_000)
+    ap.add_argument("--rmat-edges", type=int, default=160_000_000)
     ap.add_argument("--cached-graph", action="store_true",
                     help="reuse the CSR across steps (excludes graph preprocessing)")
     args = ap.parse_args()
@@ -113,6 +252,11 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     dev = torch.device(f"cuda:{local}")
+    if args.workload == "rmat":
+        run_rmat(args, world, rank, dev)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     from gatx import GATModel, clear_graph_cache
     from gatx import data as gd
@@ -140,8 +284,13 @@ def main():
         if args.mode == "fwd":
             with torch.no_grad():
                 return model(x, ei)
-        out, _, atts = model.forward_and_return_attention(x, ei)
+        # PPI_GAT.training_step (models/ppi_gat.py:15-33): BCE + the attention norm, computed
+        # every step (logged; added to the loss only with a non-zero attention_penalty)
+        out, ei2, atts = model.forward_and_return_attention(x, ei)
         loss = loss_fn(out, y)
+        attention_norm = model.calc_attention_norm(ei2, atts)
+        if args.attention_penalty != 0.0:
+            loss = loss + args.attention_penalty * attention_norm
         opt.zero_grad(set_to_none=True)
         loss.backward()
         if world > 1:   # one flat bucket (7.47 MB) all-reduced over RCCL
@@ -196,12 +345,12 @@ def main():
         fl = sum(2.0 * n * fin * nh * f + 4.0 * n * nh * nh * f for (n, _, fin, nh, f), _ in gem)
         ms_ = sum(t for _, t in gem)
         tfs = fl / (ms_ * 1e-3) / 1e12
-        roofs["gemm"] = {"bound": "mfma", "kernel": "gemm_f32_kernel<true, false, 2, 0> "
+        roofs["gemm"] = {"bound": "mfma", "kernel": "gemm_f32_kernel<true, true, true, 0, 16, 4> "
                          "(projection x.W_aug^T, layers 1-2)", "achieved": round(tfs, 2),
                          "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                          "frac": round(tfs / FP32_MFMA_PEAK_TFS, 4), "traffic": None,
                          "flops_per_launch": fl / len(gem), "avg_launch_ms": ms_ / len(gem),
-                         "_prefix": "gemm_f32_kernel<true, false, 2, 0>", "_ms": ms_}
+                         "_prefix": "gemm_f32_kernel<true, true, true, 0,", "_ms": ms_}
     edg = summ.get("edge_forward", [])
     if edg:
         by = 0.0

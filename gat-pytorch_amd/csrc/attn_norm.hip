@@ -1,0 +1,119 @@
+// Attention-norm regulariser of GATModel.calc_attention_norm (models/GATModel.py:189-234),
+// fused over the CSR of edge_index':
+//   norm_l = sum_{e,h} | alpha_l[e,h] * deg[dst_e] - 1 | / E'     (torch.norm(p=1) / E', :224-225)
+//   result = mean over layers                                          (:230)
+// deg[dst] is the in-degree over edge_index' (the reference's scatter of ones over
+// edge_index[1], :195-200) = rowptr[dst+1] - rowptr[dst]. One pass per layer reads alpha once
+// (edge_index' order, reached through the CSR's perm) instead of building (E', NH) temporaries.
+// The gradient is sign(alpha*deg - 1) * deg * g / (E' * L) (torch's |x|' = sgn x, 0 at 0).
+// Sums: per-thread partials, a fixed-order block tree and one fixed-order final pass, so the
+// result is bitwise reproducible.
+#include "gatx_common.h"
+
+namespace gatx {
+namespace {
+
+constexpr int kNormBlocks = 1024;
+
+__device__ inline float deg_of(const int32_t* __restrict__ rowptr, int32_t d) {
+  return (float)(rowptr[d + 1] - rowptr[d]);
+}
+
+// alpha * deg - 1 with the product and the difference each rounded, as torch's two fp32 ops:
+// an FMA would return the exact residual where the reference gets 0 (and a zero gradient).
+__device__ inline float excess(float a, float deg) {
+#pragma clang fp contract(off)
+  const float p = a * deg;
+  return p - 1.f;
+}
+
+__global__ void __launch_bounds__(256) attn_norm_partial_kernel(
+    const float* __restrict__ alpha, int64_t E2, int NH, const int32_t* __restrict__ perm,
+    const int32_t* __restrict__ rowidx, const int32_t* __restrict__ rowptr,
+    float* __restrict__ part) {
+  float s = 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < E2;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float deg = deg_of(rowptr, rowidx[i]);
+    const float* a = alpha + (int64_t)perm[i] * NH;
+    for (int h = 0; h < NH; ++h) s += fabsf(excess(a[h], deg));
+  }
+  s = group_sum<64>(s);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ void __launch_bounds__(256) attn_norm_final_kernel(const float* __restrict__ part,
+                                                              int nb, float scale, int accumulate,
+                                                              float* __restrict__ out) {
+  float s = 0.f;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) s += part[b];
+  s = group_sum<64>(s);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float v = ((red[0] + red[1]) + (red[2] + red[3])) * scale;
+    out[0] = accumulate ? out[0] + v : v;
+  }
+}
+
+__global__ void __launch_bounds__(256) attn_norm_backward_kernel(
+    const float* __restrict__ alpha, int64_t E2, int NH, const int32_t* __restrict__ perm,
+    const int32_t* __restrict__ rowidx, const int32_t* __restrict__ rowptr,
+    const float* __restrict__ g, float scale, float* __restrict__ g_alpha) {
+  const float gs = g[0] * scale;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < E2;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float deg = deg_of(rowptr, rowidx[i]);
+    const int64_t e = perm[i];
+    for (int h = 0; h < NH; ++h) {
+      const float t = excess(alpha[e * NH + h], deg);
+      const float sg = t > 0.f ? 1.f : (t < 0.f ? -1.f : 0.f);
+      g_alpha[e * NH + h] = gs * sg * deg;
+    }
+  }
+}
+
+inline unsigned grid_for(int64_t n, int64_t cap) {
+  const int64_t g = ceil_div(n > 0 ? n : 1, 256);
+  return (unsigned)(g < cap ? g : cap);
+}
+
+}  // namespace
+}  // namespace gatx
+
+using namespace gatx;
+
+extern "C" size_t gatx_attention_norm_workspace_bytes(void) {
+  return sizeof(float) * kNormBlocks;
+}
+
+extern "C" int gatx_attention_norm(const float* alpha, int64_t E2, int NH, const int32_t* perm,
+                                   const int32_t* rowidx, const int32_t* rowptr, float scale,
+                                   int accumulate, float* out, void* workspace,
+                                   gatx_stream_t s) {
+  GATX_REQUIRE(E2 >= 0 && NH >= 1, "attention_norm: bad sizes");
+  hipStream_t st = (hipStream_t)s;
+  const unsigned nb = grid_for(E2, kNormBlocks);
+  float* part = (float*)workspace;
+  attn_norm_partial_kernel<<<nb, 256, 0, st>>>(alpha, E2, NH, perm, rowidx, rowptr, part);
+  GATX_LAUNCH_CHECK("attention_norm");
+  attn_norm_final_kernel<<<1, 256, 0, st>>>(part, (int)nb, scale, accumulate, out);
+  GATX_LAUNCH_CHECK("attention_norm_final");
+  return 0;
+}
+
+extern "C" int gatx_attention_norm_backward(const float* alpha, int64_t E2, int NH,
+                                            const int32_t* perm, const int32_t* rowidx,
+                                            const int32_t* rowptr, const float* g, float scale,
+                                            float* g_alpha, gatx_stream_t s) {
+  GATX_REQUIRE(E2 >= 0 && NH >= 1, "attention_norm_backward: bad sizes");
+  if (E2 == 0) return 0;
+  attn_norm_backward_kernel<<<grid_for(E2, 8192), 256, 0, (hipStream_t)s>>>(
+      alpha, E2, NH, perm, rowidx, rowptr, g, scale, g_alpha);
+  GATX_LAUNCH_CHECK("attention_norm_backward");
+  return 0;
+}

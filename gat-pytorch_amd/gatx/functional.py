@@ -387,3 +387,53 @@ def gat_layer(x, edge_index, W, a, bias, num_heads, out_features, concat, add_se
     out, alpha = GATLayerFunction.apply(x, W, a, bias, resid, graph, sh, float(dropout_p),
                                         int(seed), bool(elu))
     return out, graph.edge_index, alpha
+
+
+class AttentionNormFunction(torch.autograd.Function):
+    """mean over layers of ||alpha_l * deg[dst] - 1||_1 / E' (`models/GATModel.py:189-234`) on
+    gatx_attention_norm: one fused pass per layer over the CSR, gradient by
+    gatx_attention_norm_backward."""
+
+    @staticmethod
+    def forward(ctx, graph, *alphas):
+        E2 = graph.num_edges
+        L = len(alphas)
+        dev = alphas[0].device
+        out = torch.empty(1, dtype=torch.float32, device=dev)
+        ws = torch.empty(lib.gatx_attention_norm_workspace_bytes(), dtype=torch.uint8, device=dev)
+        scale = 1.0 / (E2 * L) if E2 else float("nan")
+        s = stream()
+        alphas = tuple(a.contiguous() for a in alphas)
+        for i, a in enumerate(alphas):
+            _require(a, "attention")
+            if a.dim() != 2 or a.size(0) != E2:
+                raise RuntimeError(f"attention {i} has shape {tuple(a.shape)}, edge_index has "
+                                   f"{E2} edges")
+            call("gatx_attention_norm", ptr(a), E2, a.size(1), ptr(graph.perm), ptr(graph.rowidx),
+                 ptr(graph.rowptr), scale, int(i > 0), ptr(out), ptr(ws), s)
+        ctx.graph, ctx.scale = graph, scale
+        ctx.save_for_backward(*alphas)
+        return out.view(())
+
+    @staticmethod
+    def backward(ctx, g):
+        graph = ctx.graph
+        E2 = graph.num_edges
+        g = g.to(torch.float32).contiguous().view(1)
+        grads = []
+        for a in ctx.saved_tensors:
+            ga = torch.empty_like(a)
+            call("gatx_attention_norm_backward", ptr(a), E2, a.size(1), ptr(graph.perm),
+                 ptr(graph.rowidx), ptr(graph.rowptr), ptr(g), ctx.scale, ptr(ga), stream())
+            grads.append(ga)
+        return (None, *grads)
+
+
+def attention_norm(edge_index, attention_list):
+    """Functional GATModel.calc_attention_norm on the device (edge_index: the layers'
+    edge_index', attention_list: their alphas)."""
+    from .graph import graph_cache
+    if not attention_list:
+        raise RuntimeError("attention_norm: empty attention list")
+    graph = graph_cache.for_edges(edge_index)
+    return AttentionNormFunction.apply(graph, *attention_list)

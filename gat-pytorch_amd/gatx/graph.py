@@ -24,7 +24,8 @@ class Graph:
     rowptr [N+1], col [E2] (source), rowidx [E2] (destination), perm [E2] (CSR slot -> position
     in edge_index'); srowptr / scol / seid: the source-ordered transpose, built on first use."""
 
-    def __init__(self, edge_index: torch.Tensor, num_nodes: int, add_self_loops: bool):
+    def __init__(self, edge_index: torch.Tensor, num_nodes, add_self_loops: bool):
+        """num_nodes None: size the node range from the edges (max id + 1)."""
         if edge_index.dim() != 2 or edge_index.size(0) != 2:
             raise RuntimeError(f"edge_index must have shape (2, E), got {tuple(edge_index.shape)}")
         if edge_index.dtype not in (torch.int64, torch.int32):
@@ -35,7 +36,6 @@ class Graph:
         if edge_index.stride(1) != 1:
             edge_index = edge_index.contiguous()
         self.device = dev
-        self.num_nodes = N = int(num_nodes)
         self.add_self_loops = add_self_loops
         E = edge_index.size(1)
         is64 = int(edge_index.dtype == torch.int64)
@@ -50,6 +50,9 @@ class Graph:
                           device=dev)
         call("gatx_edge_stats", ptr(edge_index), is64, E, ld, ptr(stats), ptr(sws), s)
         mn, mx, nloops = (int(v) for v in stats.cpu())   # the one host sync per new graph
+        if num_nodes is None:
+            num_nodes = mx + 1 if E else 0
+        self.num_nodes = N = int(num_nodes)
         if E and mn < 0:
             raise RuntimeError(f"index {mn} is out of bounds: edge_index has negative node ids")
         if E and mx >= N:
@@ -123,6 +126,26 @@ class GraphCache:
         self._put(k, edge_index, g)
         if add_self_loops:
             self._put(self._key(g.edge_index, num_nodes, True), g.edge_index, g)
+        return g
+
+    def for_edges(self, edge_index: torch.Tensor) -> Graph:
+        """The Graph whose edge_index' IS this tensor (what a layer returned), else a CSR of it
+        as given (no rewrite), sized by its max id — for consumers of a layer's output edges
+        such as the attention-norm regulariser."""
+        for t, g in reversed(self._d.values()):
+            ei = g.edge_index
+            if ei is edge_index or (ei.data_ptr() == edge_index.data_ptr()
+                                    and ei._version == edge_index._version
+                                    and ei.shape == edge_index.shape
+                                    and ei.stride() == edge_index.stride()
+                                    and ei.dtype == edge_index.dtype):
+                return g
+        k = self._key(edge_index, -1, False)
+        hit = self._d.get(k)
+        if hit is not None:
+            return hit[1]
+        g = Graph(edge_index, None, False)
+        self._put(k, edge_index, g)
         return g
 
     def _put(self, k, t, g):

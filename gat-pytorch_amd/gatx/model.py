@@ -90,17 +90,10 @@ class GATModel(nn.Module):
 
     @staticmethod
     def calc_attention_norm(edge_index, attention_list):
-        """mean over layers of ||alpha * in_degree[dst] - 1||_1 / E (`models/GATModel.py:189-234`)."""
-        dst = edge_index[1]
-        E = dst.numel()
-        first = attention_list[0]
-        deg = torch.zeros(E, dtype=first.dtype, device=first.device)
-        deg.scatter_add_(0, dst, torch.ones(E, dtype=first.dtype, device=first.device))
-        deg = deg.index_select(0, dst)
-        norm = torch.zeros((), dtype=first.dtype, device=first.device)
-        for att in attention_list:
-            norm = norm + torch.norm(att * deg.unsqueeze(-1) - 1.0, p=1) / E
-        return norm / len(attention_list)
+        """mean over layers of ||alpha * in_degree[dst] - 1||_1 / E (`models/GATModel.py:189-234`),
+        fused on the device (gatx_attention_norm; degrees from the cached CSR of edge_index')."""
+        from .functional import attention_norm
+        return attention_norm(edge_index, attention_list)
 
     def configure_optimizers(self):
         return torch.optim.Adam(self.parameters(), lr=self.lr, weight_decay=self.l2_reg)

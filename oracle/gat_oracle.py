@@ -227,3 +227,18 @@ def calc_attention_norm(edge_index, attention_list):
     for al in attention_list:
         tot = tot + np.abs(al * deg[:, None] - 1.0).sum() / E
     return tot / len(attention_list)
+
+
+def calc_attention_norm_grad(edge_index, attention_list, g=1.0):
+    """Gradient of calc_attention_norm w.r.t. each alpha: g * sgn(alpha*deg - 1) * deg / (E*L)
+    (torch's d|x|/dx = sgn x, 0 at 0)."""
+    dst = edge_index[1].astype(np.int64)
+    E = dst.shape[0]
+    deg = segment_sum(np.ones(E, dtype=np.float64), dst, E)[dst]
+    L = len(attention_list)
+    out = []
+    for al in attention_list:
+        d = deg.astype(al.dtype)[:, None]
+        t = al * d - al.dtype.type(1.0)   # in alpha's precision, like the reference's fp32
+        out.append(g * np.sign(t).astype(np.float64) * deg[:, None] / (E * L))
+    return out

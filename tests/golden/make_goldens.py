@@ -31,6 +31,7 @@ sys.path.insert(0, "/root/reference")
 sys.dont_write_bytecode = True
 
 from models.gat_layer import GATLayer  # noqa: E402  (the reference)
+from models.utils import explicit_broadcast, sum_over_neighbourhood  # noqa: E402  (the reference)
 from gatx import data as gdata  # noqa: E402
 from gatx.checkpoint import read_state_dict  # noqa: E402
 from oracle.gat_oracle import dropout_keep  # noqa: E402
@@ -136,10 +137,29 @@ def gen_batch(gen):
     return b.x, b.edge_index
 
 
-def main():
+def ref_attention_norm(edge_index, alphas):
+    """GATModel.calc_attention_norm (`models/GATModel.py:189-230`, logging removed) on the
+    reference's own helpers; returns the value and d value / d alpha_l for an upstream 1."""
+    att = [torch.from_numpy(a).requires_grad_(True) for a in alphas]
+    nb = edge_index[1]
+    first = att[0]
+    degrees = sum_over_neighbourhood(torch.ones_like(first[:, 0]), neighbourhood_indices=nb,
+                                     aggregated_shape=first[:, 0].size(), broadcast_back=True)
+    norm = torch.tensor(0.0)
+    for a in att:
+        tmp = explicit_broadcast(degrees, a)
+        norm = norm + torch.norm(a * tmp - 1.0, p=1) / nb.size(0)
+    norm = norm / torch.tensor(len(att))
+    norm.backward()
+    return norm.detach().numpy(), [a.grad.numpy() for a in att]
+
+
+def main(models_only=False):
     torch.set_num_threads(8)
     sd_cora = read_state_dict(f"{CKPT}/Cora-100epochs.ckpt")
     sd_pat = read_state_dict(f"{CKPT}/PATTERN-100epochs.ckpt")
+    if models_only:
+        return model_cases(sd_pat)
 
     # 1-3: Cora shapes (SURVEY.md §8c goldens 1-2), trained and xavier weights
     gen = dict(G=1, n=2708, e=10556, in_features=1433, features="bernoulli")
@@ -218,6 +238,10 @@ def main():
     run_layer_case("edge_odd_widths", rng_x(70, 13, 81), ei, 13, 7, 5, True,
                    gdata.xavier_uniform(82, 35, 13), gdata.xavier_uniform(83, 5, 70))
 
+    model_cases(sd_pat)
+
+
+def model_cases(sd_pat):
     # 7: model level — PATTERN 4 layers with trained weights (golden 4), 2 graphs
     gp = dict(G=2, n=119, e=6099, in_features=3, feature_seed=13)
     xp, ep = gen_batch(gp)
@@ -279,9 +303,14 @@ def model_case(name, x, ei, gen, layers, skips, dataset, wgen=None):
     put(store, "out", xt.numpy())
     for i, al in enumerate(alphas):
         put(store, f"alpha{i}", al)
+    # calc_attention_norm over the returned edge_index' and alphas (+ its gradient, upstream 1)
+    norm, grads = ref_attention_norm(edge_index, alphas)
+    store["attention_norm"] = norm
+    for i, g in enumerate(grads):
+        put(store, f"attention_norm_grad{i}", g)
     np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **store)
     print(f"{name}: N={x.shape[0]} out={tuple(xt.shape)}")
 
 
 if __name__ == "__main__":
-    main()
+    main(models_only="--models-only" in sys.argv)

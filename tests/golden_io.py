@@ -118,5 +118,9 @@ def load_model_case(name):
     exp = {"out": Expected(z, "out")}
     for i in range(L):
         exp[f"alpha{i}"] = Expected(z, f"alpha{i}")
+        if f"attention_norm_grad{i}" in z or f"attention_norm_grad{i}__rows" in z:
+            exp[f"attention_norm_grad{i}"] = Expected(z, f"attention_norm_grad{i}")
+    if "attention_norm" in z:
+        exp["attention_norm"] = float(z["attention_norm"])
     return dict(meta=meta, cfg=cfg, x=x, edge_index=ei, layers=layers, skips=skips,
                 expected=exp, edge_index_out=z["edge_index_out"])

@@ -348,3 +348,131 @@ def test_gemm_splitk_and_node_scores(device):
         tol = 1e-5 * max(1.0, (NH * F) ** 0.5) * 10
         assert (S[:, :NH].double() - ref_src).abs().max().item() < tol, (NH, F)
         assert (S[:, NH:].double() - ref_dst).abs().max().item() < tol, (NH, F)
+
+
+@pytest.mark.parametrize("name", MODEL_CASES)
+def test_attention_norm_matches_reference(name, device):
+    """Fused calc_attention_norm (gatx_attention_norm) on the reference's own alphas and
+    edge_index' against the reference value and gradient (goldens), and through GATModel on the
+    HIP path's alphas."""
+    gatx = _gatx()
+    from gatx.functional import attention_norm
+    c = load_model_case(name)
+    e = c["expected"]
+    L = len(c["layers"])
+    ei = torch.from_numpy(c["edge_index_out"]).to(device)
+    alphas = [torch.from_numpy(e[f"alpha{i}"].full).to(device).requires_grad_(True)
+              for i in range(L)]
+    v = attention_norm(ei, alphas)
+    ref = e["attention_norm"]
+    assert abs(v.item() - ref) <= 1e-5 * max(1.0, abs(ref)), (v.item(), ref)
+    v.backward()
+    for i, a in enumerate(alphas):
+        e[f"attention_norm_grad{i}"].check(a.grad.cpu().numpy(), 1e-7)
+    # bitwise reproducible
+    assert attention_norm(ei, alphas).item() == v.item()
+    # the model path: alphas of the HIP layers, edge_index' returned by the HIP layers
+    cfg = c["cfg"]
+    model = gatx.GATModel(**cfg).to(device).eval()
+    with torch.no_grad():
+        for i, (W, a) in enumerate(c["layers"]):
+            model.gat_layer_list[i].W.weight.copy_(torch.from_numpy(W))
+            model.gat_layer_list[i].a.weight.copy_(torch.from_numpy(a))
+        for j, s in enumerate(c["skips"]):
+            if s is not None:
+                model.skip_layer_list[j].weight.copy_(torch.from_numpy(s))
+        out, ei2, atts = model.forward_and_return_attention(
+            torch.from_numpy(c["x"]).to(device), torch.from_numpy(c["edge_index"]).to(device))
+        mv = model.calc_attention_norm(ei2, atts).item()
+    assert abs(mv - ref) <= 1e-3 * max(1.0, abs(ref)), (mv, ref)
+
+
+def test_attention_norm_edge_cases(device):
+    """Zero terms (alpha * deg == 1 exactly) get a zero gradient; E' = 0 gives nan like 0/0."""
+    from gatx.functional import attention_norm
+    ei = torch.tensor([[0, 1, 2, 0], [1, 1, 2, 2]], device=device)   # deg: 1 -> 2, 2 -> 2
+    al = torch.tensor([[0.5], [0.5], [0.25], [2.0]], device=device, requires_grad=True)
+    v = attention_norm(ei, [al])
+    # |0.5*2-1| + |0.5*2-1| + |0.25*2-1| + |2*2-1| = 0 + 0 + 0.5 + 3 = 3.5, / E=4
+    assert v.item() == pytest.approx(3.5 / 4, abs=1e-7)
+    v.backward()
+    np.testing.assert_allclose(al.grad.cpu().numpy()[:, 0], [0, 0, -2 / 4, 2 / 4], atol=1e-7)
+
+
+def test_rmat_full_size(device):
+    """BASELINE config 5 at full size (1e7 nodes, 1.6e8 R-MAT edges, 512 -> 8 x 64 concat):
+    size-independent properties over the whole graph plus exact fp64 checks of sampled
+    destinations, including the highest in-degree one (the skewed segment)."""
+    free, total = torch.cuda.mem_get_info()
+    if free < 120 * 2 ** 30:
+        pytest.skip(f"needs ~100 GB of device memory, {free / 2**30:.0f} GB free")
+    gatx = _gatx()
+    from gatx import data as gd
+    from gatx.graph import graph_cache
+    N, E, NH, F, FIN = 10_000_000, 160_000_000, 8, 64, 512
+    ei = gd.rmat_edges_device(N, E, seed=42, device=device)
+    torch.manual_seed(0)
+    layer = gatx.GATLayer(FIN, F, NH, True, add_self_loops=True).to(device).eval()
+    g = torch.Generator(device=device)
+    g.manual_seed(1)
+    x = torch.randn(N, FIN, device=device, generator=g)
+    with torch.no_grad():
+        out, (ei2, alpha) = layer(x, ei, return_attention_weights=True)
+    torch.cuda.synchronize()
+    graph = graph_cache.get(ei, N, True)
+    E2 = graph.num_edges
+    # edge_index' = [input edges without self-loops, in input order | (i, i) for i < max+1]
+    keep = ei[0] != ei[1]
+    nk = int(keep.sum())
+    n_idx = int(ei.max()) + 1
+    assert E2 == nk + n_idx and tuple(ei2.shape) == (2, E2)
+    assert torch.equal(ei2[:, :nk], ei[:, keep])
+    ar = torch.arange(n_idx, device=device)
+    assert torch.equal(ei2[0, nk:], ar) and torch.equal(ei2[1, nk:], ar)
+    del keep, ar
+    # every destination's alpha sums to den / (den + 1e-8) = 1 (each node has its self-loop)
+    seg = torch.zeros(n_idx, NH, dtype=torch.float64, device=device)
+    seg.index_add_(0, ei2[1], alpha.double())
+    assert float((seg - 1.0).abs().max()) < 1e-5
+    del seg
+    assert torch.isfinite(out).all()
+    # the global max M (one scalar over all edges and heads), in torch fp32 from the same params
+    W = layer.W.weight.detach()
+    a = layer.a.weight.detach()
+    A = a.view(NH, NH, 2, F)
+    As = torch.einsum("hkf,kfi->hi", A[:, :, 0], W.view(NH, F, FIN))
+    Ad = torch.einsum("hkf,kfi->hi", A[:, :, 1], W.view(NH, F, FIN))
+    s_src = x @ As.t()
+    s_dst = x @ Ad.t()
+    M = -float("inf")
+    for c0 in range(0, E2, 1 << 25):
+        c1 = min(E2, c0 + (1 << 25))
+        M = max(M, float((s_src[ei2[0, c0:c1]] + s_dst[ei2[1, c0:c1]]).max()))
+    # sampled destinations: 40 random + the 4 largest in-degrees
+    rowptr = graph.rowptr.cpu().numpy()
+    deg = np.diff(rowptr)
+    top = np.argsort(deg)[-4:]
+    rng = np.random.default_rng(7)
+    nodes = np.unique(np.r_[rng.integers(0, n_idx, 40), top])
+    assert deg[top[-1]] > 10_000, deg[top[-1]]     # the skewed segment is really there
+    Wn = W.cpu().numpy().astype(np.float64).reshape(NH, F, FIN)
+    An = a.cpu().numpy().astype(np.float64).reshape(NH, NH, 2, F)
+    As_n = np.einsum("hkf,kfi->hi", An[:, :, 0], Wn)
+    Ad_n = np.einsum("hkf,kfi->hi", An[:, :, 1], Wn)
+    for n in nodes:
+        b, e = int(rowptr[n]), int(rowptr[n + 1])
+        slots = torch.arange(b, e, device=device)
+        src = graph.col[slots].long()
+        pos = graph.perm[slots].long()
+        xs = x[src].cpu().numpy().astype(np.float64)
+        xn = x[int(n)].cpu().numpy().astype(np.float64)
+        raw = xs @ As_n.T + (Ad_n @ xn)[None, :]                 # (deg, NH)
+        ex = np.exp(0.01 * (raw - M))
+        den = ex.sum(0)
+        al = ex / (den + 1e-8)
+        z = np.einsum("eh,ei->hi", al, xs)                          # sum_e alpha x[src]
+        ref = np.einsum("hfi,hi->hf", Wn, z).reshape(-1)
+        got = out[int(n)].cpu().numpy()
+        assert np.abs(got - ref).max() <= 1e-4, (int(n), e - b, np.abs(got - ref).max())
+        ga = alpha[pos].cpu().numpy()
+        assert np.abs(ga - al).max() <= 1e-4, (int(n), e - b)

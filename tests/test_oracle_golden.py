@@ -64,6 +64,23 @@ def test_oracle_matches_reference_model(name):
         c["expected"][f"alpha{i}"].check(al, OUT_TOL)
 
 
+@pytest.mark.parametrize("name", MODEL_CASES)
+def test_oracle_attention_norm_matches_reference(name):
+    """calc_attention_norm (models/GATModel.py:189-230) and its gradient on the reference's own
+    alphas / edge_index' (goldens made with the reference's sum_over_neighbourhood)."""
+    c = load_model_case(name)
+    e = c["expected"]
+    L = len(c["layers"])
+    alphas = [e[f"alpha{i}"].full for i in range(L)]
+    assert all(a is not None for a in alphas)
+    ei = c["edge_index_out"]
+    v = orc.calc_attention_norm(ei, alphas)
+    # fp32 summation-order noise of torch.norm over ~5e4 terms: relative 1e-5
+    assert abs(v - e["attention_norm"]) <= 1e-5 * max(1.0, abs(e["attention_norm"]))
+    for i, g in enumerate(orc.calc_attention_norm_grad(ei, alphas)):
+        e[f"attention_norm_grad{i}"].check(g, 1e-9)
+
+
 def test_self_loop_rewrite_order():
     ei = np.array([[0, 1, 2, 2, 4], [1, 1, 0, 2, 3]])
     got = orc.add_remaining_self_loops(ei)
