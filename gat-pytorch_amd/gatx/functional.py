@@ -113,6 +113,31 @@ def gemm_workspace(M: int, N: int, K: int, dev):
     return ptr(torch.empty(nb, dtype=torch.uint8, device=dev)), nb
 
 
+_WPAD_CACHE: "OrderedDict" = None
+
+
+def padded_weight(W, ld: int):
+    """W (rows x F_in) copied into rows of `ld` floats (zero tail, gatx_pad_rows) so GEMMs can
+    read it as float4 rows; cached on the parameter's identity and version."""
+    global _WPAD_CACHE
+    from collections import OrderedDict
+    if W.size(1) == ld:
+        return W
+    if _WPAD_CACHE is None:
+        _WPAD_CACHE = OrderedDict()
+    key = (W.data_ptr(), W._version, tuple(W.shape), W.device, ld)
+    hit = _WPAD_CACHE.get(key)
+    if hit is not None:
+        _WPAD_CACHE.move_to_end(key)
+        return hit[1]
+    Wp = torch.empty((W.size(0), ld), dtype=torch.float32, device=W.device)
+    call("gatx_pad_rows", ptr(W), W.size(0), W.size(1), W.size(1), ptr(Wp), ld, stream())
+    _WPAD_CACHE[key] = (W, Wp)
+    while len(_WPAD_CACHE) > 16:
+        _WPAD_CACHE.popitem(last=False)
+    return Wp
+
+
 def augmented_weight(W, a, sh: "LayerShape"):
     """W_aug = [W padded per head; A_src W; A_dst W] (gatx_prepare_weights). Cached on the
     parameters' identity and version counters, so inference reuses it across steps while any
@@ -224,9 +249,10 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
         with _span("attention_alpha", (E2, sh.NH)):
             call("gatx_attention_alpha", ptr(graph.col), ptr(graph.rowidx), ptr(graph.perm), E2,
                  ptr(S), ptr(M_ord), ptr(den), sh.NH, int(sh.const), ptr(alpha), ptr(argmax), s)
+        Wp = padded_weight(W, Fin_p)   # float4-readable rows
         with _span("gemm_out", (N, sh.F, sh.F_in, sh.NH)):
             call("gatx_gemm_f32_batched", sh.NH, N, sh.F, sh.F_in, ptr(Z), sh.NH * Fin_p, 1,
-                 Fin_p, ptr(W), 1, sh.F_in, sh.F * sh.F_in, ptr(out), sh.NH * sh.F, sh.F, 0,
+                 Fin_p, ptr(Wp), 1, Fin_p, sh.F * Fin_p, ptr(out), sh.NH * sh.F, sh.F, 0,
                  ptr(bias), sh.F, resid_p, sh.out_cols, sh.F, int(elu), s)
         saved.update(S=S, reassoc=True)
         return out, alpha, saved
