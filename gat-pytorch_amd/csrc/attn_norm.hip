@@ -4,7 +4,7 @@
 //   result = mean over layers                                          (:230)
 // deg[dst] is the in-degree over edge_index' (the reference's scatter of ones over
 // edge_index[1], :195-200) = rowptr[dst+1] - rowptr[dst]. One pass per layer reads alpha once
-// (edge_index' order, reached through the CSR's perm) instead of building (E', NH) temporaries.
+// in edge_index' order instead of building (E', NH) temporaries.
 // The gradient is sign(alpha*deg - 1) * deg * g / (E' * L) (torch's |x|' = sgn x, 0 at 0).
 // Sums: per-thread partials, a fixed-order block tree and one fixed-order final pass, so the
 // result is bitwise reproducible.
@@ -27,15 +27,17 @@ __device__ inline float excess(float a, float deg) {
   return p - 1.f;
 }
 
+// Edges are visited in edge_index' order (alpha rows read contiguously); the destination id
+// comes from edge_index'[1] (int64 or int32), its degree from the L2-resident rowptr.
+template <typename I>
 __global__ void __launch_bounds__(256) attn_norm_partial_kernel(
-    const float* __restrict__ alpha, int64_t E2, int NH, const int32_t* __restrict__ perm,
-    const int32_t* __restrict__ rowidx, const int32_t* __restrict__ rowptr,
-    float* __restrict__ part) {
+    const float* __restrict__ alpha, int64_t E2, int NH, const I* __restrict__ dst,
+    const int32_t* __restrict__ rowptr, float* __restrict__ part) {
   float s = 0.f;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < E2;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const float deg = deg_of(rowptr, rowidx[i]);
-    const float* a = alpha + (int64_t)perm[i] * NH;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E2;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const float deg = deg_of(rowptr, (int32_t)dst[e]);
+    const float* a = alpha + e * NH;
     for (int h = 0; h < NH; ++h) s += fabsf(excess(a[h], deg));
   }
   s = group_sum<64>(s);
@@ -60,15 +62,15 @@ __global__ void __launch_bounds__(256) attn_norm_final_kernel(const float* __res
   }
 }
 
+template <typename I>
 __global__ void __launch_bounds__(256) attn_norm_backward_kernel(
-    const float* __restrict__ alpha, int64_t E2, int NH, const int32_t* __restrict__ perm,
-    const int32_t* __restrict__ rowidx, const int32_t* __restrict__ rowptr,
-    const float* __restrict__ g, float scale, float* __restrict__ g_alpha) {
+    const float* __restrict__ alpha, int64_t E2, int NH, const I* __restrict__ dst,
+    const int32_t* __restrict__ rowptr, const float* __restrict__ g, float scale,
+    float* __restrict__ g_alpha) {
   const float gs = g[0] * scale;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < E2;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const float deg = deg_of(rowptr, rowidx[i]);
-    const int64_t e = perm[i];
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E2;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const float deg = deg_of(rowptr, (int32_t)dst[e]);
     for (int h = 0; h < NH; ++h) {
       const float t = excess(alpha[e * NH + h], deg);
       const float sg = t > 0.f ? 1.f : (t < 0.f ? -1.f : 0.f);
@@ -91,15 +93,20 @@ extern "C" size_t gatx_attention_norm_workspace_bytes(void) {
   return sizeof(float) * kNormBlocks;
 }
 
-extern "C" int gatx_attention_norm(const float* alpha, int64_t E2, int NH, const int32_t* perm,
-                                   const int32_t* rowidx, const int32_t* rowptr, float scale,
+extern "C" int gatx_attention_norm(const float* alpha, int64_t E2, int NH, const void* dst,
+                                   int dst_is64, const int32_t* rowptr, float scale,
                                    int accumulate, float* out, void* workspace,
                                    gatx_stream_t s) {
   GATX_REQUIRE(E2 >= 0 && NH >= 1, "attention_norm: bad sizes");
   hipStream_t st = (hipStream_t)s;
   const unsigned nb = grid_for(E2, kNormBlocks);
   float* part = (float*)workspace;
-  attn_norm_partial_kernel<<<nb, 256, 0, st>>>(alpha, E2, NH, perm, rowidx, rowptr, part);
+  if (dst_is64)
+    attn_norm_partial_kernel<int64_t><<<nb, 256, 0, st>>>(alpha, E2, NH, (const int64_t*)dst,
+                                                          rowptr, part);
+  else
+    attn_norm_partial_kernel<int32_t><<<nb, 256, 0, st>>>(alpha, E2, NH, (const int32_t*)dst,
+                                                          rowptr, part);
   GATX_LAUNCH_CHECK("attention_norm");
   attn_norm_final_kernel<<<1, 256, 0, st>>>(part, (int)nb, scale, accumulate, out);
   GATX_LAUNCH_CHECK("attention_norm_final");
@@ -107,13 +114,18 @@ extern "C" int gatx_attention_norm(const float* alpha, int64_t E2, int NH, const
 }
 
 extern "C" int gatx_attention_norm_backward(const float* alpha, int64_t E2, int NH,
-                                            const int32_t* perm, const int32_t* rowidx,
+                                            const void* dst, int dst_is64,
                                             const int32_t* rowptr, const float* g, float scale,
                                             float* g_alpha, gatx_stream_t s) {
   GATX_REQUIRE(E2 >= 0 && NH >= 1, "attention_norm_backward: bad sizes");
   if (E2 == 0) return 0;
-  attn_norm_backward_kernel<<<grid_for(E2, 8192), 256, 0, (hipStream_t)s>>>(
-      alpha, E2, NH, perm, rowidx, rowptr, g, scale, g_alpha);
+  hipStream_t st = (hipStream_t)s;
+  if (dst_is64)
+    attn_norm_backward_kernel<int64_t><<<grid_for(E2, 8192), 256, 0, st>>>(
+        alpha, E2, NH, (const int64_t*)dst, rowptr, g, scale, g_alpha);
+  else
+    attn_norm_backward_kernel<int32_t><<<grid_for(E2, 8192), 256, 0, st>>>(
+        alpha, E2, NH, (const int32_t*)dst, rowptr, g, scale, g_alpha);
   GATX_LAUNCH_CHECK("attention_norm_backward");
   return 0;
 }

@@ -400,33 +400,38 @@ __global__ void __launch_bounds__(256) gw_kernel(const float* __restrict__ gW_au
   }
 }
 
-// g_a[h][k*2F + f (+F)] = sum_i gW_aug[Dp + h (+NH)][i] * W[k*F + f][i]; one wave per W row c.
+// g_a[h][k*2F + f (+F)] = sum_i gW_aug[Dp + h (+NH)][i] * W[k*F + f][i]; one workgroup per W
+// row c, its 4 waves splitting F_in, then a fixed-order combine of the 4 wave sums.
+template <int H2C>
 __global__ void __launch_bounds__(256) ga_kernel(const float* __restrict__ gW_aug,
                                                  const float* __restrict__ W, int NH, int F,
                                                  int Fp, int64_t F_in, float* __restrict__ g_a) {
-  const int lane = threadIdx.x & 63;
-  const int D = NH * F;
+  __shared__ float red[4][H2C];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int D = NH * F, H2 = 2 * NH;
   const int64_t Dp = (int64_t)NH * Fp;
-  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (c >= D) return;
+  const int c = blockIdx.x;
   const int k = c / F, f = c - k * F;
-  float acc[32];
+  float acc[H2C];
 #pragma unroll
-  for (int h = 0; h < 32; ++h) acc[h] = 0.f;
-  for (int64_t i = lane; i < F_in; i += 64) {
+  for (int h = 0; h < H2C; ++h) acc[h] = 0.f;
+  for (int64_t i = threadIdx.x; i < F_in; i += 256) {
     const float w = W[(int64_t)c * F_in + i];
 #pragma unroll
-    for (int h = 0; h < 32; ++h)
-      if (h < 2 * NH) acc[h] = fmaf(gW_aug[(Dp + h) * F_in + i], w, acc[h]);
+    for (int h = 0; h < H2C; ++h)
+      if (h < H2) acc[h] = fmaf(gW_aug[(Dp + h) * F_in + i], w, acc[h]);
   }
 #pragma unroll
-  for (int h = 0; h < 32; ++h) {
-    if (h >= 2 * NH) break;
+  for (int h = 0; h < H2C; ++h) {
     const float v = group_sum<64>(acc[h]);
-    if (lane == 0) {
-      const int hh = h < NH ? h : h - NH;
-      g_a[(int64_t)hh * 2 * D + k * 2 * F + (h < NH ? 0 : F) + f] = v;
-    }
+    if (lane == 0) red[wave][h] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < H2) {
+    const int h = threadIdx.x;
+    const float v = (red[0][h] + red[1][h]) + (red[2][h] + red[3][h]);
+    const int hh = h < NH ? h : h - NH;
+    g_a[(int64_t)hh * 2 * D + k * 2 * F + (h < NH ? 0 : F) + f] = v;
   }
 }
 
@@ -583,8 +588,10 @@ extern "C" int gatx_weight_grads(const float* gW_aug, const float* W, const floa
   gw_kernel<<<grid_for((int64_t)NH * F * F_in), 256, 0, st>>>(gW_aug, a, NH, F, Fp, F_in, g_W);
   GATX_LAUNCH_CHECK("gw");
   if (a) {
-    ga_kernel<<<(unsigned)ceil_div((int64_t)NH * F, 4), 256, 0, st>>>(gW_aug, W, NH, F, Fp, F_in,
-                                                                      g_a);
+    const unsigned D = (unsigned)(NH * F);
+    if (2 * NH <= 8) ga_kernel<8><<<D, 256, 0, st>>>(gW_aug, W, NH, F, Fp, F_in, g_a);
+    else if (2 * NH <= 16) ga_kernel<16><<<D, 256, 0, st>>>(gW_aug, W, NH, F, Fp, F_in, g_a);
+    else ga_kernel<32><<<D, 256, 0, st>>>(gW_aug, W, NH, F, Fp, F_in, g_a);
     GATX_LAUNCH_CHECK("ga");
   }
   return 0;

@@ -333,29 +333,34 @@ __global__ void __launch_bounds__(256) edge_forward_kernel(EdgeFwdArgs g) {
 // W_aug rows Dp.. Dp+2NH-1 = A2 . W with A2 = [A_src; A_dst] (2NH x D), deterministic split-K:
 // block (i-chunk of 64 columns, c-chunk of 128 rows of W) -> partial[cb][h2][i].
 constexpr int kMaxH2 = 32;
+// Block (64 columns i, 16 rows c of W; 4 waves x 4 rows): the row index is wave-uniform, so
+// the 2NH coefficients of `a` per row are scalar loads; partial[cb][h2][i] over the block's rows.
+constexpr int kWeffRows = 16;
 __global__ void __launch_bounds__(256) weff_partial_kernel(const float* __restrict__ W,
                                                            const float* __restrict__ a, int NH,
                                                            int F, int64_t F_in,
                                                            float* __restrict__ partial) {
   __shared__ float red[4][kMaxH2][64];
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int tx = threadIdx.x & 63;
+  const int ty = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t i = blockIdx.x * 64ll + tx;
   const int D = NH * F, H2 = 2 * NH;
-  const int c0 = blockIdx.y * 128 + ty * 32;
+  const int c0 = blockIdx.y * kWeffRows + ty * (kWeffRows / 4);
   float acc[kMaxH2];
 #pragma unroll
   for (int h = 0; h < kMaxH2; ++h) acc[h] = 0.f;
-  for (int cc = 0; cc < 32; ++cc) {
+#pragma unroll
+  for (int cc = 0; cc < kWeffRows / 4; ++cc) {
     const int c = c0 + cc;
     if (c >= D) break;
     const float w = (i < F_in) ? W[(int64_t)c * F_in + i] : 0.f;
     const int k = c / F, f = c - k * F;
+    const float* ak = a + (int64_t)k * 2 * F + f;
 #pragma unroll
     for (int h = 0; h < kMaxH2; ++h) {
       if (h >= H2) break;
       const int hh = h < NH ? h : h - NH;
-      const float av = a[(int64_t)hh * 2 * D + k * 2 * F + (h < NH ? 0 : F) + f];
-      acc[h] = fmaf(av, w, acc[h]);
+      acc[h] = fmaf(ak[(int64_t)hh * 2 * D + (h < NH ? 0 : F)], w, acc[h]);
     }
   }
 #pragma unroll
@@ -364,7 +369,7 @@ __global__ void __launch_bounds__(256) weff_partial_kernel(const float* __restri
   __syncthreads();
   if (ty == 0 && i < F_in) {
     for (int h = 0; h < H2; ++h) {
-      float s = red[0][h][tx] + red[1][h][tx] + red[2][h][tx] + red[3][h][tx];
+      float s = (red[0][h][tx] + red[1][h][tx]) + (red[2][h][tx] + red[3][h][tx]);
       partial[((int64_t)blockIdx.y * H2 + h) * F_in + i] = s;
     }
   }
@@ -611,7 +616,7 @@ extern "C" int gatx_prepare_weights(const float* W, const float* a, int NH, int 
   const int H2 = a ? 2 * NH : 0;
   GATX_REQUIRE(H2 <= kMaxH2, "prepare_weights: num_heads > %d unsupported", kMaxH2 / 2);
   const int D = NH * F;
-  const int n_cb = (int)ceil_div(D, 128);
+  const int n_cb = (int)ceil_div(D, kWeffRows);
   float* partial = nullptr;
   if (H2) {
     // split-K partials are staged in the tail of the caller's buffer, which holds
@@ -629,7 +634,7 @@ extern "C" int gatx_prepare_weights(const float* W, const float* a, int NH, int 
 
 extern "C" int64_t gatx_prepare_weights_floats(int NH, int F, int64_t F_in, int has_a) {
   const int64_t Fp = round_up(F, 4), H2 = has_a ? 2 * NH : 0;
-  return (NH * Fp + H2 + ceil_div((int64_t)NH * F, 128) * H2) * F_in;
+  return (NH * Fp + H2 + ceil_div((int64_t)NH * F, kWeffRows) * H2) * F_in;
 }
 
 extern "C" void gatx_set_debug(int flags) { g_debug = flags; }

@@ -288,8 +288,10 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
 
 def layer_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShape, p: float,
                    seed: int, saved, need_x: bool, need_W: bool, need_a: bool, need_bias: bool,
-                   out=None, elu=False, need_resid=False):
-    """Gradients of layer_forward; returns (g_x, g_W, g_a, g_bias, g_resid)."""
+                   out=None, elu=False, need_resid=False, resid_is_x=False):
+    """Gradients of layer_forward; returns (g_x, g_W, g_a, g_bias, g_resid). With resid_is_x
+    (GATModel's identity skip) the skip gradient is folded into g_x by the g_x GEMM's
+    accumulate epilogue and g_resid is None."""
     N = x.size(0)
     dev = x.device
     s = stream()
@@ -328,10 +330,16 @@ def layer_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShape, 
          ptr(G_aug), sh.ldg, s)
     g_x = g_W = g_a = g_bias = None
     W_aug = saved["W_aug"]
+    if need_bias and bias is not None:   # before g_pre may become g_x's accumulator
+        g_bias = torch.empty_like(bias)
+        src = g_pre if elu else g_out
+        call("gatx_colsum", ptr(src), N, sh.out_cols, sh.out_cols, ptr(g_bias), s)
+    fold = resid_is_x and need_x and g_pre is not None
     if need_x:
-        g_x = torch.empty((N, sh.F_in), **f32)
+        g_x = g_pre if fold else torch.empty((N, sh.F_in), **f32)
         call("gatx_gemm_f32", N, sh.F_in, sh.K_aug, ptr(G_aug), sh.ldg, 1, ptr(W_aug), sh.F_in, 1,
-             ptr(g_x), sh.F_in, sh.F_in, None, 0, 0, *gemm_workspace(N, sh.F_in, sh.K_aug, dev), s)
+             ptr(g_x), sh.F_in, sh.F_in, None, 0, int(fold),
+             *gemm_workspace(N, sh.F_in, sh.K_aug, dev), s)
     if need_W or need_a:
         gW_aug = torch.empty((sh.K_aug, sh.F_in), **f32)
         ws_bytes = lib.gatx_gemm_splitk_workspace_bytes(sh.K_aug, sh.F_in, N)
@@ -342,12 +350,8 @@ def layer_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShape, 
         g_a = torch.empty_like(a) if a is not None else None
         call("gatx_weight_grads", ptr(gW_aug), ptr(W), ptr(a), sh.NH, sh.F, sh.F_in, ptr(g_W),
              ptr(g_a), s)
-    if need_bias and bias is not None:
-        g_bias = torch.empty_like(bias)
-        src = g_pre if elu else g_out
-        call("gatx_colsum", ptr(src), N, sh.out_cols, sh.out_cols, ptr(g_bias), s)
     g_resid = None
-    if need_resid:
+    if need_resid and not fold:
         g_resid = g_pre
     return (g_x, (g_W if need_W else None), (g_a if need_a else None), g_bias, g_resid)
 
@@ -358,6 +362,7 @@ class GATLayerFunction(torch.autograd.Function):
         out, alpha, saved = layer_forward(x, W, a, bias, graph, sh, p, seed, resid, elu)
         ctx.graph, ctx.sh, ctx.p, ctx.seed, ctx.saved, ctx.elu = graph, sh, p, seed, saved, elu
         ctx.has_resid = resid is not None
+        ctx.resid_is_x = resid is not None and resid is x
         ctx.save_for_backward(x, W, a, bias, out if elu else None)
         return out, alpha
 
@@ -370,7 +375,8 @@ class GATLayerFunction(torch.autograd.Function):
         nx, nW, na, nb, nr = ctx.needs_input_grad[:5]
         g_x, g_W, g_a, g_b, g_r = layer_backward(
             g_out, g_alpha, x, W, a, bias, ctx.graph, ctx.sh, ctx.p, ctx.seed, ctx.saved, nx, nW,
-            na, nb, out=out, elu=ctx.elu, need_resid=bool(ctx.has_resid and nr))
+            na, nb, out=out, elu=ctx.elu, need_resid=bool(ctx.has_resid and nr),
+            resid_is_x=ctx.resid_is_x)
         return g_x, g_W, g_a, g_b, g_r, None, None, None, None, None
 
 
@@ -415,6 +421,14 @@ def gat_layer(x, edge_index, W, a, bias, num_heads, out_features, concat, add_se
     return out, graph.edge_index, alpha
 
 
+def _dst_row(graph):
+    """(pointer, is64) of edge_index'[1] with unit stride."""
+    ei = graph.edge_index
+    if ei.stride(1) != 1:   # stream-ordered: the temporary outlives the enqueued kernel's use
+        ei = ei.contiguous()
+    return ptr(ei[1]), int(ei.dtype == torch.int64)
+
+
 class AttentionNormFunction(torch.autograd.Function):
     """mean over layers of ||alpha_l * deg[dst] - 1||_1 / E' (`models/GATModel.py:189-234`) on
     gatx_attention_norm: one fused pass per layer over the CSR, gradient by
@@ -435,8 +449,8 @@ class AttentionNormFunction(torch.autograd.Function):
             if a.dim() != 2 or a.size(0) != E2:
                 raise RuntimeError(f"attention {i} has shape {tuple(a.shape)}, edge_index has "
                                    f"{E2} edges")
-            call("gatx_attention_norm", ptr(a), E2, a.size(1), ptr(graph.perm), ptr(graph.rowidx),
-                 ptr(graph.rowptr), scale, int(i > 0), ptr(out), ptr(ws), s)
+            call("gatx_attention_norm", ptr(a), E2, a.size(1), *_dst_row(graph), ptr(graph.rowptr),
+                 scale, int(i > 0), ptr(out), ptr(ws), s)
         ctx.graph, ctx.scale = graph, scale
         ctx.save_for_backward(*alphas)
         return out.view(())
@@ -449,8 +463,8 @@ class AttentionNormFunction(torch.autograd.Function):
         grads = []
         for a in ctx.saved_tensors:
             ga = torch.empty_like(a)
-            call("gatx_attention_norm_backward", ptr(a), E2, a.size(1), ptr(graph.perm),
-                 ptr(graph.rowidx), ptr(graph.rowptr), ptr(g), ctx.scale, ptr(ga), stream())
+            call("gatx_attention_norm_backward", ptr(a), E2, a.size(1), *_dst_row(graph),
+                 ptr(graph.rowptr), ptr(g), ctx.scale, ptr(ga), stream())
             grads.append(ga)
         return (None, *grads)
 

@@ -236,16 +236,17 @@ int gatx_colsum(const float* X, int64_t nrows, int64_t ncols, int64_t ld, float*
 
 /* ---- attention-norm regulariser (models/GATModel.py:189-234, calc_attention_norm) ---- */
 /* out[0] = (accumulate ? out[0] : 0) + scale * sum_{e,h} |alpha[e,h] * deg[dst_e] - 1| over one
- * layer's alpha (E2 x NH, edge_index' order); deg from the dst-CSR (rowptr), edges reached via
- * perm / rowidx. scale = 1 / (E2 * num_layers) gives the reference's mean. workspace:
- * gatx_attention_norm_workspace_bytes(). Replaces GATModel.py:195-230. */
+ * layer's alpha (E2 x NH, edge_index' order); dst = edge_index'[1] (E2 entries, int64 when
+ * dst_is64 else int32), deg from the dst-CSR rowptr. scale = 1 / (E2 * num_layers) gives the
+ * reference's mean. workspace: gatx_attention_norm_workspace_bytes(). Replaces
+ * GATModel.py:195-230. */
 size_t gatx_attention_norm_workspace_bytes(void);
-int gatx_attention_norm(const float* alpha, int64_t E2, int NH, const int32_t* perm,
-                        const int32_t* rowidx, const int32_t* rowptr, float scale, int accumulate,
-                        float* out, void* workspace, gatx_stream_t stream);
+int gatx_attention_norm(const float* alpha, int64_t E2, int NH, const void* dst, int dst_is64,
+                        const int32_t* rowptr, float scale, int accumulate, float* out,
+                        void* workspace, gatx_stream_t stream);
 /* g_alpha[e,h] = g[0] * scale * sign(alpha[e,h] * deg - 1) * deg (g: device scalar). */
-int gatx_attention_norm_backward(const float* alpha, int64_t E2, int NH, const int32_t* perm,
-                                 const int32_t* rowidx, const int32_t* rowptr, const float* g,
+int gatx_attention_norm_backward(const float* alpha, int64_t E2, int NH, const void* dst,
+                                 int dst_is64, const int32_t* rowptr, const float* g,
                                  float scale, float* g_alpha, gatx_stream_t stream);
 
 #ifdef __cplusplus

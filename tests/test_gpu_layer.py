@@ -315,6 +315,35 @@ def test_fused_skip_elu_epilogue(concat, fin, device):
         assert np.abs(t.cpu().numpy() - ref).max() <= GRAD_TOL * max(1.0, np.abs(ref).max()), k
 
 
+@pytest.mark.parametrize("elu", [True, False])
+def test_identity_skip_gradient_folded(elu, device):
+    """GATModel's identity skip passes x itself as resid: x.grad = layer grad + skip grad, with
+    the skip part accumulated by the g_x GEMM epilogue (no separate add)."""
+    gatx = _gatx()
+    from gatx import data as gd
+    NH, F = 4, 16
+    fin = NH * F
+    b = gd.uniform_graph_batch(2, 100, 1200, fin, feature_seed=21)
+    W = gd.xavier_uniform(22, NH * F, fin)
+    a = gd.xavier_uniform(23, NH, NH * 2 * F)
+    layer = gatx.GATLayer(fin, F, NH, True, add_self_loops=True).to(device)
+    with torch.no_grad():
+        layer.W.weight.copy_(torch.from_numpy(W))
+        layer.a.weight.copy_(torch.from_numpy(a))
+    x = torch.from_numpy(b.x).to(device).requires_grad_(True)
+    ei = torch.from_numpy(b.edge_index).to(device)
+    out = layer(x, ei, resid=x, elu=elu)
+    g = gd.normal(24, out.numel()).reshape(tuple(out.shape))
+    (out * torch.from_numpy(g).to(device)).sum().backward()
+    o, _, _, cache = orc.gat_layer_forward(b.x, b.edge_index, W, a, NH, F, True)
+    pre = o + b.x
+    g_pre = g * np.where(pre > 0, 1.0, np.exp(pre)).astype(np.float32) if elu else g
+    gr = orc.gat_layer_backward(cache, g_pre)
+    ref = gr["x"] + g_pre
+    got = x.grad.cpu().numpy()
+    assert np.abs(got - ref).max() <= GRAD_TOL * max(1.0, np.abs(ref).max())
+
+
 def test_gemm_splitk_and_node_scores(device):
     from gatx._lib import call, lib, ptr, stream
     torch.manual_seed(1)
