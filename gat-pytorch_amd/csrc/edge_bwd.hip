@@ -95,6 +95,9 @@ struct BwdArgs {
   const float* g_corr;     // [N][NH] max() share for the src pass
   float* G_aug;
   int64_t ldg, chunk, n_items;
+  int64_t row_stride4;     // dst pass: float4s per gathered row (Wh: Dp/4; x rows: Fin_p/4)
+  int64_t head_stride4;    // float4s between heads in a gathered row (0: one row for all heads)
+  int64_t gs_off;          // column of g_s_src in G_aug (g_s_dst at gs_off + NH)
 };
 
 // dst pass: one wave per (destination n, head h); LPE lanes per edge over the head's Fp/4
@@ -111,7 +114,7 @@ __global__ void __launch_bounds__(256) edge_bwd_dst_kernel(BwdArgs g) {
   int h;
   if (!decode_item(item, g.N, g.NH, g.chunk, n, h)) return;
   const int NH = g.NH, Fp = g.Fp, F4 = Fp / 4, S2 = 2 * NH;
-  const int64_t Dp = (int64_t)NH * Fp, E2 = g.E2;
+  const int64_t E2 = g.E2;
   const float M = ord_to_float(*g.M_ord);
   const bool drop = g.p_drop > 0.f;
   const float drop_scale = drop ? 1.f / (1.f - g.p_drop) : 1.f;
@@ -125,7 +128,7 @@ __global__ void __launch_bounds__(256) edge_bwd_dst_kernel(BwdArgs g) {
   for (int c = 0; c < CPL; ++c) {
     const int q = c * LPE + li;
     vq[c] = q < F4;
-    off4[c] = h * F4 + (vq[c] ? q : 0);
+    off4[c] = (int)(h * g.head_stride4) + (vq[c] ? q : 0);
     gv[c] = vq[c] ? go4[n * g.go_stride4 + h * g.go_head4 + q] : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   const float sdst = g.S[n * S2 + NH + h];
@@ -150,7 +153,7 @@ __global__ void __launch_bounds__(256) edge_bwd_dst_kernel(BwdArgs g) {
     float my_dot = 0.f;
     for (int j0 = grp; j0 < cnt; j0 += EPW) {
       const int sj = (EPW == 1) ? __builtin_amdgcn_readlane(my_src, j0) : src_lds[j0];
-      const float4* rp = Wh4 + (int64_t)sj * (Dp / 4);
+      const float4* rp = Wh4 + (int64_t)sj * g.row_stride4;
       float p = 0.f;
 #pragma unroll
       for (int c = 0; c < CPL; ++c) {
@@ -191,8 +194,41 @@ __global__ void __launch_bounds__(256) edge_bwd_dst_kernel(BwdArgs g) {
   }
   gsum = group_sum<64>(gsum);
   if (lane == 0) {
-    g.G_aug[n * g.ldg + Dp + NH + h] = gsum;
+    g.G_aug[n * g.ldg + g.gs_off + NH + h] = gsum;
     g.gsd[n * NH + h] = gsum;
+  }
+}
+
+// Source-side logit gradients only (no message gradient; the reassociated first layer, whose
+// input needs no gradient): G[s][gs_off + h] = sum over s's out-edges of g_raw'[h] + max share.
+// One wave per source, lanes over its edges, fixed-order wave sums.
+template <int NHC>
+__global__ void __launch_bounds__(256) src_scores_kernel(const int32_t* __restrict__ srowptr,
+                                                         const int32_t* __restrict__ seid,
+                                                         int64_t N, int64_t E2, int NH_rt,
+                                                         const float* __restrict__ g_raw,
+                                                         const float* __restrict__ g_corr,
+                                                         float* __restrict__ G, int64_t ldg,
+                                                         int64_t gs_off) {
+  const int NH = NHC > 0 ? NHC : NH_rt;
+  const int lane = threadIdx.x & 63;
+  const int64_t s = blockIdx.x * 4ll + uni(threadIdx.x >> 6);
+  if (s >= N) return;
+  const int beg = uni(srowptr[s]), end = uni(srowptr[s + 1]);
+  float acc[8];
+#pragma unroll
+  for (int h = 0; h < 8; ++h) acc[h] = 0.f;
+  for (int j = beg + lane; j < end; j += 64) {
+    const int64_t e = seid[j];
+#pragma unroll
+    for (int h = 0; h < 8; ++h)
+      if (h < NH) acc[h] += g_raw[(int64_t)h * E2 + e];
+  }
+#pragma unroll
+  for (int h = 0; h < 8; ++h) {
+    if (h >= NH) break;
+    const float v = group_sum<64>(acc[h]);
+    if (lane == 0) G[s * ldg + gs_off + h] = v + (g_corr ? g_corr[s * NH + h] : 0.f);
   }
 }
 
@@ -284,7 +320,7 @@ __global__ void __launch_bounds__(256) edge_bwd_src_kernel(BwdArgs g) {
   int h;
   if (!decode_item(item, g.N, g.NH, g.chunk, s, h)) return;
   const int NH = g.NH, Fp = g.Fp, F4 = Fp / 4, S2 = 2 * NH;
-  const int64_t Dp = (int64_t)NH * Fp, E2 = g.E2;
+  const int64_t E2 = g.E2;
   const float M = g.const_att ? 0.f : ord_to_float(*g.M_ord);
   const bool drop = g.p_drop > 0.f;
   const float drop_scale = drop ? 1.f / (1.f - g.p_drop) : 1.f;
@@ -500,6 +536,41 @@ extern "C" int gatx_prepare_go(const float* g_out, const float* out, int64_t N, 
   return 0;
 }
 
+extern "C" int gatx_edge_backward_dst_ex(const float* rows, int64_t row_stride,
+                                         int64_t head_stride, const float* S,
+                                         const uint32_t* M_ord, const float* den,
+                                         const int32_t* rowptr, const int32_t* col,
+                                         const int32_t* perm, int64_t N, int64_t E2, int NH, int F,
+                                         const float* go, int64_t go_stride, int64_t go_head,
+                                         float p, uint64_t seed, const float* g_alpha,
+                                         float* g_raw, float* gsd, float* G, int64_t ldg,
+                                         int64_t gs_off, gatx_stream_t s) {
+  hipStream_t st = (hipStream_t)s;
+  if (N == 0) return 0;
+  const int Fp = (int)round_up(F, 4);
+  GATX_REQUIRE(row_stride % 4 == 0 && head_stride % 4 == 0 && go_stride % 4 == 0 &&
+                   go_head % 4 == 0 && ((uintptr_t)rows % 16) == 0 && ((uintptr_t)go % 16) == 0,
+               "edge_backward_dst: rows / go must be float4-aligned");
+  const Geom gm = head_geom(Fp / 4);
+  GATX_REQUIRE(gm.cpl <= 4, "edge_backward: out_features > 1024 unsupported");
+  BwdArgs a{};
+  a.Wh = rows; a.go = go;
+  a.go_stride4 = go_stride / 4;
+  a.go_head4 = (int)(go_head / 4);
+  a.row_stride4 = row_stride / 4;
+  a.head_stride4 = head_stride / 4;
+  a.gs_off = gs_off;
+  a.S = S; a.M_ord = M_ord; a.den = den; a.rowptr = rowptr; a.col = col; a.perm = perm;
+  a.N = N; a.E2 = E2; a.NH = NH; a.F = F; a.Fp = Fp; a.p_drop = p; a.seed = seed;
+  a.g_alpha_ret = g_alpha; a.g_raw = g_raw; a.gsd = gsd; a.G_aug = G; a.ldg = ldg;
+  a.chunk = kChunk;
+  a.n_items = ceil_div(N, kChunk) * kChunk * NH;
+  const unsigned grid = (unsigned)ceil_div(a.n_items, 4);
+  GATX_DISPATCH_HEAD(gm, edge_bwd_dst_kernel, grid, a);
+  GATX_LAUNCH_CHECK("edge_bwd_dst");
+  return 0;
+}
+
 extern "C" int gatx_edge_backward_dst(const float* Wh, const float* S, const uint32_t* M_ord,
                                       const float* den, const int32_t* rowptr,
                                       const int32_t* col, const int32_t* perm, int64_t N,
@@ -507,23 +578,28 @@ extern "C" int gatx_edge_backward_dst(const float* Wh, const float* S, const uin
                                       uint64_t seed, const float* go, const float* g_alpha,
                                       float* g_raw, float* gsd, float* G_aug, int64_t ldg,
                                       gatx_stream_t s) {
-  hipStream_t st = (hipStream_t)s;
+  const int64_t Fp = round_up(F, 4), Dp = NH * Fp;
+  return gatx_edge_backward_dst_ex(Wh, Dp, Fp, S, M_ord, den, rowptr, col, perm, N, E2, NH, F,
+                                   go, concat ? Dp : Fp, concat ? Fp : 0, p, seed, g_alpha,
+                                   g_raw, gsd, G_aug, ldg, Dp, s);
+}
+
+extern "C" int gatx_edge_backward_src_scores(const int32_t* srowptr, const int32_t* seid,
+                                             int64_t N, int64_t E2, int NH, const float* g_raw,
+                                             const float* g_corr, float* G, int64_t ldg,
+                                             int64_t gs_off, gatx_stream_t s) {
+  GATX_REQUIRE(NH >= 1 && NH <= 8, "edge_backward_src_scores: 1..8 heads");
   if (N == 0) return 0;
-  const int Fp = (int)round_up(F, 4);
-  const Geom gm = head_geom(Fp / 4);
-  GATX_REQUIRE(gm.cpl <= 4, "edge_backward: out_features > 1024 unsupported");
-  BwdArgs a{};
-  a.Wh = Wh; a.go = go;
-  a.go_stride4 = concat ? (int64_t)NH * Fp / 4 : Fp / 4;
-  a.go_head4 = concat ? Fp / 4 : 0;
-  a.S = S; a.M_ord = M_ord; a.den = den; a.rowptr = rowptr; a.col = col; a.perm = perm;
-  a.N = N; a.E2 = E2; a.NH = NH; a.F = F; a.Fp = Fp; a.p_drop = p; a.seed = seed;
-  a.g_alpha_ret = g_alpha; a.g_raw = g_raw; a.gsd = gsd; a.G_aug = G_aug; a.ldg = ldg;
-  a.chunk = kChunk;
-  a.n_items = ceil_div(N, kChunk) * kChunk * NH;
-  const unsigned grid = (unsigned)ceil_div(a.n_items, 4);
-  GATX_DISPATCH_HEAD(gm, edge_bwd_dst_kernel, grid, a);
-  GATX_LAUNCH_CHECK("edge_bwd_dst");
+  hipStream_t st = (hipStream_t)s;
+  const unsigned grid = (unsigned)ceil_div(N, 4);
+#define GATX_SS(C) src_scores_kernel<C><<<grid, 256, 0, st>>>(srowptr, seid, N, E2, NH, g_raw, \
+                                                             g_corr, G, ldg, gs_off)
+  switch (NH) {
+    case 1: GATX_SS(1); break; case 2: GATX_SS(2); break; case 4: GATX_SS(4); break;
+    case 8: GATX_SS(8); break; default: GATX_SS(0); break;
+  }
+#undef GATX_SS
+  GATX_LAUNCH_CHECK("edge_bwd_src_scores");
   return 0;
 }
 

@@ -533,6 +533,24 @@ extern "C" size_t gatx_gemm_splitk_workspace_bytes(int64_t M, int64_t N, int64_t
   return sp > 1 ? (size_t)sp * M * N * sizeof(float) : 0;
 }
 
+extern "C" size_t gatx_gemm_splitk_batched_workspace_bytes(int64_t batch, int64_t M, int64_t N,
+                                                           int64_t K) {
+  const int64_t tiles = ceil_div(M, 128) * ceil_div(N, 128) * batch;
+  const int sp = choose_splits(tiles, K, resident_blocks());
+  return sp > 1 ? (size_t)sp * batch * M * N * sizeof(float) : 0;
+}
+
+extern "C" int gatx_gemm_f32_splitk_batched(int64_t batch, int64_t M, int64_t N, int64_t K,
+                                            const float* A, int64_t sam, int64_t sak,
+                                            int64_t a_bs, const float* B, int64_t sbk,
+                                            int64_t sbn, int64_t b_bs, float* C, int64_t ldc,
+                                            int64_t c_bs, int accumulate, void* workspace,
+                                            size_t workspace_bytes, gatx_stream_t s) {
+  return gemm_impl(M, N, K, (int)batch, A, sam, sak, a_bs, B, sbk, sbn, b_bs, C, ldc, c_bs, N,
+                   nullptr, 0, 0, accumulate, nullptr, 0, nullptr, 0, 0, 0, workspace,
+                   workspace_bytes, 2, (hipStream_t)s);
+}
+
 extern "C" int gatx_gemm_f32_splitk(int64_t M, int64_t N, int64_t K, const float* A, int64_t sam,
                                     int64_t sak, const float* B, int64_t sbk, int64_t sbn,
                                     float* C, int64_t ldc, int accumulate, void* workspace,

@@ -254,7 +254,7 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
             call("gatx_gemm_f32_batched", sh.NH, N, sh.F, sh.F_in, ptr(Z), sh.NH * Fin_p, 1,
                  Fin_p, ptr(Wp), 1, Fin_p, sh.F * Fin_p, ptr(out), sh.NH * sh.F, sh.F, 0,
                  ptr(bias), sh.F, resid_p, sh.out_cols, sh.F, int(elu), s)
-        saved.update(S=S, reassoc=True)
+        saved.update(S=S, reassoc=True, Z=Z, x_rows=x_rows)
         return out, alpha, saved
     Wh = torch.empty((N, sh.Dp), **f32)
     S = torch.empty((N, max(sh.H2, 1)), **f32)
@@ -299,6 +299,9 @@ def layer_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShape, 
     g_out = g_out.contiguous()
     E2 = graph.num_edges
     graph.ensure_transpose()
+    if saved.get("reassoc") and not need_x and not sh.const and sh.NH <= 8:
+        return _reassoc_backward(g_out, g_alpha, x, W, a, bias, graph, sh, p, seed, saved,
+                                 need_W, need_a, need_bias, out, elu, need_resid)
     if saved["Wh"] is None:   # reassociated forward never built Wh: project now
         Wh = torch.empty((N, sh.Dp), **f32)
         call("gatx_gemm_f32", N, sh.Dp, sh.F_in, ptr(x), sh.F_in, 1, ptr(saved["W_aug"]), 1,
@@ -354,6 +357,71 @@ def layer_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShape, 
     if need_resid and not fold:
         g_resid = g_pre
     return (g_x, (g_W if need_W else None), (g_a if need_a else None), g_bias, g_resid)
+
+
+def _reassoc_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShape, p, seed,
+                      saved, need_W, need_a, need_bias, out, elu, need_resid):
+    """Backward of the reassociated first layer when its input needs no gradient (the model
+    input): never forms Wh or its (N, NH*F) gradient.
+      g_Z[n,h] = go[n,h] . W_h                      batched GEMM (g_Z[n,h] . x_src == g_alpha)
+      dst pass over x rows (F_in floats, not NH*F)  -> g_raw', g_s_dst
+      src scores: g_s_src = sum over out-edges      (no row gathers)
+      g_W_h = go_h^T Z_h                            batched split-K GEMM, Z saved by the forward
+      g_W_score = [g_s_src | g_s_dst]^T x           split-K GEMM
+    then gatx_weight_grads maps g_W_aug to (g_W, g_a) exactly as the general path."""
+    N = x.size(0)
+    dev = x.device
+    s = stream()
+    f32 = dict(dtype=torch.float32, device=dev)
+    E2 = graph.num_edges
+    NH, F, Fp, F_in = sh.NH, sh.F, sh.Fp, sh.F_in
+    Fin_p = _round4(F_in)
+    Z, x_rows = saved["Z"], saved["x_rows"]
+    go = torch.empty((N, sh.Dp), **f32)
+    g_pre = torch.empty((N, sh.out_cols), **f32) if (need_resid or (need_bias and elu)) else None
+    call("gatx_prepare_go", ptr(g_out), ptr(out) if elu else None, N, NH, F, 1, int(elu),
+         ptr(go), ptr(g_pre), s)
+    Wp = padded_weight(W, Fin_p)                      # [NH*F][Fin_p], zero tail
+    g_Z = torch.empty((N, NH * Fin_p), **f32)
+    call("gatx_gemm_f32_batched", NH, N, Fin_p, F, ptr(go), sh.Dp, 1, Fp, ptr(Wp), Fin_p, 1,
+         F * Fin_p, ptr(g_Z), NH * Fin_p, Fin_p, 0, None, 0, None, 0, 0, 0, s)
+    G_s = torch.empty((N, 2 * NH), **f32)            # [g_s_src | g_s_dst]
+    g_raw = torch.empty((NH, max(E2, 1)), **f32)
+    gsd = torch.empty((N, NH), **f32)
+    call("gatx_edge_backward_dst_ex", ptr(x_rows), Fin_p, 0, ptr(saved["S"]), ptr(saved["M_ord"]),
+         ptr(saved["den"]), ptr(graph.rowptr), ptr(graph.col), ptr(graph.perm), N, E2, NH, Fin_p,
+         ptr(g_Z), NH * Fin_p, Fin_p, float(p), seed,
+         ptr(g_alpha.contiguous()) if g_alpha is not None else None, ptr(g_raw), ptr(gsd),
+         ptr(G_s), 2 * NH, 0, s)
+    g_corr = torch.zeros((N, NH), **f32)
+    mws = torch.empty(lib.gatx_max_backward_workspace_bytes(), dtype=torch.uint8, device=dev)
+    call("gatx_max_backward", ptr(saved["argmax"]), ptr(gsd), ptr(saved["S"]),
+         ptr(saved["M_ord"]), ptr(graph.col), ptr(graph.rowidx), N, E2, NH, ptr(g_corr),
+         ptr(G_s), 2 * NH, 0, ptr(mws), s)
+    call("gatx_edge_backward_src_scores", ptr(graph.srowptr), ptr(graph.seid), N, E2, NH,
+         ptr(g_raw), ptr(g_corr), ptr(G_s), 2 * NH, 0, s)
+    g_W = g_a = g_bias = None
+    if need_W or need_a:
+        gW_aug = torch.empty((sh.K_aug, F_in), **f32)
+        # main rows, head h at rows h*Fp.. : go_h^T (F x N) . Z_h (N x F_in)
+        wb = lib.gatx_gemm_splitk_batched_workspace_bytes(NH, F, F_in, N)
+        ws = torch.empty(max(wb, 1), dtype=torch.uint8, device=dev)
+        call("gatx_gemm_f32_splitk_batched", NH, F, F_in, N, ptr(go), 1, sh.Dp, Fp, ptr(Z),
+             NH * Fin_p, 1, Fin_p, ptr(gW_aug), F_in, Fp * F_in, 0, ptr(ws), wb, s)
+        # score rows: G_s^T (2NH x N) . x (N x F_in)
+        wb2 = lib.gatx_gemm_splitk_workspace_bytes(2 * NH, F_in, N)
+        ws2 = torch.empty(max(wb2, 1), dtype=torch.uint8, device=dev)
+        call("gatx_gemm_f32_splitk", 2 * NH, F_in, N, ptr(G_s), 1, 2 * NH, ptr(x), F_in, 1,
+             ptr(gW_aug) + 4 * sh.Dp * F_in, F_in, 0, ptr(ws2), wb2, s)
+        g_W = torch.empty_like(W)
+        g_a = torch.empty_like(a)
+        call("gatx_weight_grads", ptr(gW_aug), ptr(W), ptr(a), NH, F, F_in, ptr(g_W), ptr(g_a), s)
+    if need_bias and bias is not None:
+        g_bias = torch.empty_like(bias)
+        src = g_pre if elu else g_out
+        call("gatx_colsum", ptr(src), N, sh.out_cols, sh.out_cols, ptr(g_bias), s)
+    return (None, (g_W if need_W else None), (g_a if need_a else None), g_bias,
+            g_pre if need_resid else None)
 
 
 class GATLayerFunction(torch.autograd.Function):

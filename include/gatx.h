@@ -104,6 +104,16 @@ int gatx_gemm_f32_splitk(int64_t M, int64_t N, int64_t K, const float* A, int64_
                          gatx_stream_t stream);
 
 
+/* Batched split-K: `batch` independent products (A, B, C offset by b*a_bs, b*b_bs, b*c_bs
+ * floats), each summed over K in deterministic slabs (the reassociated first layer's per-head
+ * weight gradient g_W_h = go_h^T Z_h, K = #nodes). */
+size_t gatx_gemm_splitk_batched_workspace_bytes(int64_t batch, int64_t M, int64_t N, int64_t K);
+int gatx_gemm_f32_splitk_batched(int64_t batch, int64_t M, int64_t N, int64_t K, const float* A,
+                                 int64_t sam, int64_t sak, int64_t a_bs, const float* B,
+                                 int64_t sbk, int64_t sbn, int64_t b_bs, float* C, int64_t ldc,
+                                 int64_t c_bs, int accumulate, void* workspace,
+                                 size_t workspace_bytes, gatx_stream_t stream);
+
 /* gatx_gemm_f32 for the forward projection x . W_aug^T (accumulate = 0); a separate entry point
  * only so profiles can tell the projection launches from the auxiliary products. */
 int gatx_projection_gemm(int64_t M, int64_t N, int64_t K, const float* A, int64_t sam,
@@ -204,6 +214,23 @@ int gatx_edge_backward_dst(const float* Wh, const float* S, const uint32_t* M_or
                            int concat, float dropout_p, uint64_t seed, const float* go,
                            const float* g_alpha_ret, float* g_raw, float* gsd, float* G_aug,
                            int64_t ldg, gatx_stream_t stream);
+/* The dst pass over arbitrary gathered rows: g_alpha[e,h] = <go[n, h], rows[src_e] + h *
+ * head_stride> over F floats (row_stride / head_stride / go_stride / go_head in floats, all
+ * multiples of 4), g_s_dst into G[n][gs_off + NH + h]. With rows = the padded layer input x
+ * (head_stride 0) and go = g_Z = go . W_h per head this is the reassociated first layer's
+ * backward (<go_h, W_h x_src> == <go_h W_h, x_src>). */
+int gatx_edge_backward_dst_ex(const float* rows, int64_t row_stride, int64_t head_stride,
+                              const float* S, const uint32_t* M_ord, const float* den,
+                              const int32_t* rowptr, const int32_t* col, const int32_t* perm,
+                              int64_t num_nodes, int64_t E2, int NH, int F, const float* go,
+                              int64_t go_stride, int64_t go_head, float p, uint64_t seed,
+                              const float* g_alpha_ret, float* g_raw, float* gsd, float* G,
+                              int64_t ldg, int64_t gs_off, gatx_stream_t stream);
+/* Source-side logit gradients only: G[s][gs_off + h] = sum over s's out-edges (src-CSR) of
+ * g_raw'[h][e] + g_corr[s][h] (NULL allowed). No message gradient. NH <= 8. */
+int gatx_edge_backward_src_scores(const int32_t* srowptr, const int32_t* seid, int64_t num_nodes,
+                                  int64_t E2, int NH, const float* g_raw, const float* g_corr,
+                                  float* G, int64_t ldg, int64_t gs_off, gatx_stream_t stream);
 
 /* max() backward (torch splits the gradient evenly over ties): g_M = -sum gsd (two-stage
  * fixed-order reduction); g_corr_src[src,h] += g_M/k and G_aug[dst][Dp+NH+h] += g_M/k for each

@@ -20,7 +20,7 @@ def _gatx():
     return gatx
 
 
-def run_gpu_layer(c, device, with_grads=True):
+def run_gpu_layer(c, device, with_grads=True, x_grad=True):
     gatx = _gatx()
     m = c["meta"]
     layer = gatx.GATLayer(m["in_features"], m["out_features"], m["num_heads"], m["concat"],
@@ -35,7 +35,8 @@ def run_gpu_layer(c, device, with_grads=True):
     if m["dropout"] > 0:
         layer._dropout_seed = lambda: m["seed"]
         layer.train()
-    x = torch.from_numpy(np.ascontiguousarray(c["x"])).to(device).requires_grad_(with_grads)
+    x = torch.from_numpy(np.ascontiguousarray(c["x"])).to(device).requires_grad_(
+        with_grads and x_grad)
     ei = torch.from_numpy(np.ascontiguousarray(c["edge_index"])).to(device)
     out, (ei2, alpha) = layer(x, ei, return_attention_weights=True)
     res = dict(out=out.detach().cpu().numpy(), alpha=alpha.detach().cpu().numpy(),
@@ -46,7 +47,7 @@ def run_gpu_layer(c, device, with_grads=True):
         if m["use_g_alpha"]:
             loss = loss + (alpha * torch.from_numpy(g_alpha).to(device)).sum()
         loss.backward()
-        res["grad_x"] = x.grad.cpu().numpy()
+        res["grad_x"] = x.grad.cpu().numpy() if x.grad is not None else None
         res["grad_W"] = layer.W.weight.grad.cpu().numpy()
         if not m["const_attention"]:
             res["grad_a"] = layer.a.weight.grad.cpu().numpy()
@@ -198,7 +199,8 @@ def test_graph_build_matches_oracle(device):
     np.testing.assert_array_equal(scol, dst[order][seid])
 
 
-def _layer_vs_oracle(device, G, n, e, fin, NH, F, concat, seed=5, grads=True, dropout=0.0):
+def _layer_vs_oracle(device, G, n, e, fin, NH, F, concat, seed=5, grads=True, dropout=0.0,
+                     x_grad=True):
     gatx = _gatx()
     from gatx import data as gd
     b = gd.uniform_graph_batch(G, n, e, fin, feature_seed=seed)
@@ -208,7 +210,7 @@ def _layer_vs_oracle(device, G, n, e, fin, NH, F, concat, seed=5, grads=True, dr
                        dropout=dropout, add_self_loops=True, has_bias=False,
                        const_attention=False, seed=77, use_g_alpha=True),
              x=b.x, edge_index=b.edge_index, W=W, a=a, bias=None)
-    r = run_gpu_layer(c, device, with_grads=grads)
+    r = run_gpu_layer(c, device, with_grads=grads, x_grad=x_grad)
     keep = orc.dropout_keep(77, r["alpha"].shape[0], NH, dropout) if dropout > 0 else None
     out, ei2, alpha, cache = orc.gat_layer_forward(b.x, b.edge_index, W, a, NH, F, concat,
                                                    dropout_p=dropout, keep=keep)
@@ -218,7 +220,7 @@ def _layer_vs_oracle(device, G, n, e, fin, NH, F, concat, seed=5, grads=True, dr
     if grads:
         g_out, g_alpha = grad_seeds(out.shape, alpha.shape)
         gr = orc.gat_layer_backward(cache, g_out, g_alpha)
-        for k in ("x", "W", "a"):
+        for k in (("x", "W", "a") if x_grad else ("W", "a")):
             ref = gr[k]
             err = np.abs(r[f"grad_{k}"] - ref).max()
             assert err <= GRAD_TOL * max(1.0, np.abs(ref).max()), (k, err, np.abs(ref).max())
@@ -265,13 +267,21 @@ def test_errors_mirror_reference(device):
         layer(x.cpu(), torch.tensor([[0, 1], [1, 2]]))
 
 
+@pytest.mark.parametrize("x_grad", [True, False])
 @pytest.mark.parametrize("reassoc", ["0", "1"])
-@pytest.mark.parametrize("fin,NH,F", [(50, 4, 256), (3, 4, 12), (13, 2, 40)])
-def test_reassociation_paths(reassoc, fin, NH, F, device, monkeypatch):
+@pytest.mark.parametrize("fin,NH,F", [(50, 4, 256), (3, 4, 12), (13, 2, 40), (8, 8, 30)])
+def test_reassociation_paths(reassoc, fin, NH, F, x_grad, device, monkeypatch):
     """First-layer reassociation (aggregate x rows, then project per head) vs the direct path;
-    both against the oracle, forward and backward."""
+    both against the oracle, forward and backward. Without an input gradient the reassociated
+    backward runs (g_Z = go W_h, dst pass over x rows, no Wh)."""
     monkeypatch.setenv("GATX_REASSOC", reassoc)
-    _layer_vs_oracle(device, 2, 150, 2500, fin, NH, F, True)
+    _layer_vs_oracle(device, 2, 150, 2500, fin, NH, F, True, x_grad=x_grad)
+
+
+def test_reassociated_backward_ppi_l0_dropout(device):
+    """The reassociated backward at the PPI L0 shape on a full PPI graph, and with dropout."""
+    _layer_vs_oracle(device, 1, 2245, 61318, 50, 4, 256, True, x_grad=False)
+    _layer_vs_oracle(device, 2, 300, 4000, 20, 8, 48, True, x_grad=False, dropout=0.6)
 
 
 @pytest.mark.parametrize("hs", ["1", "2", "4"])
