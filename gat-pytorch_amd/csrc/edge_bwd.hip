@@ -320,7 +320,7 @@ __global__ void __launch_bounds__(256) edge_bwd_src_kernel(BwdArgs g) {
   int h;
   if (!decode_item(item, g.N, g.NH, g.chunk, s, h)) return;
   const int NH = g.NH, Fp = g.Fp, F4 = Fp / 4, S2 = 2 * NH;
-  const int64_t E2 = g.E2;
+  const int64_t Dp = (int64_t)NH * Fp, E2 = g.E2;
   const float M = g.const_att ? 0.f : ord_to_float(*g.M_ord);
   const bool drop = g.p_drop > 0.f;
   const float drop_scale = drop ? 1.f / (1.f - g.p_drop) : 1.f;

@@ -403,6 +403,11 @@ int choose_splits(int64_t tiles, int64_t K, int64_t slots) {
 int choose_tail_split(int64_t tiles, int64_t K, int64_t slots, int64_t& rem) {
   rem = tiles % slots;
   if (rem == 0 || tiles < 1) return 1;
+  static const int forced = [] {   // tuning only: GATX_TAIL_SPLIT=s forces s slices
+    const char* e = getenv("GATX_TAIL_SPLIT");
+    return e ? atoi(e) : 0;
+  }();
+  if (forced > 0) return (int)std::min<int64_t>(std::min(forced, 16), ceil_div(K, 2 * KSTEP));
   const double wave_s = 2.0 * BM * BN * (double)K / (157e12 / (double)slots);
   int best = 1;
   double best_c = 0.75 / 0.95;   // only clear wins: wave boundaries are soft in practice
