@@ -105,6 +105,7 @@ struct BwdArgs {
 template <int LPE, int CPL>
 __global__ void __launch_bounds__(256) edge_bwd_dst_kernel(BwdArgs g) {
   constexpr int EPW = 64 / LPE;
+  constexpr int U = CPL <= 1 ? 4 : 2;
   const int lane = threadIdx.x & 63;
   const int wave = uni(threadIdx.x >> 6);
   const int grp = lane / LPE, li = lane % LPE;
@@ -151,20 +152,31 @@ __global__ void __launch_bounds__(256) edge_bwd_dst_kernel(BwdArgs g) {
     if (EPW > 1) src_lds[lane] = my_src;
     if (EPW > 1) wave_lds_sync();
     float my_dot = 0.f;
-    for (int j0 = grp; j0 < cnt; j0 += EPW) {
-      const int sj = (EPW == 1) ? __builtin_amdgcn_readlane(my_src, j0) : src_lds[j0];
-      const float4* rp = Wh4 + (int64_t)sj * g.row_stride4;
-      float p = 0.f;
+    // U rows in flight per lane group: all loads of a step issue before any reduction
+    for (int j0 = grp; j0 < cnt; j0 += EPW * U) {
+      float4 v[U][CPL];
 #pragma unroll
-      for (int c = 0; c < CPL; ++c) {
-        const float4 v = rp[off4[c]];
-        p += gv[c].x * v.x + gv[c].y * v.y + gv[c].z * v.z + gv[c].w * v.w;
+      for (int u = 0; u < U; ++u) {
+        const int jj = min(j0 + u * EPW, cnt - 1);
+        const int sj = (EPW == 1) ? __builtin_amdgcn_readlane(my_src, jj) : src_lds[jj];
+        const float4* rp = Wh4 + (int64_t)sj * g.row_stride4;
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) v[u][c] = rp[off4[c]];
       }
-      p = group_sum<LPE>(p);
-      if (EPW == 1) {
-        if (lane == j0) my_dot = p;
-      } else if (li == 0) {
-        dot_lds[j0] = p;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int jj = j0 + u * EPW;
+        float p = 0.f;
+#pragma unroll
+        for (int c = 0; c < CPL; ++c)
+          p += gv[c].x * v[u][c].x + gv[c].y * v[u][c].y + gv[c].z * v[u][c].z +
+               gv[c].w * v[u][c].w;
+        p = group_sum<LPE>(p);
+        if (EPW == 1) {
+          if (lane == jj) my_dot = p;
+        } else if (li == 0 && jj < cnt) {
+          dot_lds[jj] = p;
+        }
       }
     }
     if (EPW > 1) {
@@ -385,11 +397,22 @@ __global__ void __launch_bounds__(256) edge_bwd_src_kernel(BwdArgs g) {
           for (int c = 0; c < CPL; ++c) acc[c] = fma4(wsc[u], v[u][c], acc[c]);
       }
     } else {
-      for (int j0 = grp; j0 < cnt; j0 += EPW) {
-        const float4* rp = go4 + (int64_t)src_lds[j0] * g.go_stride4;
-        const float wj = w_lds[j0];
+      for (int j0 = grp; j0 < cnt; j0 += EPW * U) {
+        float4 v[U][CPL];
+        float wj[U];
 #pragma unroll
-        for (int c = 0; c < CPL; ++c) acc[c] = fma4(wj, rp[off4[c]], acc[c]);
+        for (int u = 0; u < U; ++u) {
+          const int jj = j0 + u * EPW;
+          const int jc = min(jj, cnt - 1);
+          const float4* rp = go4 + (int64_t)src_lds[jc] * g.go_stride4;
+          wj[u] = jj < cnt ? w_lds[jc] : 0.f;
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) v[u][c] = rp[off4[c]];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) acc[c] = fma4(wj[u], v[u][c], acc[c]);
       }
       wave_lds_sync();
     }
