@@ -592,7 +592,7 @@ inline unsigned grid_for(int64_t n, int block = 256, int64_t cap = 16384) {
 
 template <int LPE, int CPL>
 int launch_edge_forward(unsigned grid, size_t lds, hipStream_t st, const EdgeFwdArgs& g) {
-  constexpr int U = CPL <= 1 ? 8 : (CPL <= 2 ? 4 : (CPL <= 4 ? 2 : 1));
+  constexpr int U = CPL <= 1 ? 8 : (CPL <= 4 ? 4 : 2);
   // one head per item with whole 64-lane chunks: every chunk's weight is wave-uniform
   const bool scalar_w = (LPE == 64) && g.HS == 1 && ((g.Fp / 4) % 64 == 0);
   if (scalar_w)

@@ -24,15 +24,15 @@ namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
-constexpr int BM = 128, BN = 128, THREADS = 256;
+constexpr int BM = 128, BN = 128;
 constexpr int KSTEP = 32;   // split-K / tail slice granularity
 
 // One operand tile of ROWS rows x BK k. KC: k-contiguous in memory (row stride ld).
-template <bool KC, int ROWS, int BK>
+template <bool KC, int ROWS, int BK, int NT>
 struct Tile {
   static constexpr int LD = KC ? BK + 4 : ROWS + 4;
   static constexpr int SIZE = KC ? ROWS * LD : BK * LD;   // floats per stage
-  static constexpr int NV = ROWS * BK / 4 / THREADS;      // float4 per thread
+  static constexpr int NV = ROWS * BK / 4 / NT;           // float4 per thread
   // VEC (16-byte aligned rows, ld % 4 == 0): every thread issues NV float4 loads from clamped
   // in-bounds addresses and zeroes the components outside the matrix; otherwise scalar loads.
   template <bool VEC>
@@ -40,7 +40,7 @@ struct Tile {
                                      int64_t rmax, int64_t k0, int64_t kmax, float4 (&v)[NV]) {
 #pragma unroll
     for (int c = 0; c < NV; ++c) {
-      const int idx = threadIdx.x + THREADS * c;
+      const int idx = threadIdx.x + NT * c;
       int64_t r, k;
       if (KC) { r = r0 + idx / (BK / 4); k = k0 + 4 * (idx % (BK / 4)); }
       else { k = k0 + idx / (ROWS / 4); r = r0 + 4 * (idx % (ROWS / 4)); }
@@ -68,7 +68,7 @@ struct Tile {
                                       int64_t k0, int64_t kmax) {
 #pragma unroll
     for (int c = 0; c < NV; ++c) {
-      const int idx = threadIdx.x + THREADS * c;
+      const int idx = threadIdx.x + NT * c;
       const int row = KC ? idx / (BK / 4) : 4 * (idx % (ROWS / 4));
       const int kk = KC ? 4 * (idx % (BK / 4)) : idx / (ROWS / 4);
       if (VEC) {
@@ -168,41 +168,42 @@ __device__ inline void tile_of(int64_t b, int64_t T, int64_t tiles_n, int64_t& t
 
 // Epilogue shared by both kernels. C/D map of a 32x32 f32 MFMA block: col = lane&31,
 // row = (r&3) + 8*(r>>2) + 4*(lane>>5).
-__device__ inline void write_tile(const GemmArgs& g, floatx16 (&acc)[2][2], int tail_z,
+template <int MB, int NB>
+__device__ inline void write_tile(const GemmArgs& g, floatx16 (&acc)[MB][NB], int tail_z,
                                   int64_t tail_ti, int64_t m0, int64_t n0, int wm, int wn,
                                   int lane) {
   const int64_t M = g.M, N = g.N;
   if (tail_z >= 0) {   // tail slice: tile-local partial, summed by tail_fixup_kernel
     float* P = g.tail_partial + ((int64_t)tail_z * g.tail_rem + tail_ti) * (BM * BN);
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
+    for (int mi = 0; mi < MB; ++mi)
 #pragma unroll
-      for (int ni = 0; ni < 2; ++ni)
+      for (int ni = 0; ni < NB; ++ni)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int rl = wm * 64 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          P[rl * BN + wn * 64 + ni * 32 + (lane & 31)] = acc[mi][ni][r];
+          const int rl = wm * (MB * 32) + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          P[rl * BN + wn * (NB * 32) + ni * 32 + (lane & 31)] = acc[mi][ni][r];
         }
     return;
   }
 #pragma unroll
-  for (int mi = 0; mi < 2; ++mi)
+  for (int mi = 0; mi < MB; ++mi)
 #pragma unroll
-    for (int ni = 0; ni < 2; ++ni) {
-      const int64_t col = n0 + wn * 64 + ni * 32 + (lane & 31);
+    for (int ni = 0; ni < NB; ++ni) {
+      const int64_t col = n0 + wn * (NB * 32) + ni * 32 + (lane & 31);
       if (col >= N) continue;
       if (g.splits > 1) {   // partial slab z: plain [M][N] store, reduced by splitk_reduce_kernel
         float* P = g.partial + ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * M * N;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int64_t row = m0 + wm * 64 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          const int64_t row = m0 + wm * (MB * 32) + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
           if (row < M) P[row * N + col] = acc[mi][ni][r];
         }
         continue;
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int64_t row = m0 + wm * 64 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int64_t row = m0 + wm * (MB * 32) + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         if (row < M) store_out(g, blockIdx.y, row, col, acc[mi][ni][r]);
       }
     }
@@ -211,10 +212,12 @@ __device__ inline void write_tile(const GemmArgs& g, floatx16 (&acc)[2][2], int 
 // A_KC: A is k-contiguous (sak == 1, ld = sam) else m-contiguous; B_KC: B is k-contiguous
 // (sbk == 1, ld = sbn) else n-contiguous. TAG only separates the symbol names of the call sites
 // in profiles (0 = forward projection, 1 = auxiliary products, 2 = split-K weight gradient).
-template <bool A_KC, bool B_KC, bool VEC, int TAG, int BK, int MINB>
-__global__ void __launch_bounds__(THREADS, MINB) gemm_f32_kernel(GemmArgs g) {
-  using TA = Tile<A_KC, BM, BK>;
-  using TB = Tile<B_KC, BN, BK>;
+// WGM x WGN waves per workgroup, each owning (BM/WGM) x (BN/WGN) = MB x NB MFMA blocks of 32x32.
+template <bool A_KC, bool B_KC, bool VEC, int TAG, int BK, int MINB, int WGM, int WGN>
+__global__ void __launch_bounds__(64 * WGM * WGN, MINB) gemm_f32_kernel(GemmArgs g) {
+  constexpr int NT = 64 * WGM * WGN, MB = 4 / WGM, NB = 4 / WGN;
+  using TA = Tile<A_KC, BM, BK, NT>;
+  using TB = Tile<B_KC, BN, BK, NT>;
   constexpr int STAGE = TA::SIZE + TB::SIZE;
   __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
 
@@ -246,14 +249,14 @@ __global__ void __launch_bounds__(THREADS, MINB) gemm_f32_kernel(GemmArgs g) {
   const float* __restrict__ B = g.B + blockIdx.y * g.b_bs;
   const int64_t M = g.M, N = g.N;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WGN, wn = wave % WGN;
   const int il = lane & 31, h4 = 4 * (lane >> 5);
 
-  floatx16 acc[2][2];
+  floatx16 acc[MB][NB];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MB; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NB; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
@@ -276,33 +279,35 @@ __global__ void __launch_bounds__(THREADS, MINB) gemm_f32_kernel(GemmArgs g) {
     }
     const float* ai = cur;
     const float* bi = cur + TA::SIZE;
-    float4 fa[2], fb[2];
+    float4 fa[MB], fb[NB];
 #pragma unroll
-    for (int x = 0; x < 2; ++x) {
-      fa[x] = TA::frag(ai, wm * 64 + x * 32 + il, h4);
-      fb[x] = TB::frag(bi, wn * 64 + x * 32 + il, h4);
-    }
+    for (int x = 0; x < MB; ++x) fa[x] = TA::frag(ai, wm * (MB * 32) + x * 32 + il, h4);
+#pragma unroll
+    for (int x = 0; x < NB; ++x) fb[x] = TB::frag(bi, wn * (NB * 32) + x * 32 + il, h4);
 #pragma unroll
     for (int grp = 0; grp < BK / 8; ++grp) {
-      float4 na[2], nb[2];
+      float4 na[MB], nb[NB];
       if (grp + 1 < BK / 8) {
 #pragma unroll
-        for (int x = 0; x < 2; ++x) {
-          na[x] = TA::frag(ai, wm * 64 + x * 32 + il, 8 * (grp + 1) + h4);
-          nb[x] = TB::frag(bi, wn * 64 + x * 32 + il, 8 * (grp + 1) + h4);
-        }
+        for (int x = 0; x < MB; ++x)
+          na[x] = TA::frag(ai, wm * (MB * 32) + x * 32 + il, 8 * (grp + 1) + h4);
+#pragma unroll
+        for (int x = 0; x < NB; ++x)
+          nb[x] = TB::frag(bi, wn * (NB * 32) + x * 32 + il, 8 * (grp + 1) + h4);
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float a0 = get4(fa[0], j), a1 = get4(fa[1], j);
-        const float b0 = get4(fb[0], j), b1 = get4(fb[1], j);
-        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
-      }
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int mi = 0; mi < MB; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NB; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(fa[mi], j), get4(fb[ni], j),
+                                                              acc[mi][ni], 0, 0, 0);
       if (grp + 1 < BK / 8) {
-        fa[0] = na[0]; fa[1] = na[1]; fb[0] = nb[0]; fb[1] = nb[1];
+#pragma unroll
+        for (int x = 0; x < MB; ++x) fa[x] = na[x];
+#pragma unroll
+        for (int x = 0; x < NB; ++x) fb[x] = nb[x];
       }
     }
     if (more) {
@@ -312,13 +317,14 @@ __global__ void __launch_bounds__(THREADS, MINB) gemm_f32_kernel(GemmArgs g) {
     __syncthreads();
   }
 
-  write_tile(g, acc, tail_z, tail_ti, m0, n0, wm, wn, lane);
+  write_tile<MB, NB>(g, acc, tail_z, tail_ti, m0, n0, wm, wn, lane);
 }
 
 // K-tile depth / occupancy of the GEMM kernel, env GATX_GEMM_BK (tuning only): 17 (default) =
 // BK 16 at 4 workgroups per CU (LDS 4 x 40 KB, <= 128 VGPRs), 16 = BK 16 at 3, 32 = BK 32 at 2,
 // 64 = BK 64 at 1. Measured on the PPI shapes: 118 / 115 / 111 / 93 TF (occupancy hides the
-// barrier and LDS latency that one K-tile of MFMAs cannot).
+// barrier and LDS latency that one K-tile of MFMAs cannot). 8-wave workgroups with 32 x 64 wave
+// tiles (84 VGPRs, 2 workgroups per CU) measured 113 TF, no better; the template keeps WGM x WGN.
 int gemm_variant() {
   static const int v = [] {
     const char* e = getenv("GATX_GEMM_BK");
@@ -338,10 +344,10 @@ int launch_gemm(const GemmArgs& g0, bool a_kc, bool b_kc, int batch, hipStream_t
   const int var = gemm_variant();
 #define GATX_GEMM_V(AK, BKC, V)                                                                 \
   do {                                                                                         \
-    if (var == 16) gemm_f32_kernel<AK, BKC, V, TAG, 16, 3><<<grid, THREADS, 0, stream>>>(g);   \
-    else if (var == 17) gemm_f32_kernel<AK, BKC, V, TAG, 16, 4><<<grid, THREADS, 0, stream>>>(g); \
-    else if (var == 64) gemm_f32_kernel<AK, BKC, V, TAG, 64, 1><<<grid, THREADS, 0, stream>>>(g); \
-    else gemm_f32_kernel<AK, BKC, V, TAG, 32, 2><<<grid, THREADS, 0, stream>>>(g);             \
+    if (var == 16) gemm_f32_kernel<AK, BKC, V, TAG, 16, 3, 2, 2><<<grid, 256, 0, stream>>>(g);  \
+    else if (var == 17) gemm_f32_kernel<AK, BKC, V, TAG, 16, 4, 2, 2><<<grid, 256, 0, stream>>>(g); \
+    else if (var == 64) gemm_f32_kernel<AK, BKC, V, TAG, 64, 1, 2, 2><<<grid, 256, 0, stream>>>(g); \
+    else gemm_f32_kernel<AK, BKC, V, TAG, 32, 2, 2, 2><<<grid, 256, 0, stream>>>(g);            \
   } while (0)
 #define GATX_GEMM_GO(AK, BKC)                                                                  \
   do {                                                                                        \
@@ -375,13 +381,14 @@ int64_t resident_blocks() {
   if (cached) return cached;
   int dev = 0, cus = 0, per_cu = 0;
   const int var = gemm_variant();
-  const void* fn = var == 17 ? reinterpret_cast<const void*>(&gemm_f32_kernel<true, true, true, 0, 16, 4>)
-                 : var == 16 ? reinterpret_cast<const void*>(&gemm_f32_kernel<true, true, true, 0, 16, 3>)
-                 : var == 64 ? reinterpret_cast<const void*>(&gemm_f32_kernel<true, true, true, 0, 64, 1>)
-                             : reinterpret_cast<const void*>(&gemm_f32_kernel<true, true, true, 0, 32, 2>);
+  int nt = 256;
+  const void* fn = reinterpret_cast<const void*>(&gemm_f32_kernel<true, true, true, 0, 32, 2, 2, 2>);
+  if (var == 16) fn = reinterpret_cast<const void*>(&gemm_f32_kernel<true, true, true, 0, 16, 3, 2, 2>);
+  if (var == 17) fn = reinterpret_cast<const void*>(&gemm_f32_kernel<true, true, true, 0, 16, 4, 2, 2>);
+  if (var == 64) fn = reinterpret_cast<const void*>(&gemm_f32_kernel<true, true, true, 0, 64, 1, 2, 2>);
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, THREADS, 0) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, nt, 0) != hipSuccess ||
       cus <= 0 || per_cu <= 0) {
     (void)hipGetLastError();
     return cached = 512;
