@@ -168,7 +168,8 @@ def run_rmat(args, world, rank, dev):
     elapsed = time.perf_counter() - t0
     set_kernel_timer(None)
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms = elapsed / args.steps * 1e3
@@ -248,10 +249,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU over RCCL. Test-only overrides (exercise the multi-rank logic on a
+    # one-GPU box): GATX_BENCH_BACKEND=gloo, GATX_BENCH_ONE_DEVICE=1 (every rank on cuda:0).
+    dev_idx = 0 if os.environ.get("GATX_BENCH_ONE_DEVICE") == "1" else local
+    backend = os.environ.get("GATX_BENCH_BACKEND", "nccl")
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    dev = torch.device(f"cuda:{local}")
+        torch.cuda.set_device(dev_idx)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{dev_idx}"))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device(f"cuda:{dev_idx}")
     if args.workload == "rmat":
         run_rmat(args, world, rank, dev)
         if world > 1:
@@ -322,7 +330,8 @@ def main():
     elapsed = time.perf_counter() - t0
     set_kernel_timer(None)
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms = elapsed / args.steps * 1e3

@@ -56,7 +56,12 @@ def allreduce_gradients(params: Iterable[torch.nn.Parameter], world: int | None 
             continue
         if bucket:
             flat = torch.cat([b.reshape(-1) for b in bucket])
-            dist.all_reduce(flat, group=group)
+            if flat.is_cuda and dist.get_backend(group) != "nccl":   # gloo: host staging
+                host = flat.cpu()
+                dist.all_reduce(host, group=group)
+                flat.copy_(host)
+            else:
+                dist.all_reduce(flat, group=group)
             flat.mul_(1.0 / world)
             off = 0
             for b in bucket:
