@@ -234,12 +234,15 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--graphs", type=int, default=20, help="PPI graphs per rank")
+    ap.add_argument("--graphs", type=int, default=None,
+                    help="graphs per rank (PPI default 20, PATTERN default 32)")
     ap.add_argument("--mode", choices=["fwd", "train"], default="fwd")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--attention-penalty", type=float, default=0.0,
                     help="PPI_GAT attention_penalty (train mode)")
-    ap.add_argument("--workload", choices=["ppi", "rmat"], default="ppi")
+    ap.add_argument("--workload", choices=["ppi", "pattern", "rmat"], default="ppi",
+                    help="ppi: the BASELINE metric; pattern: config 4 (batch-sharded PATTERN "
+                         "training); rmat: config 5")
     ap.add_argument("--rmat-nodes", type=int, default=10_000_000)
     ap.add_argument("--rmat-edges", type=int, default=160_000_000)
     ap.add_argument("--cached-graph", action="store_true",
@@ -272,18 +275,24 @@ def main():
     from gatx.distributed import allreduce_gradients
     from gatx.functional import KernelTimer, set_kernel_timer
 
-    cfg = dict(data_config["PPI"])
+    ds = "PATTERN" if args.workload == "pattern" else "PPI"
+    if args.graphs is None:
+        args.graphs = 32 if ds == "PATTERN" else 20
+    cfg = dict(data_config[ds])
     torch.manual_seed(0)
     model = GATModel(**cfg).to(dev)
     model.train(args.mode == "train")
     if args.mode == "fwd":
         model.eval()
-    b = gd.dataset_batch("PPI", args.graphs, graph_seed=42 + 1000 * rank, feature_seed=1 + rank)
+    b = gd.dataset_batch(ds, args.graphs, graph_seed=42 + 1000 * rank, feature_seed=1 + rank)
     x = torch.from_numpy(b.x).to(dev)
     ei = torch.from_numpy(b.edge_index).to(dev)
     y = (torch.rand(b.num_nodes, cfg["num_classes"], device=dev) > 0.5).float()
     opt = torch.optim.Adam(model.parameters(), lr=cfg["learning_rate"])
     loss_fn = torch.nn.BCEWithLogitsLoss()
+    if ds == "PATTERN":   # PatternGAT (models/pattern_gat.py:11-15): class-balanced BCE
+        loss_fn = torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([1 / 0.1765], device=dev))
+        y = y[:, 0]
     params = [p for p in model.parameters()]
 
     def step():
@@ -292,6 +301,15 @@ def main():
         if args.mode == "fwd":
             with torch.no_grad():
                 return model(x, ei)
+        if ds == "PATTERN":   # PatternGAT.training_step (models/pattern_gat.py:18-25)
+            out = model(x, ei).squeeze(-1)
+            loss = loss_fn(out, y)
+            opt.zero_grad(set_to_none=True)
+            loss.backward()
+            if world > 1:
+                allreduce_gradients(params, world)
+            opt.step()
+            return out
         # PPI_GAT.training_step (models/ppi_gat.py:15-33): BCE + the attention norm, computed
         # every step (logged; added to the loss only with a non-zero attention_penalty)
         out, ei2, atts = model.forward_and_return_attention(x, ei)
@@ -394,14 +412,16 @@ def main():
     other = ordered[1] if len(ordered) > 1 else None
 
     result = {
-        "metric": "GAT-layer edges/sec + achieved HBM GB/s, PPI 3-layer fwd"
+        "metric": f"GAT-layer edges/sec + achieved HBM GB/s, {ds} {len(dims)}-layer fwd"
                   + ("" if args.mode == "fwd" else " (+bwd, train step)"),
         "value": round(value, 1), "unit": "layer-edges/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
-        "data": "synthetic PPI-shaped graphs (uniform random edges, N(0,1) features), xavier "
+        "data": f"synthetic {ds}-shaped graphs (uniform random edges, N(0,1) features), xavier "
                 "weights",
-        "config": {"workload": f"PPI 3-layer GAT {args.mode} (4/4/6 heads, 256/256/121), "
+        "config": {"workload": f"{ds} {len(dims)}-layer GAT {args.mode} ("
+                               + "/".join(str(d[1]) for d in dims) + " heads, "
+                               + "/".join(str(d[2]) for d in dims) + f"), "
                                f"{args.graphs} graphs per GPU"
                                + (", CSR cached" if args.cached_graph else ", CSR built per step"),
                    "graphs_per_gpu": args.graphs, "nodes_per_gpu": N, "edges_per_layer": E2,
@@ -414,7 +434,7 @@ def main():
         "roofline_other": other,
         "kernels": kern,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.mode == "fwd":
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.mode == "fwd" and ds == "PPI":
         model_np = {"layers": [(l.W.weight.detach().cpu().numpy(), l.a.weight.detach().cpu().numpy())
                                for l in model.gat_layer_list],
                     "skips": [None if isinstance(s, torch.nn.Identity) else s.weight.detach().cpu().numpy()

@@ -242,3 +242,50 @@ def calc_attention_norm_grad(edge_index, attention_list, g=1.0):
         t = al * d - al.dtype.type(1.0)   # in alpha's precision, like the reference's fp32
         out.append(g * np.sign(t).astype(np.float64) * deg[:, None] / (E * L))
     return out
+
+
+def gat_model_forward_backward(x, edge_index, layers, skips, num_heads, out_features, concat,
+                               add_skip, g_out, dtype=np.float64):
+    """gat_model_forward plus its backward for an upstream gradient g_out: the layer backward
+    (gat_layer_backward) chained through ELU (d elu = 1 for x > 0 else exp(x)), the skip add
+    (concat: add; head-mean: add of the skip's per-head mean, models/GATModel.py:135-145) and
+    the skip projection. Returns (out, {"W": [...], "a": [...], "skip": [...], "x": g_x})."""
+    x = np.asarray(x, dtype=dtype)
+    L = len(layers)
+    saved, skip_i = [], 0
+    for i in range(L):
+        inp = x
+        W, a = layers[i]
+        o, edge_index, alpha, cache = gat_layer_forward(x, edge_index, W, a, num_heads[i],
+                                                        out_features[i], concat[i], dtype=dtype)
+        Ws = None
+        if add_skip[i]:
+            Ws = skips[skip_i]
+            skip_i += 1
+            so = inp if Ws is None else inp @ np.asarray(Ws, dtype=dtype).T
+            o = o + (so if concat[i] else so.reshape(-1, num_heads[i], out_features[i]).mean(axis=1))
+        saved.append((inp, cache, o, Ws))
+        x = elu(o) if i != L - 1 else o
+    g = np.asarray(g_out, dtype=dtype)
+    gW, ga, gs = [None] * L, [None] * L, []
+    for i in reversed(range(L)):
+        inp, cache, pre, Ws = saved[i]
+        g_pre = g * np.where(pre > 0, 1.0, np.exp(np.minimum(pre, 0))) if i != L - 1 else g
+        gr = gat_layer_backward(cache, g_pre)
+        gW[i], ga[i] = gr["W"], gr["a"]
+        g_inp = gr["x"]
+        if add_skip[i]:
+            if concat[i]:
+                g_so = g_pre
+            else:
+                g_so = np.repeat(g_pre[:, None, :] / num_heads[i], num_heads[i], axis=1)
+                g_so = g_so.reshape(g_pre.shape[0], -1)
+            if Ws is None:
+                g_inp = g_inp + g_so
+                gs.append(None)
+            else:
+                Wsd = np.asarray(Ws, dtype=dtype)
+                gs.append(g_so.T @ inp)
+                g_inp = g_inp + g_so @ Wsd
+        g = g_inp
+    return x, {"W": gW, "a": ga, "skip": gs[::-1], "x": g}

@@ -515,3 +515,47 @@ def test_rmat_full_size(device):
         assert np.abs(got - ref).max() <= 1e-4, (int(n), e - b, np.abs(got - ref).max())
         ga = alpha[pos].cpu().numpy()
         assert np.abs(ga - al).max() <= 1e-4, (int(n), e - b)
+
+
+@pytest.mark.parametrize("name", MODEL_CASES)
+def test_model_backward_vs_oracle(name, device):
+    """GATModel training gradients (fused skip + ELU epilogues, identity-skip folding, the
+    reassociated first-layer backward) against the oracle's layer backward chained through the
+    model wiring in fp64."""
+    gatx = _gatx()
+    from gatx import data as gd
+    c = load_model_case(name)
+    cfg = c["cfg"]
+    model = gatx.GATModel(**cfg).to(device).train()
+    with torch.no_grad():
+        for i, (W, a) in enumerate(c["layers"]):
+            model.gat_layer_list[i].W.weight.copy_(torch.from_numpy(W))
+            model.gat_layer_list[i].a.weight.copy_(torch.from_numpy(a))
+        for j, s in enumerate(c["skips"]):
+            if s is not None:
+                model.skip_layer_list[j].weight.copy_(torch.from_numpy(s))
+    x = torch.from_numpy(c["x"]).to(device)
+    ei = torch.from_numpy(c["edge_index"]).to(device)
+    out = model(x, ei)
+    g = gd.normal(31, out.numel()).reshape(tuple(out.shape)).astype(np.float32)
+    (out * torch.from_numpy(g).to(device)).sum().backward()
+    skips = [model.skip_layer_list[j].weight.detach().cpu().numpy()
+             if isinstance(model.skip_layer_list[j], torch.nn.Linear) else None
+             for j in range(len(model.skip_layer_list))]
+    ref_out, ref = orc.gat_model_forward_backward(
+        c["x"], c["edge_index"], c["layers"], skips, cfg["num_heads_per_layer"],
+        cfg["head_output_features_per_layer"][1:], cfg["heads_concat_per_layer"],
+        cfg["add_skip_connection"], g)
+    # model level: the reference's own fp32 noise floor grows with depth and logit size
+    # (PATTERN logits ~42), so 2e-4 relative to the gradient's scale
+    tol = 2e-4
+    for i, lay in enumerate(model.gat_layer_list):
+        for k, t in (("W", lay.W.weight.grad), ("a", lay.a.weight.grad)):
+            r = ref[k][i]
+            err = np.abs(t.cpu().numpy() - r).max()
+            assert err <= tol * max(1.0, np.abs(r).max()), (name, i, k, err, np.abs(r).max())
+    for j, s in enumerate(model.skip_layer_list):
+        if isinstance(s, torch.nn.Linear):
+            r = ref["skip"][j]
+            err = np.abs(s.weight.grad.cpu().numpy() - r).max()
+            assert err <= tol * max(1.0, np.abs(r).max()), (name, "skip", j, err)
