@@ -285,7 +285,8 @@ __global__ void __launch_bounds__(256) max_bwd_kernel(const float* __restrict__ 
     const long long ent = argmax[1 + j];
     const long long e = ent / NH;
     const int h = (int)(ent - e * NH);
-    g_corr_src[(int64_t)col[e] * NH + h] += share;
+    if (g_corr_src) g_corr_src[(int64_t)col[e] * NH + h] += share;
+    else G_aug[(int64_t)col[e] * ldg + Dp + h] += share;   // after the src pass wrote g_s_src
     G_aug[(int64_t)rowidx[e] * ldg + Dp + NH + h] += share;
   }
 }
@@ -310,7 +311,8 @@ __global__ void __launch_bounds__(256) max_bwd_scan_kernel(const float* __restri
     const int h = (int)(t - e * NH);
     const int64_t s = col[e], d = rowidx[e];
     if (S[s * S2 + h] + S[d * S2 + NH + h] == M) {
-      atomicAdd(&g_corr_src[s * NH + h], share);
+      if (g_corr_src) atomicAdd(&g_corr_src[s * NH + h], share);
+      else atomicAdd(&G_aug[s * ldg + Dp + h], share);
       atomicAdd(&G_aug[d * ldg + Dp + NH + h], share);
     }
   }
@@ -432,7 +434,7 @@ __global__ void __launch_bounds__(256) edge_bwd_src_kernel(BwdArgs g) {
   }
   if (!g.const_att) {
     gs = group_sum<64>(gs);
-    if (lane == 0) row[Dp + h] = gs + g.g_corr[s * NH + h];
+    if (lane == 0) row[Dp + h] = gs + (g.g_corr ? g.g_corr[s * NH + h] : 0.f);
   }
 }
 

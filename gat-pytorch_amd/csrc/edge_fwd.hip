@@ -45,7 +45,8 @@ __global__ void __launch_bounds__(256) attention_max_kernel(const int32_t* __res
 }
 
 __global__ void __launch_bounds__(256) max_final_kernel(const float* __restrict__ part, int nb,
-                                                        uint32_t* __restrict__ M_ord) {
+                                                        uint32_t* __restrict__ M_ord,
+                                                        long long* __restrict__ argmax) {
   float m = -INFINITY;
   for (int b = threadIdx.x; b < nb; b += blockDim.x) m = fmaxf(m, part[b]);
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
@@ -55,6 +56,7 @@ __global__ void __launch_bounds__(256) max_final_kernel(const float* __restrict_
   if (threadIdx.x == 0) {
     m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
     *M_ord = m > -INFINITY ? float_to_ord(m) : 0u;
+    if (argmax) argmax[0] = 0;   // tie counter for attention_alpha (no separate fill)
   }
 }
 
@@ -701,14 +703,14 @@ extern "C" int gatx_pad_rows(const float* src, int64_t rows, int64_t cols, int64
 }
 
 extern "C" int gatx_attention_max(const int32_t* col, const int32_t* rowidx, int64_t E2,
-                                  const float* S, int NH, uint32_t* M_ord, void* workspace,
-                                  gatx_stream_t s) {
+                                  const float* S, int NH, uint32_t* M_ord, int64_t* argmax,
+                                  void* workspace, gatx_stream_t s) {
   hipStream_t st = (hipStream_t)s;
   const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(E2, 256), kMaxBlocks));
   float* part = (float*)workspace;
   attention_max_kernel<<<nb, 256, 0, st>>>(col, rowidx, E2, S, NH, part);
   GATX_LAUNCH_CHECK("attention_max");
-  max_final_kernel<<<1, 256, 0, st>>>(part, nb, M_ord);
+  max_final_kernel<<<1, 256, 0, st>>>(part, nb, M_ord, (long long*)argmax);
   GATX_LAUNCH_CHECK("attention_max_final");
   return 0;
 }

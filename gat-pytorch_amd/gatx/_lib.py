@@ -54,7 +54,7 @@ SIGNATURES = {
                                    c_i, P, c_sz, P]),
     "gatx_node_scores": (c_i, [P, c_i64, c_i, c_i, P, P, P]),
     "gatx_attention_max_workspace_bytes": (c_sz, []),
-    "gatx_attention_max": (c_i, [P, P, c_i64, P, c_i, P, P, P]),
+    "gatx_attention_max": (c_i, [P, P, c_i64, P, c_i, P, P, P, P]),
     "gatx_edge_forward": (c_i, [P, P, P, P, P, P, P, c_i64, c_i64, c_i, c_i, c_i, c_i, P, c_f,
                                 c_u64, P, P, P, P, P]),
     "gatx_attention_alpha": (c_i, [P, P, P, c_i64, P, P, P, c_i, c_i, P, P, P]),

@@ -218,8 +218,9 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
     out = torch.empty((N, sh.out_cols), **f32)
     alpha = torch.empty((E2, sh.NH), **f32)
     den = torch.empty((N, sh.NH), **f32)
-    argmax = torch.zeros(ARGMAX_CAP + 2, dtype=torch.int64, device=dev)
-    M_ord = torch.zeros(1, dtype=torch.int32, device=dev)
+    # argmax[0] (tie count) is reset by gatx_attention_max; M_ord is written by it
+    argmax = torch.empty(ARGMAX_CAP + 2, dtype=torch.int64, device=dev)
+    M_ord = torch.empty(1, dtype=torch.int32, device=dev)
     resid_p = ptr(resid) if resid is not None else None
     W_aug = augmented_weight(W, a, sh)
     saved = dict(W_aug=W_aug, M_ord=M_ord, den=den, argmax=argmax, Wh=None)
@@ -238,7 +239,7 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
                      0, 0, *gemm_workspace(N, sh.H2, sh.F_in, dev), s)
             with _span("attention_max", (E2, sh.NH)):
                 call("gatx_attention_max", ptr(graph.col), ptr(graph.rowidx), E2, ptr(S),
-                     sh.NH, ptr(M_ord), ptr(_max_ws(dev)), s)
+                     sh.NH, ptr(M_ord), ptr(argmax), ptr(_max_ws(dev)), s)
         Z = torch.empty((N, sh.NH * Fin_p), **f32)
         with _span("edge_forward", (N, E2, sh.NH, Fin_p, "x")):
             hs_x = max(d for d in range(1, 9) if sh.NH % d == 0)   # heads sharing one x row
@@ -273,7 +274,7 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
     if not sh.const:
         with _span("attention_max", (E2, sh.NH)):
             call("gatx_attention_max", ptr(graph.col), ptr(graph.rowidx), E2, ptr(S), sh.NH,
-                 ptr(M_ord), ptr(_max_ws(dev)), s)
+                 ptr(M_ord), ptr(argmax), ptr(_max_ws(dev)), s)
     with _span("edge_forward", (N, E2, sh.NH, sh.F, sh.concat)):
         call("gatx_edge_forward_ex", ptr(Wh), sh.Dp, sh.Fp, ptr(S), ptr(M_ord),
              ptr(graph.rowptr), ptr(graph.col), ptr(graph.perm), N, sh.NH, sh.F,
@@ -322,15 +323,15 @@ def layer_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShape, 
              sh.NH, sh.F, int(sh.concat), float(p), seed, ptr(go),
              ptr(g_alpha.contiguous()) if g_alpha is not None else None, ptr(g_raw), ptr(gsd),
              ptr(G_aug), sh.ldg, s)
-        g_corr = torch.zeros((N, sh.NH), **f32)
-        mws = torch.empty(lib.gatx_max_backward_workspace_bytes(), dtype=torch.uint8, device=dev)
-        call("gatx_max_backward", ptr(saved["argmax"]), ptr(gsd), ptr(saved["S"]),
-             ptr(saved["M_ord"]), ptr(graph.col), ptr(graph.rowidx), N, E2, sh.NH, ptr(g_corr),
-             ptr(G_aug), sh.ldg, sh.Dp, ptr(mws), s)
     call("gatx_edge_backward_src", ptr(saved["S"]), ptr(saved["M_ord"]), ptr(saved["den"]),
          ptr(graph.srowptr), ptr(graph.scol), ptr(graph.seid), ptr(graph.perm), N, E2, sh.NH,
-         sh.F, int(sh.concat), int(sh.const), float(p), seed, ptr(go), ptr(g_raw), ptr(g_corr),
+         sh.F, int(sh.concat), int(sh.const), float(p), seed, ptr(go), ptr(g_raw), None,
          ptr(G_aug), sh.ldg, s)
+    if not sh.const:   # max()'s share, added into both logit-gradient columns of G_aug
+        mws = torch.empty(lib.gatx_max_backward_workspace_bytes(), dtype=torch.uint8, device=dev)
+        call("gatx_max_backward", ptr(saved["argmax"]), ptr(gsd), ptr(saved["S"]),
+             ptr(saved["M_ord"]), ptr(graph.col), ptr(graph.rowidx), N, E2, sh.NH, None,
+             ptr(G_aug), sh.ldg, sh.Dp, ptr(mws), s)
     g_x = g_W = g_a = g_bias = None
     W_aug = saved["W_aug"]
     if need_bias and bias is not None:   # before g_pre may become g_x's accumulator
@@ -393,13 +394,12 @@ def _reassoc_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShap
          ptr(g_Z), NH * Fin_p, Fin_p, float(p), seed,
          ptr(g_alpha.contiguous()) if g_alpha is not None else None, ptr(g_raw), ptr(gsd),
          ptr(G_s), 2 * NH, 0, s)
-    g_corr = torch.zeros((N, NH), **f32)
+    call("gatx_edge_backward_src_scores", ptr(graph.srowptr), ptr(graph.seid), N, E2, NH,
+         ptr(g_raw), None, ptr(G_s), 2 * NH, 0, s)
     mws = torch.empty(lib.gatx_max_backward_workspace_bytes(), dtype=torch.uint8, device=dev)
     call("gatx_max_backward", ptr(saved["argmax"]), ptr(gsd), ptr(saved["S"]),
-         ptr(saved["M_ord"]), ptr(graph.col), ptr(graph.rowidx), N, E2, NH, ptr(g_corr),
+         ptr(saved["M_ord"]), ptr(graph.col), ptr(graph.rowidx), N, E2, NH, None,
          ptr(G_s), 2 * NH, 0, ptr(mws), s)
-    call("gatx_edge_backward_src_scores", ptr(graph.srowptr), ptr(graph.seid), N, E2, NH,
-         ptr(g_raw), ptr(g_corr), ptr(G_s), 2 * NH, 0, s)
     g_W = g_a = g_bias = None
     if need_W or need_a:
         gW_aug = torch.empty((sh.K_aug, F_in), **f32)

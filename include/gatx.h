@@ -134,10 +134,13 @@ int gatx_gemm_f32_batched(int64_t batch, int64_t M, int64_t N, int64_t K, const 
 /* ---------------------------------------------------------------- attention + aggregation */
 
 /* Global max M = max_{e,h} s_src[col[e],h] + s_dst[rowidx[e],h]  (gat_layer.py:85), written as an
- * order-preserving uint32 into *M_ord (device). workspace: gatx_attention_max_workspace_bytes(). */
+ * order-preserving uint32 into *M_ord (device). argmax (nullable): its tie counter argmax[0] is
+ * reset to 0 for the following gatx_attention_alpha. workspace:
+ * gatx_attention_max_workspace_bytes(). */
 size_t gatx_attention_max_workspace_bytes(void);
 int gatx_attention_max(const int32_t* col, const int32_t* rowidx, int64_t E2, const float* S,
-                       int NH, uint32_t* M_ord, void* workspace, gatx_stream_t stream);
+                       int NH, uint32_t* M_ord, int64_t* argmax, void* workspace,
+                       gatx_stream_t stream);
 
 /* Fused edge pass per destination segment (gat_layer.py:85-135), then the attention output:
  *   ex = exp(0.01 * (s_src[src] + s_dst[dst] - M))   (LeakyReLU(0.01) of a non-positive value)
@@ -233,9 +236,11 @@ int gatx_edge_backward_src_scores(const int32_t* srowptr, const int32_t* seid, i
                                   float* G, int64_t ldg, int64_t gs_off, gatx_stream_t stream);
 
 /* max() backward (torch splits the gradient evenly over ties): g_M = -sum gsd (two-stage
- * fixed-order reduction); g_corr_src[src,h] += g_M/k and G_aug[dst][Dp+NH+h] += g_M/k for each
- * recorded argmax entry. g_corr_src [N][NH] must be zeroed by the caller. Falls back to a full
- * scan of the edges when more than GATX_ARGMAX_CAP entries tie. */
+ * fixed-order reduction); g_M/k is added to G_aug[dst][Dp+NH+h] and to the source side for
+ * each recorded argmax entry: into g_corr_src[src,h] ([N][NH], zeroed by the caller, consumed
+ * by the src pass) or, with g_corr_src NULL, straight into G_aug[src][Dp+h] (call it after the
+ * src pass). Falls back to a full scan of the edges when more than GATX_ARGMAX_CAP entries
+ * tie. */
 size_t gatx_max_backward_workspace_bytes(void);
 int gatx_max_backward(const int64_t* argmax, const float* gsd, const float* S,
                       const uint32_t* M_ord, const int32_t* col, const int32_t* rowidx,
@@ -244,7 +249,7 @@ int gatx_max_backward(const int64_t* argmax, const float* gsd, const float* S,
 
 /* Source pass, one wave per (node s, head h): G_aug[s][h*Fp:] = sum_{e: src=s} alpha~[e,h] *
  * go[dst_e,h,:] (the message gradient), G_aug[s][Dp+h] = sum_{e: src=s} g_raw'[e,h] +
- * g_corr_src[s,h] (g_s_src; skipped for const_attention). */
+ * g_corr_src[s,h] (g_s_src, g_corr_src nullable; skipped for const_attention). */
 int gatx_edge_backward_src(const float* S, const uint32_t* M_ord, const float* den,
                            const int32_t* srowptr, const int32_t* scol, const int32_t* seid,
                            const int32_t* perm, int64_t num_nodes, int64_t E2, int NH, int F,

@@ -34,7 +34,7 @@ for (NH, F, concat) in [(4, 256, 1), (6, 121, 0), (6, 121, 1)]:
     S = torch.randn(N, 2 * NH, device=dev)
     M = torch.zeros(1, dtype=torch.int32, device=dev)
     ws = torch.empty(lib.gatx_attention_max_workspace_bytes(), dtype=torch.uint8, device=dev)
-    call("gatx_attention_max", ptr(g.col), ptr(g.rowidx), E2, ptr(S), NH, ptr(M), ptr(ws), stream())
+    call("gatx_attention_max", ptr(g.col), ptr(g.rowidx), E2, ptr(S), NH, ptr(M), None, ptr(ws), stream())
     out = torch.empty(N, NH * F if concat else F, device=dev)
     alpha = torch.empty(E2, NH, device=dev)
     den = torch.empty(N, NH, device=dev)

@@ -25,7 +25,7 @@ Wh = torch.randn(N, NH * Fp, device=dev)
 S = torch.randn(N, 2 * NH, device=dev)
 M = torch.zeros(1, dtype=torch.int32, device=dev)
 mws = torch.empty(lib.gatx_attention_max_workspace_bytes(), dtype=torch.uint8, device=dev)
-call("gatx_attention_max", ptr(g.col), ptr(g.rowidx), E2, ptr(S), NH, ptr(M), ptr(mws),
+call("gatx_attention_max", ptr(g.col), ptr(g.rowidx), E2, ptr(S), NH, ptr(M), None, ptr(mws),
      torch.cuda.current_stream().cuda_stream)
 out = torch.empty(N, NH * F, device=dev)
 den = torch.empty(N, NH, device=dev)
