@@ -7,7 +7,8 @@
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/$1
 mkdir -p "$OUT"
-step() { echo "== $1"; shift; "$@"; rc=$?; echo "rc=$rc"; [ $rc -ne 0 ] && exit $rc; return 0; }
+exec 3>&1   # progress lines go to the call's stdout, never into a step's redirected output
+step() { echo "== $1" >&3; shift; "$@"; rc=$?; echo "rc=$rc" >&3; [ $rc -ne 0 ] && exit $rc; return 0; }
 step tests timeout -k 10 600 python -m pytest "$R/tests" -m gpu -x -q -p no:cacheprovider \
   --junitxml="$OUT/gpu_tests.xml" > "$OUT/gpu_tests.log" 2>&1
 tail -2 "$OUT/gpu_tests.log"
