@@ -17,116 +17,15 @@
 // can be split along K (tail split) so it does not leave most of the chip idle. A barrier-free
 // variant streaming each wave's fragments from L1/L2 into registers (no LDS) reached only 74 TF
 // on the same shapes (TA-bound), so operands are shared through LDS.
-#include "gatx_common.h"
+#include "gemm_common.h"
+
+#include <string.h>
+
+#include <string.h>
 
 namespace gatx {
 namespace {
-
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-
-constexpr int BM = 128, BN = 128;
-constexpr int KSTEP = 32;   // split-K / tail slice granularity
-
-// One operand tile of ROWS rows x BK k. KC: k-contiguous in memory (row stride ld).
-template <bool KC, int ROWS, int BK, int NT>
-struct Tile {
-  static constexpr int LD = KC ? BK + 4 : ROWS + 4;
-  static constexpr int SIZE = KC ? ROWS * LD : BK * LD;   // floats per stage
-  static constexpr int NV = ROWS * BK / 4 / NT;           // float4 per thread
-  // VEC (16-byte aligned rows, ld % 4 == 0): every thread issues NV float4 loads from clamped
-  // in-bounds addresses and zeroes the components outside the matrix; otherwise scalar loads.
-  template <bool VEC>
-  static __device__ inline void load(const float* __restrict__ P, int64_t ld, int64_t r0,
-                                     int64_t rmax, int64_t k0, int64_t kmax, float4 (&v)[NV]) {
-#pragma unroll
-    for (int c = 0; c < NV; ++c) {
-      const int idx = threadIdx.x + NT * c;
-      int64_t r, k;
-      if (KC) { r = r0 + idx / (BK / 4); k = k0 + 4 * (idx % (BK / 4)); }
-      else { k = k0 + idx / (ROWS / 4); r = r0 + 4 * (idx % (ROWS / 4)); }
-      if (VEC) {
-        // KC: lanes j run along k (valid while k + j < kmax); RC: along rows
-        const bool rok = r < rmax, kok = k < kmax;
-        const int64_t rc = rok ? r : (KC ? rmax - 1 : 0);
-        const int64_t kc = kok ? k : (KC ? 0 : kmax - 1);
-        v[c] = *(const float4*)(KC ? P + rc * ld + kc : P + kc * ld + rc);   // masked in store
-      } else {
-        float e[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const bool ok = KC ? (r < rmax && k + j < kmax) : (k < kmax && r + j < rmax);
-          e[j] = ok ? (KC ? P[r * ld + k + j] : P[k * ld + r + j]) : 0.f;
-        }
-        v[c] = make_float4(e[0], e[1], e[2], e[3]);
-      }
-    }
-  }
-  // Components outside the matrix are zeroed here, after the MFMAs of the current tile, so the
-  // loads' latency stays hidden (a select right after the load would wait for it).
-  template <bool VEC>
-  static __device__ inline void store(float* img, float4 (&v)[NV], int64_t r0, int64_t rmax,
-                                      int64_t k0, int64_t kmax) {
-#pragma unroll
-    for (int c = 0; c < NV; ++c) {
-      const int idx = threadIdx.x + NT * c;
-      const int row = KC ? idx / (BK / 4) : 4 * (idx % (ROWS / 4));
-      const int kk = KC ? 4 * (idx % (BK / 4)) : idx / (ROWS / 4);
-      if (VEC) {
-        const int64_t r = r0 + row, k = k0 + kk;
-        const bool ok = r < rmax && k < kmax;
-        const int64_t lim = KC ? kmax - k : rmax - r;
-        v[c].x = ok ? v[c].x : 0.f;
-        v[c].y = ok && lim > 1 ? v[c].y : 0.f;
-        v[c].z = ok && lim > 2 ? v[c].z : 0.f;
-        v[c].w = ok && lim > 3 ? v[c].w : 0.f;
-      }
-      const int off = KC ? row * LD + kk : kk * LD + row;
-      *(float4*)&img[off] = v[c];
-    }
-  }
-  // k = kb .. kb+3 of row `row`
-  static __device__ inline float4 frag(const float* img, int row, int kb) {
-    if (KC) return *(const float4*)&img[row * LD + kb];
-    return make_float4(img[kb * LD + row], img[(kb + 1) * LD + row], img[(kb + 2) * LD + row],
-                       img[(kb + 3) * LD + row]);
-  }
-};
-
-struct GemmArgs {
-  int64_t M, N, K;
-  const float* A; int64_t lda, a_bs;
-  const float* B; int64_t ldb, b_bs;
-  float* C0; int64_t ldc0, c0_bs;
-  int64_t n_split;
-  float* C1; int64_t ldc1, c1_bs;
-  int accumulate, a_vec, b_vec;
-  int64_t tiles_m, tiles_n;
-  // epilogue on C0 columns: C = elu?(acc (+C) + bias[col] + resid[row][col])
-  const float* bias; int64_t bias_bs;
-  const float* resid; int64_t resid_ld, resid_bs;
-  int elu;
-  int64_t k_per_split; int splits; float* partial;
-  // tail split (splits == 1): blocks >= dp_blocks each take K-slice z of one of the last
-  // tail_rem tiles and write a BM x BN partial; tail_fixup_kernel sums the slices in z order
-  int64_t dp_blocks, tail_rem; int tail_s, bm; float* tail_partial;
-};
-
-// C = elu?(v (+C) + bias + resid) for one output element (columns >= n_split go to C1 raw)
-__device__ inline void store_out(const GemmArgs& g, int64_t b, int64_t row, int64_t col, float v) {
-  float* Cb;
-  int64_t ldc, c;
-  const bool first = col < g.n_split;
-  if (first) { Cb = g.C0 + b * g.c0_bs; ldc = g.ldc0; c = col; }
-  else { Cb = g.C1 + b * g.c1_bs; ldc = g.ldc1; c = col - g.n_split; }
-  float* p = Cb + row * ldc + c;
-  if (g.accumulate) v += *p;
-  if (first) {
-    if (g.bias) v += g.bias[b * g.bias_bs + c];
-    if (g.resid) v += g.resid[b * g.resid_bs + row * g.resid_ld + c];
-    if (g.elu) v = v > 0.f ? v : expm1f(v);
-  }
-  *p = v;
-}
+using namespace gk;
 
 // Deterministic split-K combine: C = epilogue(sum over slabs in slab order), one pass.
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(GemmArgs g, int batch) {
@@ -142,7 +41,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(GemmArgs g, int batc
 
 // Tail fix-up: the last tail_rem tiles, each the sum of tail_s K-slices in slice order.
 __global__ void __launch_bounds__(256) tail_fixup_kernel(GemmArgs g) {
-  const int64_t BN = 128, TS = (int64_t)g.bm * BN, total = g.tail_rem * TS;
+  const int64_t BN = g.bn, TS = (int64_t)g.bm * BN, total = g.tail_rem * TS;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t ti = t / TS, rc = t - ti * TS, rl = rc / BN, cl = rc - rl * BN;
@@ -153,60 +52,6 @@ __global__ void __launch_bounds__(256) tail_fixup_kernel(GemmArgs g) {
     for (int z = 0; z < g.tail_s; ++z) v += g.tail_partial[((int64_t)z * g.tail_rem + ti) * TS + rc];
     store_out(g, 0, row, col, v);
   }
-}
-
-// Workgroup -> output tile. Workgroups are dealt round-robin over the 8 XCDs (b % 8), so give
-// XCD x a contiguous run of m-major tiles: an A row-tile (x rows) is then fetched into one XCD's
-// L2 and reused there by all its n-tiles. Placement only changes speed, never results.
-__device__ inline void tile_of(int64_t b, int64_t T, int64_t tiles_n, int64_t& tm, int64_t& tn) {
-  const int64_t q = T / 8, r = T % 8;
-  const int64_t xcd = b % 8, j = b / 8;
-  const int64_t t = (xcd < r) ? xcd * (q + 1) + j : r * (q + 1) + (xcd - r) * q + j;
-  tm = t / tiles_n;
-  tn = t % tiles_n;
-}
-
-// Epilogue shared by both kernels. C/D map of a 32x32 f32 MFMA block: col = lane&31,
-// row = (r&3) + 8*(r>>2) + 4*(lane>>5).
-template <int MB, int NB>
-__device__ inline void write_tile(const GemmArgs& g, floatx16 (&acc)[MB][NB], int tail_z,
-                                  int64_t tail_ti, int64_t m0, int64_t n0, int wm, int wn,
-                                  int lane) {
-  const int64_t M = g.M, N = g.N;
-  if (tail_z >= 0) {   // tail slice: tile-local partial, summed by tail_fixup_kernel
-    float* P = g.tail_partial + ((int64_t)tail_z * g.tail_rem + tail_ti) * (BM * BN);
-#pragma unroll
-    for (int mi = 0; mi < MB; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < NB; ++ni)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int rl = wm * (MB * 32) + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          P[rl * BN + wn * (NB * 32) + ni * 32 + (lane & 31)] = acc[mi][ni][r];
-        }
-    return;
-  }
-#pragma unroll
-  for (int mi = 0; mi < MB; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < NB; ++ni) {
-      const int64_t col = n0 + wn * (NB * 32) + ni * 32 + (lane & 31);
-      if (col >= N) continue;
-      if (g.splits > 1) {   // partial slab z: plain [M][N] store, reduced by splitk_reduce_kernel
-        float* P = g.partial + ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * M * N;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int64_t row = m0 + wm * (MB * 32) + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          if (row < M) P[row * N + col] = acc[mi][ni][r];
-        }
-        continue;
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t row = m0 + wm * (MB * 32) + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (row < M) store_out(g, blockIdx.y, row, col, acc[mi][ni][r]);
-      }
-    }
 }
 
 // A_KC: A is k-contiguous (sak == 1, ld = sam) else m-contiguous; B_KC: B is k-contiguous
@@ -320,6 +165,17 @@ __global__ void __launch_bounds__(64 * WGM * WGN, MINB) gemm_f32_kernel(GemmArgs
   write_tile<MB, NB>(g, acc, tail_z, tail_ti, m0, n0, wm, wn, lane);
 }
 
+// GEMM arithmetic, env GATX_GEMM (or gatx_set_gemm_mode): "x3" (default) = the split-bf16
+// kernel of gemm_x3.hip, "f32" = v_mfma_f32_32x32x2_f32.
+int g_gemm_mode = -1;   // -1: read the environment on first use; 0: f32; 1: x3
+int gemm_mode() {
+  if (g_gemm_mode < 0) {
+    const char* e = getenv("GATX_GEMM");
+    g_gemm_mode = (e && strcmp(e, "f32") == 0) ? 0 : 1;
+  }
+  return g_gemm_mode;
+}
+
 // K-tile depth / occupancy of the GEMM kernel, env GATX_GEMM_BK (tuning only): 17 (default) =
 // BK 16 at 4 workgroups per CU (LDS 4 x 40 KB, <= 128 VGPRs), 16 = BK 16 at 3, 32 = BK 32 at 2,
 // 64 = BK 64 at 1. Measured on the PPI shapes: 118 / 115 / 111 / 93 TF (occupancy hides the
@@ -342,6 +198,9 @@ int launch_gemm(const GemmArgs& g0, bool a_kc, bool b_kc, int batch, hipStream_t
   const int64_t gx = g.tail_s > 1 ? g.dp_blocks + g.tail_rem * g.tail_s : tiles;
   dim3 grid((unsigned)gx, (unsigned)batch, (unsigned)g.splits);
   const int var = gemm_variant();
+  if (gemm_mode() == 1) {
+    GATX_CALL(launch_gemm_x3(g, a_kc, b_kc, batch, TAG, stream));
+  } else {
 #define GATX_GEMM_V(AK, BKC, V)                                                                 \
   do {                                                                                         \
     if (var == 16) gemm_f32_kernel<AK, BKC, V, TAG, 16, 3, 2, 2><<<grid, 256, 0, stream>>>(g);  \
@@ -360,7 +219,8 @@ int launch_gemm(const GemmArgs& g0, bool a_kc, bool b_kc, int batch, hipStream_t
   else GATX_GEMM_GO(false, false);
 #undef GATX_GEMM_GO
 #undef GATX_GEMM_V
-  GATX_LAUNCH_CHECK("gemm_f32");
+    GATX_LAUNCH_CHECK("gemm_f32");
+  }
   if (g.splits > 1) {
     const int64_t total = g.M * g.N * batch;
     const unsigned rg = (unsigned)std::min<int64_t>(ceil_div(total, 256), 8192);
@@ -368,32 +228,53 @@ int launch_gemm(const GemmArgs& g0, bool a_kc, bool b_kc, int batch, hipStream_t
     GATX_LAUNCH_CHECK("splitk_reduce");
   }
   if (g.tail_s > 1) {
-    const int64_t total = g.tail_rem * BM * BN;
+    const int64_t total = g.tail_rem * g.bm * g.bn;
     tail_fixup_kernel<<<(unsigned)std::min<int64_t>(ceil_div(total, 256), 8192), 256, 0, stream>>>(g);
     GATX_LAUNCH_CHECK("tail_fixup");
   }
   return 0;
 }
 
-// Workgroups of one gemm_f32_kernel instance resident on the whole device at once.
-int64_t resident_blocks() {
-  static int64_t cached = 0;
-  if (cached) return cached;
+// Kernel kind for an M x N output: 0 = f32 MFMA (128 x 128 tiles); 1 = x3, 128 x 128 tiles;
+// 2 = x3, 256 x 256 tiles (one 8-wave workgroup per CU: half the LDS staging per MFMA) when the
+// output is large and the bigger tiles cover it with at most 5% more padding.
+struct Kind {
+  int id, bm, bn;
+};
+Kind choose_kind(int64_t M, int64_t N) {
+  if (gemm_mode() == 0) return {0, 128, 128};
+  static const int force = [] {   // tuning only: GATX_X3_TILE=128|256
+    const char* e = getenv("GATX_X3_TILE");
+    return e ? atoi(e) : 0;
+  }();
+  if (force == 128) return {1, 128, 128};
+  const int64_t small_area = round_up(M, 128) * round_up(N, 128);
+  const int64_t big_area = round_up(M, 256) * round_up(N, 256);
+  if (force == 256 || (M >= 256 && N >= 256 && big_area * 100 <= small_area * 105))
+    return {2, 256, 256};
+  return {1, 128, 128};
+}
+
+// Workgroups of the chosen kernel resident on the whole device at once.
+int64_t resident_blocks(const Kind& kd) {
+  static int64_t cached[3] = {0, 0, 0};
+  if (cached[kd.id]) return cached[kd.id];
   int dev = 0, cus = 0, per_cu = 0;
   const int var = gemm_variant();
-  int nt = 256;
+  int nt = kd.id == 2 ? 512 : 256;
   const void* fn = reinterpret_cast<const void*>(&gemm_f32_kernel<true, true, true, 0, 32, 2, 2, 2>);
   if (var == 16) fn = reinterpret_cast<const void*>(&gemm_f32_kernel<true, true, true, 0, 16, 3, 2, 2>);
   if (var == 17) fn = reinterpret_cast<const void*>(&gemm_f32_kernel<true, true, true, 0, 16, 4, 2, 2>);
   if (var == 64) fn = reinterpret_cast<const void*>(&gemm_f32_kernel<true, true, true, 0, 64, 1, 2, 2>);
+  if (kd.id >= 1) fn = gemm_x3_occupancy_fn(kd.id == 2 ? 1 : 0);
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, nt, 0) != hipSuccess ||
       cus <= 0 || per_cu <= 0) {
     (void)hipGetLastError();
-    return cached = 512;
+    return cached[kd.id] = kd.id == 2 ? 256 : 512;
   }
-  return cached = (int64_t)cus * per_cu;
+  return cached[kd.id] = (int64_t)cus * per_cu;
 }
 
 // Split K when the output alone cannot fill the chip (g_W = G^T x: ~70 tiles, K = #nodes):
@@ -406,8 +287,8 @@ int choose_splits(int64_t tiles, int64_t K, int64_t slots) {
 
 // Tail split of a data-parallel GEMM: the last `rem` tiles (the partial wave) are each cut into
 // s K-slices; s minimises the tail's length in waves, ceil(rem*s/slots)/s, plus the fix-up's
-// partial-tile traffic (~5 TB/s) measured in waves of 128x128xK tiles at ~157 TF.
-int choose_tail_split(int64_t tiles, int64_t K, int64_t slots, int64_t& rem) {
+// partial-tile traffic (~5 TB/s) measured in waves of bm x bn x K tiles at the kernel's rate.
+int choose_tail_split(int64_t tiles, int64_t K, int64_t slots, const Kind& kd, int64_t& rem) {
   rem = tiles % slots;
   if (rem == 0 || tiles < 1) return 1;
   static const int forced = [] {   // tuning only: GATX_TAIL_SPLIT=s forces s slices
@@ -415,13 +296,14 @@ int choose_tail_split(int64_t tiles, int64_t K, int64_t slots, int64_t& rem) {
     return e ? atoi(e) : 0;
   }();
   if (forced > 0) return (int)std::min<int64_t>(std::min(forced, 16), ceil_div(K, 2 * KSTEP));
-  const double wave_s = 2.0 * BM * BN * (double)K / (157e12 / (double)slots);
+  const double peak = kd.id == 0 ? 120e12 : 200e12;   // sustained rates, f32 vs x3
+  const double wave_s = 2.0 * kd.bm * kd.bn * (double)K / (peak / (double)slots);
   int best = 1;
   double best_c = 0.75 / 0.95;   // only clear wins: wave boundaries are soft in practice
   for (int s = 2; s <= 16; ++s) {
     if (ceil_div(K, s) < 2 * KSTEP) break;
     const double waves = (double)ceil_div(rem * s, slots) / s;
-    const double fix = (double)rem * (s + 1) * BM * BN * 4.0 / 5e12 / wave_s;
+    const double fix = (double)rem * (s + 1) * kd.bm * kd.bn * 4.0 / 5e12 / wave_s;
     if (waves + fix < best_c * 0.95) { best = s; best_c = waves + fix; }
   }
   return best;
@@ -465,11 +347,13 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
   };
   g.a_vec = aligned(A, g.lda, a_bs);
   g.b_vec = aligned(B, g.ldb, b_bs);
-  g.tiles_m = ceil_div(M, BM);
-  g.tiles_n = ceil_div(N, BN);
-  g.dp_blocks = 0; g.tail_rem = 0; g.tail_s = 1; g.bm = BM; g.tail_partial = nullptr;
+  const Kind kd = choose_kind(M, N);
+  g.tiles_m = ceil_div(M, kd.bm);
+  g.tiles_n = ceil_div(N, kd.bn);
+  g.dp_blocks = 0; g.tail_rem = 0; g.tail_s = 1; g.bm = kd.bm; g.bn = kd.bn;
+  g.tail_partial = nullptr;
   const int64_t tiles = g.tiles_m * g.tiles_n * batch;
-  const int64_t slots = resident_blocks();
+  const int64_t slots = resident_blocks(kd);
   if (workspace && tag == 2) {   // explicit split-K into [M][N] slabs
     int sp = choose_splits(tiles, K, slots);
     while (sp > 1 && (size_t)sp * batch * M * N * sizeof(float) > workspace_bytes) --sp;
@@ -480,8 +364,8 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
     }
   } else if (workspace && batch == 1) {   // tail split of the last partial wave
     int64_t rem = 0;
-    int ts = choose_tail_split(tiles, K, slots, rem);
-    while (ts > 1 && (size_t)ts * rem * BM * BN * sizeof(float) > workspace_bytes) --ts;
+    int ts = choose_tail_split(tiles, K, slots, kd, rem);
+    while (ts > 1 && (size_t)ts * rem * kd.bm * kd.bn * sizeof(float) > workspace_bytes) --ts;
     if (ts > 1) {
       g.k_per_split = round_up(ceil_div(K, ts), KSTEP);
       g.tail_s = (int)ceil_div(K, g.k_per_split);
@@ -500,11 +384,16 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
   return launch_gemm<1>(g, a_kc, b_kc, batch, stream);
 }
 
+extern "C" void gatx_set_gemm_mode(int mode) { g_gemm_mode = mode ? 1 : 0; }
+
+extern "C" int gatx_get_gemm_mode(void) { return gemm_mode(); }
+
 extern "C" size_t gatx_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K) {
   int64_t rem = 0;
-  const int ts = choose_tail_split(ceil_div(M, BM) * ceil_div(N, BN), K,
-                                   resident_blocks(), rem);
-  return ts > 1 ? (size_t)ts * rem * 128 * 128 * sizeof(float) : 0;
+  const Kind kd = choose_kind(M, N);
+  const int ts = choose_tail_split(ceil_div(M, kd.bm) * ceil_div(N, kd.bn), K,
+                                   resident_blocks(kd), kd, rem);
+  return ts > 1 ? (size_t)ts * rem * kd.bm * kd.bn * sizeof(float) : 0;
 }
 
 extern "C" int gatx_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t sam,
@@ -540,15 +429,17 @@ extern "C" int gatx_gemm_f32_batched(int64_t batch, int64_t M, int64_t N, int64_
 }
 
 extern "C" size_t gatx_gemm_splitk_workspace_bytes(int64_t M, int64_t N, int64_t K) {
-  const int64_t tiles = ceil_div(M, 128) * ceil_div(N, 128);
-  const int sp = choose_splits(tiles, K, resident_blocks());
+  const Kind kd = choose_kind(M, N);
+  const int64_t tiles = ceil_div(M, kd.bm) * ceil_div(N, kd.bn);
+  const int sp = choose_splits(tiles, K, resident_blocks(kd));
   return sp > 1 ? (size_t)sp * M * N * sizeof(float) : 0;
 }
 
 extern "C" size_t gatx_gemm_splitk_batched_workspace_bytes(int64_t batch, int64_t M, int64_t N,
                                                            int64_t K) {
-  const int64_t tiles = ceil_div(M, 128) * ceil_div(N, 128) * batch;
-  const int sp = choose_splits(tiles, K, resident_blocks());
+  const Kind kd = choose_kind(M, N);
+  const int64_t tiles = ceil_div(M, kd.bm) * ceil_div(N, kd.bn) * batch;
+  const int sp = choose_splits(tiles, K, resident_blocks(kd));
   return sp > 1 ? (size_t)sp * batch * M * N * sizeof(float) : 0;
 }
 

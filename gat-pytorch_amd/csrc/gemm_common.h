@@ -1,0 +1,178 @@
+// Shared pieces of the two GEMM kernels (gemm.hip: f32 MFMA; gemm_x3.hip: split-bf16):
+// operand tile staging, launch arguments, tile order and the fused epilogue.
+#pragma once
+
+#include "gatx_common.h"
+
+namespace gatx {
+namespace gk {
+
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int BM = 128, BN = 128;
+constexpr int KSTEP = 32;   // split-K / tail slice granularity
+
+// One operand tile of ROWS rows x BK k. KC: k-contiguous in memory (row stride ld).
+template <bool KC, int ROWS, int BK, int NT>
+struct Tile {
+  static constexpr int LD = KC ? BK + 4 : ROWS + 4;
+  static constexpr int SIZE = KC ? ROWS * LD : BK * LD;   // floats per stage
+  static constexpr int NV = ROWS * BK / 4 / NT;           // float4 per thread
+  // VEC (16-byte aligned rows, ld % 4 == 0): every thread issues NV float4 loads from clamped
+  // in-bounds addresses and zeroes the components outside the matrix; otherwise scalar loads.
+  template <bool VEC>
+  static __device__ inline void load(const float* __restrict__ P, int64_t ld, int64_t r0,
+                                     int64_t rmax, int64_t k0, int64_t kmax, float4 (&v)[NV]) {
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      const int idx = threadIdx.x + NT * c;
+      int64_t r, k;
+      if (KC) { r = r0 + idx / (BK / 4); k = k0 + 4 * (idx % (BK / 4)); }
+      else { k = k0 + idx / (ROWS / 4); r = r0 + 4 * (idx % (ROWS / 4)); }
+      if (VEC) {
+        // KC: lanes j run along k (valid while k + j < kmax); RC: along rows
+        const bool rok = r < rmax, kok = k < kmax;
+        const int64_t rc = rok ? r : (KC ? rmax - 1 : 0);
+        const int64_t kc = kok ? k : (KC ? 0 : kmax - 1);
+        v[c] = *(const float4*)(KC ? P + rc * ld + kc : P + kc * ld + rc);   // masked in store
+      } else {
+        float e[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const bool ok = KC ? (r < rmax && k + j < kmax) : (k < kmax && r + j < rmax);
+          e[j] = ok ? (KC ? P[r * ld + k + j] : P[k * ld + r + j]) : 0.f;
+        }
+        v[c] = make_float4(e[0], e[1], e[2], e[3]);
+      }
+    }
+  }
+  // Components outside the matrix are zeroed here, after the MFMAs of the current tile, so the
+  // loads' latency stays hidden (a select right after the load would wait for it).
+  template <bool VEC>
+  static __device__ inline void store(float* img, float4 (&v)[NV], int64_t r0, int64_t rmax,
+                                      int64_t k0, int64_t kmax) {
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      const int idx = threadIdx.x + NT * c;
+      const int row = KC ? idx / (BK / 4) : 4 * (idx % (ROWS / 4));
+      const int kk = KC ? 4 * (idx % (BK / 4)) : idx / (ROWS / 4);
+      if (VEC) {
+        const int64_t r = r0 + row, k = k0 + kk;
+        const bool ok = r < rmax && k < kmax;
+        const int64_t lim = KC ? kmax - k : rmax - r;
+        v[c].x = ok ? v[c].x : 0.f;
+        v[c].y = ok && lim > 1 ? v[c].y : 0.f;
+        v[c].z = ok && lim > 2 ? v[c].z : 0.f;
+        v[c].w = ok && lim > 3 ? v[c].w : 0.f;
+      }
+      const int off = KC ? row * LD + kk : kk * LD + row;
+      *(float4*)&img[off] = v[c];
+    }
+  }
+  // k = kb .. kb+3 of row `row`
+  static __device__ inline float4 frag(const float* img, int row, int kb) {
+    if (KC) return *(const float4*)&img[row * LD + kb];
+    return make_float4(img[kb * LD + row], img[(kb + 1) * LD + row], img[(kb + 2) * LD + row],
+                       img[(kb + 3) * LD + row]);
+  }
+};
+
+struct GemmArgs {
+  int64_t M, N, K;
+  const float* A; int64_t lda, a_bs;
+  const float* B; int64_t ldb, b_bs;
+  float* C0; int64_t ldc0, c0_bs;
+  int64_t n_split;
+  float* C1; int64_t ldc1, c1_bs;
+  int accumulate, a_vec, b_vec;
+  int64_t tiles_m, tiles_n;
+  // epilogue on C0 columns: C = elu?(acc (+C) + bias[col] + resid[row][col])
+  const float* bias; int64_t bias_bs;
+  const float* resid; int64_t resid_ld, resid_bs;
+  int elu;
+  int64_t k_per_split; int splits; float* partial;
+  // tail split (splits == 1): blocks >= dp_blocks each take K-slice z of one of the last
+  // tail_rem tiles and write a BM x BN partial; tail_fixup_kernel sums the slices in z order
+  int64_t dp_blocks, tail_rem; int tail_s, bm, bn; float* tail_partial;
+};
+
+// C = elu?(v (+C) + bias + resid) for one output element (columns >= n_split go to C1 raw)
+__device__ inline void store_out(const GemmArgs& g, int64_t b, int64_t row, int64_t col, float v) {
+  float* Cb;
+  int64_t ldc, c;
+  const bool first = col < g.n_split;
+  if (first) { Cb = g.C0 + b * g.c0_bs; ldc = g.ldc0; c = col; }
+  else { Cb = g.C1 + b * g.c1_bs; ldc = g.ldc1; c = col - g.n_split; }
+  float* p = Cb + row * ldc + c;
+  if (g.accumulate) v += *p;
+  if (first) {
+    if (g.bias) v += g.bias[b * g.bias_bs + c];
+    if (g.resid) v += g.resid[b * g.resid_bs + row * g.resid_ld + c];
+    if (g.elu) v = v > 0.f ? v : expm1f(v);
+  }
+  *p = v;
+}
+
+// Workgroup -> output tile. Workgroups are dealt round-robin over the 8 XCDs (b % 8), so give
+// XCD x a contiguous run of m-major tiles: an A row-tile (x rows) is then fetched into one XCD's
+// L2 and reused there by all its n-tiles. Placement only changes speed, never results.
+__device__ inline void tile_of(int64_t b, int64_t T, int64_t tiles_n, int64_t& tm, int64_t& tn) {
+  const int64_t q = T / 8, r = T % 8;
+  const int64_t xcd = b % 8, j = b / 8;
+  const int64_t t = (xcd < r) ? xcd * (q + 1) + j : r * (q + 1) + (xcd - r) * q + j;
+  tm = t / tiles_n;
+  tn = t % tiles_n;
+}
+
+// Epilogue shared by both kernels. C/D map of a 32x32 f32 MFMA block: col = lane&31,
+// row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+template <int MB, int NB, int TBM = BM, int TBN = BN>
+__device__ inline void write_tile(const GemmArgs& g, floatx16 (&acc)[MB][NB], int tail_z,
+                                  int64_t tail_ti, int64_t m0, int64_t n0, int wm, int wn,
+                                  int lane) {
+  const int64_t M = g.M, N = g.N;
+  if (tail_z >= 0) {   // tail slice: tile-local partial, summed by tail_fixup_kernel
+    float* P = g.tail_partial + ((int64_t)tail_z * g.tail_rem + tail_ti) * (TBM * TBN);
+#pragma unroll
+    for (int mi = 0; mi < MB; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NB; ++ni)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rl = wm * (MB * 32) + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          P[rl * TBN + wn * (NB * 32) + ni * 32 + (lane & 31)] = acc[mi][ni][r];
+        }
+    return;
+  }
+#pragma unroll
+  for (int mi = 0; mi < MB; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NB; ++ni) {
+      const int64_t col = n0 + wn * (NB * 32) + ni * 32 + (lane & 31);
+      if (col >= N) continue;
+      if (g.splits > 1) {   // partial slab z: plain [M][N] store, reduced by splitk_reduce_kernel
+        float* P = g.partial + ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * M * N;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int64_t row = m0 + wm * (MB * 32) + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          if (row < M) P[row * N + col] = acc[mi][ni][r];
+        }
+        continue;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = m0 + wm * (MB * 32) + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (row < M) store_out(g, blockIdx.y, row, col, acc[mi][ni][r]);
+      }
+    }
+}
+
+}  // namespace gk
+
+// gemm_x3.hip: launch the split-bf16 kernel for GemmArgs prepared by gemm_impl (gemm.hip).
+int launch_gemm_x3(const gk::GemmArgs& g, bool a_kc, bool b_kc, int batch, int tag, hipStream_t stream);
+// the x3 kernel instance whose occupancy sizes tail / split-K decisions
+const void* gemm_x3_occupancy_fn(int cfg);   // cfg 0: 128 x 128 tiles, 1: 256 x 256
+
+}  // namespace gatx

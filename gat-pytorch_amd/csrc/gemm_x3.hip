@@ -1,0 +1,354 @@
+// fp32 GEMM as a three-way bf16 split on v_mfma_f32_32x32x16_bf16 (see the comment below).
+#include "gemm_common.h"
+
+namespace gatx {
+namespace {
+using namespace gk;
+
+// ---------------------------------------------------------------------------------------------
+// fp32 GEMM as a three-way bf16 split ("x3"): every fp32 operand element is written exactly as
+// x = h + m + l with h = bf16_rn(x), m = bf16_rn(x - h), l = x - h - m (exactly a bf16: 24 =
+// 8 + 8 + 8 significand bits), and the product as the six bf16 MFMA products whose magnitude
+// reaches fp32 resolution: a_h b_h + a_h b_m + a_m b_h + a_h b_l + a_l b_h + a_m b_m. The dropped
+// terms a_m b_l + a_l b_m + a_l b_l are below 2^-23 |a||b| — the size of one fp32 rounding — and
+// bf16 products are exact in the f32 accumulator, so the result has the fp32 GEMM's accuracy
+// (checked against fp64 beside the f32-MFMA kernel in tests/test_gpu_layer.py) at 6 x 32 cycles
+// per 32x32x16 step instead of 8 x 64 for v_mfma_f32_32x32x2_f32: 2.7x fewer MFMA cycles.
+//
+// Two tile configurations (XCD-contiguous tile order, tail split and fused epilogue shared with
+// gemm_f32_kernel): CFG 1 = 256 x 256 per 8-wave workgroup, 128 x 64 per wave (4 x 2 blocks of
+// v_mfma_f32_32x32x16_bf16), 96 KB of LDS, one workgroup per CU — the large products; CFG 0 =
+// 128 x 128 per 4-wave workgroup, 64 x 64 per wave, 48 KB, three per CU — small outputs.
+// Measured on the PPI projection shape (44900 x 1024 x 1024), 128 x 128 tiles reach 148 TF:
+// re-staging 6 bytes per element per 24 MFMAs keeps the LDS ~65% busy; 256 x 256 tiles halve
+// the staging per MFMA.
+// The fp32 tiles are split once per workgroup while they are staged into LDS (each element then
+// feeds several waves), into three bf16 planes per operand:
+//  * k-contiguous operand: [slot = k/8][row ^ (slot*64/BK)][8 k] — 16-byte fragment reads
+//    (ds_read_b128) and 8-byte staging stores, both conflict-free;
+//  * row-contiguous operand: [k][128 rows] with 256-byte rows whose 16-byte chunks are XOR'd by k
+//    — the fragment is read transposed by two ds_read_b64_tr_b16 (4 k each), conflict-free.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// Two floats -> packed bf16 pair, round to nearest even (v_cvt_pk_bf16_f32). The empty asm keeps
+// the compiler from re-deriving each half from its own single-value conversion.
+__device__ inline uint32_t cvt_pk_bf16(float a, float b) {
+  typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+  bf2 v = {(__bf16)a, (__bf16)b};
+  uint32_t u = __builtin_bit_cast(uint32_t, v);
+  asm("" : "+v"(u));
+  return u;
+}
+
+// (x, y) -> the three bf16 planes of both, packed as pairs (x in the low half).
+__device__ inline void split_pair(float x, float y, uint32_t& h, uint32_t& m, uint32_t& l) {
+  h = cvt_pk_bf16(x, y);
+  const float rx = x - __uint_as_float(h << 16), ry = y - __uint_as_float(h & 0xffff0000u);
+  m = cvt_pk_bf16(rx, ry);
+  l = cvt_pk_bf16(rx - __uint_as_float(m << 16), ry - __uint_as_float(m & 0xffff0000u));
+}
+
+// One bf16 plane image of a ROWS-row x BK-k operand tile (byte offsets).
+template <bool KC, int ROWS, int BK>
+struct PlaneImg {
+  static constexpr int BYTES = ROWS * BK * 2;
+  // offset of the 4 consecutive k (KC, k % 4 == 0) or 4 consecutive rows (RC, r % 4 == 0)
+  // starting at (r, k)
+  static __device__ inline int off(int r, int k) {
+    if (KC) {
+      const int s = k >> 3;
+      return s * (ROWS * 16) + ((r ^ (s * (64 / BK))) << 4) + ((k & 4) << 1);
+    }
+    const int c = (r >> 3) ^ (((k & 3) << 2) | ((k >> 2) & 3));
+    return k * (ROWS * 2) + (c << 4) + ((r & 7) << 1);
+  }
+};
+
+// Staging of one operand tile: NV float4 per thread, thread idx -> (row, k) as Tile<> maps it.
+template <bool KC, int ROWS, int BK, int NT, int DBG = 0>
+struct X3Tile {
+  using T = Tile<KC, ROWS, BK, NT>;
+  static constexpr int NV = T::NV;
+  using Img = PlaneImg<KC, ROWS, BK>;
+  static __device__ inline int row_of(int idx) { return KC ? idx / (BK / 4) : 4 * (idx % (ROWS / 4)); }
+  static __device__ inline int k_of(int idx) { return KC ? 4 * (idx % (BK / 4)) : idx / (ROWS / 4); }
+  // Fast path: per-thread pointers at K-tile 0 (rows past rmax clamped to a valid row: their
+  // products only reach output rows/columns that are never stored) and the per-tile step.
+  static __device__ inline void setup(const float* P, int64_t ld, int64_t r0, int64_t rmax,
+                                      int64_t k0, const float* (&p)[NV], int64_t& step) {
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      const int idx = threadIdx.x + NT * c;
+      int64_t r = r0 + row_of(idx);
+      if (r >= rmax) r = KC ? rmax - 1 : 0;
+      const int64_t k = k0 + k_of(idx);
+      p[c] = KC ? P + r * ld + k : P + k * ld + r;
+    }
+    step = KC ? BK : BK * ld;
+  }
+  // Split the staged float4s into the three planes at img. KTAIL: zero k >= kmax (the last,
+  // partial K-tile); MASK: also rows >= rmax (generic path, Tile::load's clamped addresses).
+  template <bool MASK, bool KTAIL>
+  static __device__ inline void store(char* img, float4 (&v)[NV], int64_t r0, int64_t rmax,
+                                      int64_t k0, int64_t kmax) {
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      const int idx = threadIdx.x + NT * c;
+      const int row = row_of(idx), kk = k_of(idx);
+      if (MASK || KTAIL) {
+        const int64_t r = r0 + row, k = k0 + kk;
+        const bool ok = (!MASK || r < rmax) && k < kmax;
+        const int64_t lim = (KC || !MASK) ? (KC ? kmax - k : 4) : rmax - r;
+        v[c].x = ok ? v[c].x : 0.f;
+        v[c].y = ok && lim > 1 ? v[c].y : 0.f;
+        v[c].z = ok && lim > 2 ? v[c].z : 0.f;
+        v[c].w = ok && lim > 3 ? v[c].w : 0.f;
+      }
+      uint32_t h0, m0, l0, h1, m1, l1;
+      if (DBG == 1) {   // tuning probe: conversion only (wrong values), measures the split's cost
+        h0 = m0 = l0 = cvt_pk_bf16(v[c].x, v[c].y);
+        h1 = m1 = l1 = cvt_pk_bf16(v[c].z, v[c].w);
+      } else {
+        split_pair(v[c].x, v[c].y, h0, m0, l0);
+        split_pair(v[c].z, v[c].w, h1, m1, l1);
+      }
+      const int o = Img::off(row, kk);
+      *(uint2*)(img + o) = make_uint2(h0, h1);
+      *(uint2*)(img + Img::BYTES + o) = make_uint2(m0, m1);
+      *(uint2*)(img + 2 * Img::BYTES + o) = make_uint2(l0, l1);
+    }
+  }
+  // MFMA 32x32x16 operand fragment of rows rb..rb+31, k = k16..k16+15 from one plane.
+  static __device__ inline bf16x8 frag(const char* plane, int rb, int k16, int lane) {
+    if (KC) {
+      return *(const bf16x8*)(plane + Img::off(rb + (lane & 31), k16 + 8 * (lane >> 5)));
+    } else {
+      const int g = lane >> 4, i = lane & 15;
+      const int r = rb + 16 * (g & 1) + 4 * (i & 3), k = k16 + 8 * (g >> 1) + (i >> 2);
+      const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_s16x4*)(__attribute__((address_space(3))) char*)(plane + Img::off(r, k)));
+      const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_s16x4*)(__attribute__((address_space(3))) char*)(plane + Img::off(r, k + 4)));
+      typedef short s16x8 __attribute__((ext_vector_type(8)));
+      const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      return __builtin_bit_cast(bf16x8, v);
+    }
+  }
+};
+
+// Tile configurations: CFG 0 = 128 x 128, 2 x 2 waves; CFG 1 = 256 x 256, 2 x 4 waves.
+template <int CFG>
+struct X3Cfg {
+  static constexpr int TBM = CFG ? 256 : 128, TBN = CFG ? 256 : 128;
+  static constexpr int WGM = 2, WGN = CFG ? 4 : 2;
+  static constexpr int NT = 64 * WGM * WGN;
+  static constexpr int MB = TBM / WGM / 32, NB = TBN / WGN / 32;
+  static constexpr int MINB = CFG ? 1 : 3;
+  static constexpr int BK = 16;
+};
+
+// Main loop over nk K-tiles starting at kb. MASK (unaligned operands): every tile through
+// Tile::load's clamped scalar/vector loads and full masking. Otherwise each thread streams its
+// float4s from fixed per-thread pointers; only a partial last K-tile is masked (k >= K zeroed).
+template <bool A_KC, bool B_KC, bool MASK, int CFG, int DBG>
+__device__ inline void x3_mainloop(const GemmArgs& g, const float* __restrict__ A,
+                                   const float* __restrict__ B, int64_t m0, int64_t n0,
+                                   int64_t kb, int64_t K, int64_t nk, char* smem, int wm, int wn,
+                                   int lane, floatx16 (&acc)[X3Cfg<CFG>::MB][X3Cfg<CFG>::NB]) {
+  using C = X3Cfg<CFG>;
+  constexpr int NT = C::NT, BK = C::BK, MB = C::MB, NB = C::NB;
+  using TA = X3Tile<A_KC, C::TBM, BK, NT, DBG>;
+  using TB = X3Tile<B_KC, C::TBN, BK, NT, DBG>;
+  constexpr int PA = TA::Img::BYTES, PBy = TB::Img::BYTES;   // bytes per plane
+  constexpr int STAGE = 3 * (PA + PBy);                      // A planes h, m, l then B's
+  const int64_t M = g.M, N = g.N;
+  const bool ktail = (K - kb) % BK != 0;
+  float4 va[TA::NV], vb[TB::NV];
+  const float* pa[TA::NV];
+  const float* pb[TB::NV];
+  int64_t sa = 0, sb = 0;
+  if (!MASK) {
+    TA::setup(A, g.lda, m0, M, kb, pa, sa);
+    TB::setup(B, g.ldb, n0, N, kb, pb, sb);
+  }
+  auto load = [&](int64_t k0) {
+    if (MASK) {
+      TA::T::template load<false>(A, g.lda, m0, M, k0, K, va);
+      TB::T::template load<false>(B, g.ldb, n0, N, k0, K, vb);
+    } else if (k0 + BK > K) {
+      // partial last K-tile: a k >= K reads k = kb instead (always inside the matrix) and is
+      // zeroed in store; k < K reads in place (KC: k % 4 == 0 and ld % 4 == 0 keep the float4
+      // inside the row's ld)
+#pragma unroll
+      for (int c = 0; c < TA::NV; ++c) {
+        const int64_t k = k0 + TA::k_of(threadIdx.x + NT * c);
+        va[c] = *(const float4*)(k < K ? pa[c] : pa[c] - (k - kb) * (A_KC ? 1 : g.lda));
+      }
+#pragma unroll
+      for (int c = 0; c < TB::NV; ++c) {
+        const int64_t k = k0 + TB::k_of(threadIdx.x + NT * c);
+        vb[c] = *(const float4*)(k < K ? pb[c] : pb[c] - (k - kb) * (B_KC ? 1 : g.ldb));
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < TA::NV; ++c) { va[c] = *(const float4*)pa[c]; pa[c] += sa; }
+#pragma unroll
+      for (int c = 0; c < TB::NV; ++c) { vb[c] = *(const float4*)pb[c]; pb[c] += sb; }
+    }
+  };
+  auto store = [&](char* st, int64_t k0) {
+    if (MASK) {
+      TA::template store<true, true>(st, va, m0, M, k0, K);
+      TB::template store<true, true>(st + 3 * PA, vb, n0, N, k0, K);
+    } else if (k0 + BK > K) {
+      TA::template store<false, true>(st, va, m0, M, k0, K);
+      TB::template store<false, true>(st + 3 * PA, vb, n0, N, k0, K);
+    } else {
+      TA::template store<false, false>(st, va, m0, M, k0, K);
+      TB::template store<false, false>(st + 3 * PA, vb, n0, N, k0, K);
+    }
+  };
+  (void)ktail;
+  load(kb);
+  store(smem, kb);
+  __syncthreads();
+  for (int64_t kt = 0; kt < nk; ++kt) {
+    char* cur = smem + (kt & 1) * STAGE;
+    char* nxt = smem + ((kt & 1) ^ 1) * STAGE;
+    const bool more = kt + 1 < nk;
+    if (more) load(kb + (kt + 1) * BK);
+    bf16x8 fa[MB][3], fb[NB][3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+#pragma unroll
+      for (int x = 0; x < MB; ++x) fa[x][p] = TA::frag(cur + p * PA, wm * (MB * 32) + x * 32, 0, lane);
+#pragma unroll
+      for (int x = 0; x < NB; ++x)
+        fb[x][p] = TB::frag(cur + 3 * PA + p * PBy, wn * (NB * 32) + x * 32, 0, lane);
+    }
+    // small terms first: (l,h) (h,l) (m,m) (m,h) (h,m) (h,h)
+    constexpr int PLA[6] = {2, 0, 1, 1, 0, 0};
+    constexpr int PLB[6] = {0, 2, 1, 0, 1, 0};
+#pragma unroll
+    for (int t = 0; t < 6; ++t)
+#pragma unroll
+      for (int mi = 0; mi < MB; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NB; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[mi][PLA[t]], fb[ni][PLB[t]],
+                                                                acc[mi][ni], 0, 0, 0);
+    if (more && DBG != 2) store(nxt, kb + (kt + 1) * BK);
+    __syncthreads();
+  }
+}
+
+template <bool A_KC, bool B_KC, bool VEC, int TAG, int CFG, int DBG = 0>
+__global__ void __launch_bounds__(X3Cfg<CFG>::NT, X3Cfg<CFG>::MINB) gemm_x3_kernel(GemmArgs g) {
+  using C = X3Cfg<CFG>;
+  constexpr int STAGE = 3 * 2 * (C::TBM + C::TBN) * C::BK;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+  const int64_t T = g.tiles_m * g.tiles_n;
+  int64_t tm, tn, kb, K;
+  int tail_z = -1;
+  int64_t tail_ti = 0;
+  if (g.tail_s > 1 && (int64_t)blockIdx.x >= g.dp_blocks) {
+    const int64_t j = blockIdx.x - g.dp_blocks;
+    tail_ti = j % g.tail_rem;
+    tail_z = (int)(j / g.tail_rem);
+    const int64_t lin = g.dp_blocks + tail_ti;
+    tm = lin / g.tiles_n;
+    tn = lin - tm * g.tiles_n;
+    kb = tail_z * g.k_per_split;
+    K = min(g.K, kb + g.k_per_split);
+  } else if (g.tail_s > 1) {
+    tile_of(blockIdx.x, g.dp_blocks, g.tiles_n, tm, tn);
+    kb = 0;
+    K = g.K;
+  } else {
+    tile_of(blockIdx.x, T, g.tiles_n, tm, tn);
+    kb = blockIdx.z * g.k_per_split;
+    K = min(g.K, kb + g.k_per_split);
+  }
+  const int64_t m0 = tm * C::TBM, n0 = tn * C::TBN;
+  const float* __restrict__ A = g.A + blockIdx.y * g.a_bs;
+  const float* __restrict__ B = g.B + blockIdx.y * g.b_bs;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave / C::WGN, wn = wave % C::WGN;
+
+  floatx16 acc[C::MB][C::NB];
+#pragma unroll
+  for (int i = 0; i < C::MB; ++i)
+#pragma unroll
+    for (int j = 0; j < C::NB; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int64_t nk = K > kb ? ceil_div(K - kb, C::BK) : 0;
+  if (nk > 0) {
+    if (VEC)
+      x3_mainloop<A_KC, B_KC, false, CFG, DBG>(g, A, B, m0, n0, kb, K, nk, smem, wm, wn, lane, acc);
+    else
+      x3_mainloop<A_KC, B_KC, true, CFG, DBG>(g, A, B, m0, n0, kb, K, nk, smem, wm, wn, lane, acc);
+  }
+  write_tile<C::MB, C::NB, C::TBM, C::TBN>(g, acc, tail_z, tail_ti, m0, n0, wm, wn, lane);
+}
+
+}  // namespace
+
+int launch_gemm_x3(const gk::GemmArgs& g, bool a_kc, bool b_kc, int batch, int tag,
+                   hipStream_t stream) {
+  const int64_t tiles = g.tiles_m * g.tiles_n;
+  const int64_t gx = g.tail_s > 1 ? g.dp_blocks + g.tail_rem * g.tail_s : tiles;
+  dim3 grid((unsigned)gx, (unsigned)batch, (unsigned)g.splits);
+  const int cfg = g.bm == 256 ? 1 : 0;
+  static const int dbg = [] {   // tuning probes only (wrong results): GATX_X3_DBG=1|2
+    const char* e = getenv("GATX_X3_DBG");
+    return e ? atoi(e) : 0;
+  }();
+  if (dbg && a_kc && b_kc && g.a_vec && g.b_vec) {
+    if (cfg == 1) {
+      if (dbg == 1) gemm_x3_kernel<true, true, true, 0, 1, 1><<<grid, 512, 0, stream>>>(g);
+      else gemm_x3_kernel<true, true, true, 0, 1, 2><<<grid, 512, 0, stream>>>(g);
+    } else {
+      if (dbg == 1) gemm_x3_kernel<true, true, true, 0, 0, 1><<<grid, 256, 0, stream>>>(g);
+      else gemm_x3_kernel<true, true, true, 0, 0, 2><<<grid, 256, 0, stream>>>(g);
+    }
+    GATX_LAUNCH_CHECK("gemm_x3 (probe)");
+    return 0;
+  }
+#define GATX_X3_V(AK, BKC, V, TG)                                                             \
+  do {                                                                                        \
+    if (cfg == 1) gemm_x3_kernel<AK, BKC, V, TG, 1><<<grid, 512, 0, stream>>>(g);             \
+    else gemm_x3_kernel<AK, BKC, V, TG, 0><<<grid, 256, 0, stream>>>(g);                      \
+  } while (0)
+#define GATX_X3_T(AK, BKC, V)                                                                 \
+  do {                                                                                        \
+    if (tag == 0) GATX_X3_V(AK, BKC, V, 0);                                                   \
+    else if (tag == 2) GATX_X3_V(AK, BKC, V, 2);                                              \
+    else GATX_X3_V(AK, BKC, V, 1);                                                            \
+  } while (0)
+#define GATX_X3_GO(AK, BKC)                                                                   \
+  do {                                                                                        \
+    if (g.a_vec && g.b_vec) GATX_X3_T(AK, BKC, true);                                         \
+    else GATX_X3_T(AK, BKC, false);                                                           \
+  } while (0)
+  if (a_kc && b_kc) GATX_X3_GO(true, true);
+  else if (a_kc) GATX_X3_GO(true, false);
+  else if (b_kc) GATX_X3_GO(false, true);
+  else GATX_X3_GO(false, false);
+#undef GATX_X3_GO
+#undef GATX_X3_T
+#undef GATX_X3_V
+  GATX_LAUNCH_CHECK("gemm_x3");
+  return 0;
+}
+
+const void* gemm_x3_occupancy_fn(int cfg) {
+  return cfg ? reinterpret_cast<const void*>(&gemm_x3_kernel<true, true, true, 0, 1>)
+             : reinterpret_cast<const void*>(&gemm_x3_kernel<true, true, true, 0, 0>);
+}
+
+}  // namespace gatx

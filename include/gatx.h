@@ -90,6 +90,12 @@ int gatx_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t sam, 
                   const float* B, int64_t sbk, int64_t sbn, float* C0, int64_t ldc0,
                   int64_t n_split, float* C1, int64_t ldc1, int accumulate, void* workspace,
                   size_t workspace_bytes, gatx_stream_t stream);
+/* Arithmetic of every gatx GEMM (process-wide; env GATX_GEMM=f32|x3 sets the initial value):
+ * 1 = "x3" (default): each fp32 operand split exactly into three bf16 planes, the six partial
+ *     products above fp32 resolution on v_mfma_f32_32x32x16_bf16 with f32 accumulation — fp32
+ *     GEMM accuracy at 2.7x fewer MFMA cycles; 0 = "f32": v_mfma_f32_32x32x2_f32. */
+void gatx_set_gemm_mode(int mode);
+int gatx_get_gemm_mode(void);
 /* Workspace that lets gatx_gemm_f32 / gatx_projection_gemm split the K range of the tiles in
  * their last, partially filled wave (0 = no split for this shape; NULL workspace = never split).
  * The slices are summed in a fixed order by a fix-up kernel, so results stay deterministic. */

@@ -143,6 +143,83 @@ def test_gemm_mfma_layout(device):
 
 
 @pytest.mark.gpu
+def test_gemm_x3_split_accuracy(device):
+    """The split-bf16 GEMM ("x3": 3 bf16 planes per operand, 6 MFMA products) against float64,
+    beside the f32-MFMA kernel on the same data: error relative to sum|a||b| must stay at the
+    fp32 GEMM's level (<= 1.25x f32's, and < 1e-6 absolute-relative) for every operand layout,
+    128- and 256-wide tiles (kind chosen by size), partial K-tiles, ragged edges, unaligned
+    leading dimensions and split-K; repeated launches are bitwise identical."""
+    from gatx._lib import call, lib, ptr, stream
+    torch.manual_seed(11)
+    cases = [(600, 520, 1100), (300, 257, 33), (1000, 760, 70), (2000, 1024, 1100),
+             (513, 300, 4096), (129, 129, 17), (44, 1030, 70)]
+    try:
+        for (M, N, K) in cases:
+            A = torch.randn(M, K, device=device) * torch.rand(M, 1, device=device) * 30
+            B = torch.randn(K, N, device=device)
+            ref = A.double() @ B.double()
+            S = (A.double().abs() @ B.double().abs()).clamp_min(1e-30)
+            for a_t in (False, True):
+                for b_t in (False, True):
+                    Am = A.t().contiguous() if a_t else A
+                    Bm = B.t().contiguous() if b_t else B
+                    sam, sak = (1, M) if a_t else (K, 1)
+                    sbk, sbn = (1, K) if b_t else (N, 1)
+                    rel = {}
+                    for mode in (0, 1):
+                        lib.gatx_set_gemm_mode(mode)
+                        outs = []
+                        for _ in range(2):
+                            C = torch.full((M, N), float("nan"), device=device)
+                            call("gatx_gemm_f32", M, N, K, ptr(Am), sam, sak, ptr(Bm), sbk, sbn,
+                                 ptr(C), N, N, None, 0, 0, None, 0, stream())
+                            outs.append(C)
+                        torch.cuda.synchronize()
+                        assert torch.equal(outs[0], outs[1]), (M, N, K, a_t, b_t, mode)
+                        rel[mode] = ((outs[0].double() - ref).abs() / S).max().item()
+                    assert rel[1] <= max(1.25 * rel[0], 2e-7) and rel[1] < 1e-6, \
+                        (M, N, K, a_t, b_t, rel)
+        # unaligned leading dimensions (scalar staging path) and split-K through x3
+        lib.gatx_set_gemm_mode(1)
+        M, N, K = 301, 263, 1433
+        A = torch.randn(M, K, device=device)
+        B = torch.randn(N, K, device=device)
+        C = torch.empty(M, N, device=device)
+        call("gatx_gemm_f32", M, N, K, ptr(A), K, 1, ptr(B), 1, K, ptr(C), N, N, None, 0, 0,
+             None, 0, stream())
+        ref = A.double() @ B.double().t()
+        S = A.double().abs() @ B.double().abs().t()
+        torch.cuda.synchronize()
+        assert ((C.double() - ref).abs() / S).max().item() < 1e-6
+        M, N, K = 1032, 1024, 44900
+        A = torch.randn(K, M, device=device)
+        B = torch.randn(K, N, device=device)
+        wsb = lib.gatx_gemm_splitk_workspace_bytes(M, N, K)
+        ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=device)
+        C = torch.empty(M, N, device=device)
+        call("gatx_gemm_f32_splitk", M, N, K, ptr(A), 1, M, ptr(B), N, 1, ptr(C), N, 0, ptr(ws),
+             wsb, stream())
+        ref = A.double().t() @ B.double()
+        S = A.double().abs().t() @ B.double().abs()
+        torch.cuda.synchronize()
+        assert ((C.double() - ref).abs() / S).max().item() < 1e-6
+    finally:
+        lib.gatx_set_gemm_mode(1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["cora_l0_trained", "ppi_small_l1"])
+def test_layer_goldens_f32_gemm(name, device):
+    """The f32-MFMA GEMM kernels (GATX_GEMM=f32) stay parity-green on the reference goldens."""
+    from gatx._lib import lib
+    lib.gatx_set_gemm_mode(0)
+    try:
+        test_layer_matches_reference_goldens(name, device)
+    finally:
+        lib.gatx_set_gemm_mode(1)
+
+
+@pytest.mark.gpu
 def test_gemm_tail_split(device):
     """Shapes whose last wave of tiles is split along K (fix-up kernel sums the slices):
     same result as the unsplit GEMM to fp32 rounding, bitwise run to run, split output kept."""
