@@ -35,6 +35,24 @@ import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 FP32_MFMA_PEAK_TFS = 157.3   # v_mfma_f32_32x32x2_f32 dense peak (same table)
+BF16_MFMA_PEAK_TFS = 2500.0  # dense bf16 MFMA peak (same table; no sparsity)
+X3_PRODUCTS = 6              # bf16 MFMA products per fp32 multiply-add in the x3 split GEMM
+
+
+def gemm_roof():
+    """Peak and kernel name of the projection GEMM in the library's active arithmetic mode.
+
+    "f32": v_mfma_f32_32x32x2_f32, priced at the fp32 MFMA peak. "x3" (default): each fp32
+    operand is split into three bf16 planes and every fp32 multiply-add costs six bf16 MFMA
+    products (csrc/gemm_x3.hip), so the ceiling for fp32 flops is the dense bf16 peak / 6.
+    """
+    from gatx import _lib
+    if _lib.lib.gatx_get_gemm_mode() == 1:
+        return dict(mode="x3", peak=BF16_MFMA_PEAK_TFS / X3_PRODUCTS, prefix="gemm_x3_kernel<true, true, true, 0,",
+                    kernel="gemm_x3_kernel (fp32 as 3 bf16 planes x 6 MFMA products; peak = "
+                           "dense bf16 2500 TF / 6)")
+    return dict(mode="f32", peak=FP32_MFMA_PEAK_TFS, prefix="gemm_f32_kernel<true, true, true, 0,",
+                kernel="gemm_f32_kernel (v_mfma_f32_32x32x2_f32)")
 
 
 def layer_dims(cfg):
@@ -195,10 +213,12 @@ def run_rmat(args, world, rank, dev):
         fl = 2.0 * N * FIN * NH * F
         ms_ = sum(t for _, t in gem) / len(gem)
         tfs = fl / (ms_ * 1e-3) / 1e12
-        roofs.append({"bound": "mfma", "kernel": "gemm_f32_kernel (projection x.W^T)",
-                      "achieved": round(tfs, 2), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                      "frac": round(tfs / FP32_MFMA_PEAK_TFS, 4), "traffic": None,
-                      "flops_per_launch": fl, "avg_launch_ms": ms_, "_ms": ms_})
+        gr = gemm_roof()
+        roofs.append({"bound": "mfma", "kernel": gr["kernel"] + ", projection x.W^T",
+                      "achieved": round(tfs, 2), "peak": round(gr["peak"], 1), "unit": "TFLOP/s",
+                      "frac": round(tfs / gr["peak"], 4), "traffic": None,
+                      "gemm_mode": gr["mode"], "flops_per_launch": fl, "avg_launch_ms": ms_,
+                      "_ms": ms_})
     roofs.sort(key=lambda r: -r["_ms"])
     for r in roofs:
         r.pop("_ms")
@@ -216,7 +236,7 @@ def run_rmat(args, world, rank, dev):
         "achieved_GBps_algorithmic_per_gpu": round((alg["b_gemm"] + alg["b_edge"])
                                                    / (elapsed / args.steps) / 1e9, 1),
         "roofline_time_frac": round(max((alg["b_gemm"] + alg["b_edge"]) / (HBM_PEAK_GBS * 1e9),
-                                        alg["f_gemm"] / (FP32_MFMA_PEAK_TFS * 1e12))
+                                        alg["f_gemm"] / (gemm_roof()["peak"] * 1e12))
                                     / (ms * 1e-3), 4),
         "roofline": roofs[0] if roofs else None,
         "roofline_other": roofs[1] if len(roofs) > 1 else None,
@@ -372,12 +392,12 @@ def main():
         fl = sum(2.0 * n * fin * nh * f + 4.0 * n * nh * nh * f for (n, _, fin, nh, f), _ in gem)
         ms_ = sum(t for _, t in gem)
         tfs = fl / (ms_ * 1e-3) / 1e12
-        roofs["gemm"] = {"bound": "mfma", "kernel": "gemm_f32_kernel<true, true, true, 0, 16, 4> "
-                         "(projection x.W_aug^T, layers 1-2)", "achieved": round(tfs, 2),
-                         "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                         "frac": round(tfs / FP32_MFMA_PEAK_TFS, 4), "traffic": None,
-                         "flops_per_launch": fl / len(gem), "avg_launch_ms": ms_ / len(gem),
-                         "_prefix": "gemm_f32_kernel<true, true, true, 0,", "_ms": ms_}
+        gr = gemm_roof()
+        roofs["gemm"] = {"bound": "mfma", "kernel": gr["kernel"] + ", projection x.W_aug^T",
+                         "achieved": round(tfs, 2), "peak": round(gr["peak"], 1),
+                         "unit": "TFLOP/s", "frac": round(tfs / gr["peak"], 4), "traffic": None,
+                         "gemm_mode": gr["mode"], "flops_per_launch": fl / len(gem),
+                         "avg_launch_ms": ms_ / len(gem), "_prefix": gr["prefix"], "_ms": ms_}
     edg = summ.get("edge_forward", [])
     if edg:
         by = 0.0
@@ -428,7 +448,7 @@ def main():
                    "parallelism": f"graph-batch dp{world}"},
         "achieved_GBps_algorithmic_per_gpu": round(bytes_step / (elapsed / args.steps) / 1e9, 1),
         "roofline_time_frac": round(sum(max((a["b_gemm"] + a["b_edge"]) / (HBM_PEAK_GBS * 1e9),
-                                            a["f_gemm"] / (FP32_MFMA_PEAK_TFS * 1e12))
+                                            a["f_gemm"] / (gemm_roof()["peak"] * 1e12))
                                         for a in alg) / (ms * 1e-3), 4),
         "roofline": dominant,
         "roofline_other": other,
