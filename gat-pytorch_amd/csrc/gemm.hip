@@ -347,6 +347,16 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
   };
   g.a_vec = aligned(A, g.lda, a_bs);
   g.b_vec = aligned(B, g.ldb, b_bs);
+  static const bool smallk_on = [] {   // A/B switch: GATX_SMALLK=0 keeps the tiled kernel
+    const char* e = getenv("GATX_SMALLK");
+    return !(e && strcmp(e, "0") == 0);
+  }();
+  if (smallk_on && gemm_mode() == 1 && n_split >= N &&
+      gemm_smallk_fits(M, N, K, a_kc, b_kc, accumulate, resid != nullptr)) {
+    g.splits = 1; g.tail_s = 1; g.tiles_m = g.tiles_n = 1; g.dp_blocks = g.tail_rem = 0;
+    g.bm = g.bn = 32; g.tail_partial = nullptr;
+    return launch_gemm_smallk(g, batch, stream);
+  }
   const Kind kd = choose_kind(M, N);
   g.tiles_m = ceil_div(M, kd.bm);
   g.tiles_n = ceil_div(N, kd.bn);

@@ -114,6 +114,42 @@ __device__ inline void store_out(const GemmArgs& g, int64_t b, int64_t row, int6
   *p = v;
 }
 
+// One finished 32 x 32 MFMA block through the epilogue of store_out: this lane's column `col`
+// and rows row0 + (r & 3) + 8 (r >> 2) (row0 includes the lane half's 4 (lane >> 5)). Column
+// terms are resolved once per block instead of per element (the per-element 64-bit index
+// arithmetic of store_out cost the projection GEMMs ~3% of their time), and the column's bias
+// comes in from the caller, loaded before any store: on gfx9 loads and stores share the vmcnt
+// counter, so a load issued after a block's stores waits for all of them to reach memory
+// (the accumulate / residual loads still do; no forward projection uses them).
+__device__ inline float block_bias(const GemmArgs& g, int64_t b, int64_t col) {
+  return (g.bias && col < g.N && col < g.n_split) ? g.bias[b * g.bias_bs + col] : 0.f;
+}
+__device__ inline void store_block(const GemmArgs& g, int64_t b, int64_t row0, int64_t col,
+                                   const floatx16& acc, float bias) {
+  if (col >= g.N) return;
+  const bool first = col < g.n_split;
+  float* base;
+  int64_t ldc;
+  if (first) { base = g.C0 + b * g.c0_bs + col; ldc = g.ldc0; }
+  else { base = g.C1 + b * g.c1_bs + (col - g.n_split); ldc = g.ldc1; }
+  const bool has_bias = first && g.bias != nullptr;
+  const float* rp = (first && g.resid) ? g.resid + b * g.resid_bs + col : nullptr;
+  const bool elu = first && g.elu;
+  const bool full = row0 + 27 < g.M;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int64_t row = row0 + (r & 3) + 8 * (r >> 2);
+    if (!full && row >= g.M) continue;
+    float* p = base + row * ldc;
+    float v = acc[r];
+    if (g.accumulate) v += *p;   // the order of store_out: ((acc + C) + bias) + resid
+    if (has_bias) v += bias;
+    if (rp) v += rp[row * g.resid_ld];
+    if (elu) v = v > 0.f ? v : expm1f(v);
+    *p = v;
+  }
+}
+
 // Workgroup -> output tile. Workgroups are dealt round-robin over the 8 XCDs (b % 8), so give
 // XCD x a contiguous run of m-major tiles: an A row-tile (x rows) is then fetched into one XCD's
 // L2 and reused there by all its n-tiles. Placement only changes speed, never results.
@@ -145,6 +181,10 @@ __device__ inline void write_tile(const GemmArgs& g, floatx16 (&acc)[MB][NB], in
         }
     return;
   }
+  float bias[NB];   // loaded before the first store (see store_block)
+#pragma unroll
+  for (int ni = 0; ni < NB; ++ni)
+    bias[ni] = g.splits > 1 ? 0.f : block_bias(g, blockIdx.y, n0 + wn * (NB * 32) + ni * 32 + (lane & 31));
 #pragma unroll
   for (int mi = 0; mi < MB; ++mi)
 #pragma unroll
@@ -160,11 +200,8 @@ __device__ inline void write_tile(const GemmArgs& g, floatx16 (&acc)[MB][NB], in
         }
         continue;
       }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t row = m0 + wm * (MB * 32) + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (row < M) store_out(g, blockIdx.y, row, col, acc[mi][ni][r]);
-      }
+      store_block(g, blockIdx.y, m0 + wm * (MB * 32) + mi * 32 + 4 * (lane >> 5), col,
+                  acc[mi][ni], bias[ni]);
     }
 }
 
@@ -172,6 +209,10 @@ __device__ inline void write_tile(const GemmArgs& g, floatx16 (&acc)[MB][NB], in
 
 // gemm_x3.hip: launch the split-bf16 kernel for GemmArgs prepared by gemm_impl (gemm.hip).
 int launch_gemm_x3(const gk::GemmArgs& g, bool a_kc, bool b_kc, int batch, int tag, hipStream_t stream);
+// gemm_smallk.hip: K <= 64, N <= 256 products with the fused epilogue (x3 arithmetic)
+bool gemm_smallk_fits(int64_t M, int64_t N, int64_t K, bool a_kc, bool b_kc, int accumulate,
+                      bool resid);
+int launch_gemm_smallk(const gk::GemmArgs& g, int batch, hipStream_t stream);
 // the x3 kernel instance whose occupancy sizes tail / split-K decisions
 const void* gemm_x3_occupancy_fn(int cfg);   // cfg 0: 128 x 128 tiles, 1: 256 x 256
 

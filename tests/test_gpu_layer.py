@@ -220,6 +220,49 @@ def test_layer_goldens_f32_gemm(name, device):
 
 
 @pytest.mark.gpu
+def test_gemm_smallk(device):
+    """The small-K path (K <= 64, N <= 256: csrc/gemm_smallk.hip, B split once into LDS) against
+    float64 and beside the tiled kernel (GATX_SMALLK is read once, so the tiled result comes from
+    the f32 kernel): fused bias / residual / ELU epilogue, batched with strided heads, ragged M,
+    N and K, unaligned lda (scalar loads); error relative to sum|a||b| at the fp32 GEMM's level;
+    bitwise repeatable."""
+    from gatx._lib import call, lib, ptr, stream
+    torch.manual_seed(5)
+    cases = [(44900 // 8, 4, 256, 50, 52), (1000, 1, 7, 1, 4), (777, 3, 33, 17, 17),
+             (300, 2, 256, 64, 64), (4096, 1, 8, 50, 50), (513, 5, 130, 3, 4)]
+    try:
+        for (M, NB, N, K, ldk) in cases:
+            Z = torch.randn(M, NB * ldk, device=device) * torch.rand(M, 1, device=device) * 10
+            W = torch.randn(NB * N, ldk, device=device)
+            bias = torch.randn(NB * N, device=device)
+            resid = torch.randn(M, NB * N, device=device)
+            Zv = Z.view(M, NB, ldk)[:, :, :K].double()
+            Wv = W.view(NB, N, ldk)[:, :, :K].double()
+            prod = torch.einsum("mbk,bnk->mbn", Zv, Wv).reshape(M, NB * N)
+            S = torch.einsum("mbk,bnk->mbn", Zv.abs(), Wv.abs()).reshape(M, NB * N)
+            for elu in (0, 1):
+                for use_resid in (False, True):
+                    pre = prod + bias.double() + (resid.double() if use_resid else 0)
+                    ref = torch.where(pre > 0, pre, torch.expm1(pre)) if elu else pre
+                    outs = []
+                    for mode in (1, 1, 0):
+                        lib.gatx_set_gemm_mode(mode)
+                        C = torch.full((M, NB * N), float("nan"), device=device)
+                        call("gatx_gemm_f32_batched", NB, M, N, K, ptr(Z), NB * ldk, 1, ldk,
+                             ptr(W), 1, ldk, N * ldk, ptr(C), NB * N, N, 0, ptr(bias), N,
+                             ptr(resid) if use_resid else None, NB * N, N, elu, stream())
+                        outs.append(C)
+                    torch.cuda.synchronize()
+                    assert torch.equal(outs[0], outs[1]), (M, NB, N, K)
+                    rel = ((outs[0].double() - ref).abs() / (S + 1.0)).max().item()
+                    rel_f32 = ((outs[2].double() - ref).abs() / (S + 1.0)).max().item()
+                    assert rel <= max(1.5 * rel_f32, 3e-7) and rel < 1e-6, (M, NB, N, K, elu, rel,
+                                                                           rel_f32)
+    finally:
+        lib.gatx_set_gemm_mode(1)
+
+
+@pytest.mark.gpu
 def test_gemm_tail_split(device):
     """Shapes whose last wave of tiles is split along K (fix-up kernel sums the slices):
     same result as the unsplit GEMM to fp32 rounding, bitwise run to run, split output kept."""
