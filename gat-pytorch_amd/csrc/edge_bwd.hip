@@ -73,6 +73,42 @@ __global__ void __launch_bounds__(256) prepare_go_kernel(const float* __restrict
   }
 }
 
+// The same for F % 4 == 0 (Fp == F: go has g_out's layout): float4 streams, 4 per thread per
+// round with all loads issued before any store (loads and stores share vmcnt). g_pre == go is
+// allowed (the caller then reads the residual gradient from go).
+__global__ void __launch_bounds__(256) prepare_go_vec_kernel(const float4* __restrict__ g_out,
+                                                             const float4* __restrict__ out,
+                                                             int64_t n4, int elu, float scale,
+                                                             float4* go, float4* g_pre) {
+  constexpr int U = 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t0 < n4; t0 += U * stride) {
+    float4 v[U], o[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t t = t0 + u * stride;
+      if (t < n4) {
+        v[u] = g_out[t];
+        if (elu) o[u] = out[t];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t t = t0 + u * stride;
+      if (t >= n4) continue;
+      float4 w = v[u];
+      if (elu) {   // d elu(x) = elu(x) + 1 for x <= 0
+        w.x = o[u].x > 0.f ? w.x : w.x * (o[u].x + 1.f);
+        w.y = o[u].y > 0.f ? w.y : w.y * (o[u].y + 1.f);
+        w.z = o[u].z > 0.f ? w.z : w.z * (o[u].z + 1.f);
+        w.w = o[u].w > 0.f ? w.w : w.w * (o[u].w + 1.f);
+      }
+      if (g_pre && g_pre != go) g_pre[t] = w;
+      go[t] = make_float4(w.x * scale, w.y * scale, w.z * scale, w.w * scale);
+    }
+  }
+}
+
 struct BwdArgs {
   const float* Wh;      // [N][Dp]
   const float* go;      // prepared upstream gradient rows
@@ -141,8 +177,11 @@ __global__ void __launch_bounds__(256) edge_bwd_dst_kernel(BwdArgs g) {
   float* dot_lds = dot_sh[wave];
 
   const int beg = uni(g.rowptr[n]), end = uni(g.rowptr[n + 1]);
-  // sweep 1: g_alpha per edge (stored), c = sum g_alpha * alpha
-  float c_acc = 0.f;
+  // sweep 1: g_alpha per edge, c = sum g_alpha * alpha. The first 64 edges' g_alpha and exp
+  // stay in registers for sweep 2 (at PPI that is every edge of nearly every node); later
+  // batches go through g_raw. Besides the reload, a store ahead of sweep 2's loads would make
+  // them wait for it to reach memory (loads and stores share vmcnt).
+  float c_acc = 0.f, ga0 = 0.f, ex0 = 0.f;
   for (int base = beg; base < end; base += 64) {
     const int cnt = min(64, end - base);
     const bool valid = lane < cnt;
@@ -188,7 +227,12 @@ __global__ void __launch_bounds__(256) edge_bwd_dst_kernel(BwdArgs g) {
       float ga = my_dot;
       if (drop) ga = dropout_keep(g.seed, (int64_t)g.perm[e] * NH + h, g.p_drop) ? ga * drop_scale : 0.f;
       if (g.g_alpha_ret) ga += g.g_alpha_ret[(int64_t)g.perm[e] * NH + h];
-      graw[e] = ga;
+      if (base == beg) {
+        ga0 = ga;
+        ex0 = ex;
+      } else {
+        graw[e] = ga;
+      }
       c_acc += ga * ex * dinv;
     }
   }
@@ -198,8 +242,9 @@ __global__ void __launch_bounds__(256) edge_bwd_dst_kernel(BwdArgs g) {
   for (int base = beg; base < end; base += 64) {
     const int e = base + lane;
     if (e < end) {
-      const float ex = att_exp(g.S[(int64_t)g.col[e] * S2 + h] + sdst, M);
-      const float gr = kLeakySlope * ex * (graw[e] - cc) * dinv;
+      const bool first = base == beg;
+      const float ex = first ? ex0 : att_exp(g.S[(int64_t)g.col[e] * S2 + h] + sdst, M);
+      const float gr = kLeakySlope * ex * ((first ? ga0 : graw[e]) - cc) * dinv;
       graw[e] = gr;
       gsum += gr;
     }
@@ -555,6 +600,18 @@ extern "C" int gatx_prepare_go(const float* g_out, const float* out, int64_t N, 
   const int Fp = (int)round_up(F, 4);
   const int64_t GW = concat ? (int64_t)NH * Fp : Fp;
   GATX_REQUIRE(!elu || out, "prepare_go: elu needs the forward output");
+  GATX_REQUIRE(g_pre != go || (concat && F % 4 == 0),
+               "prepare_go: g_pre may alias go only for concat layers with F % 4 == 0");
+  const bool aligned = ((uintptr_t)g_out % 16 == 0) && ((uintptr_t)go % 16 == 0) &&
+                       (!elu || (uintptr_t)out % 16 == 0) && ((uintptr_t)g_pre % 16 == 0);
+  if (F % 4 == 0 && aligned) {
+    const int64_t n4 = N * GW / 4;
+    prepare_go_vec_kernel<<<grid_for(ceil_div(n4, 4), 256, 8192), 256, 0, (hipStream_t)s>>>(
+        (const float4*)g_out, (const float4*)out, n4, elu, concat ? 1.f : 1.f / (float)NH,
+        (float4*)go, (float4*)g_pre);
+    GATX_LAUNCH_CHECK("prepare_go");
+    return 0;
+  }
   prepare_go_kernel<<<grid_for(N * GW), 256, 0, (hipStream_t)s>>>(g_out, out, N, NH, F, Fp,
                                                                   concat, elu, go, g_pre);
   GATX_LAUNCH_CHECK("prepare_go");

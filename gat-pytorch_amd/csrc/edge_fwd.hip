@@ -273,8 +273,8 @@ __global__ void __launch_bounds__(256) edge_forward_kernel(EdgeFwdArgs g) {
 #pragma unroll
     for (int h = 0; h < kMaxHS; ++h)
       if (h == lane) d = dnl[h];
-    den_lds[lane] = d;
-    g.den[n * NH + h0 + lane] = d;
+    den_lds[lane] = d;   // to memory at the very end: a store ahead of the epilogue's bias /
+                         // residual loads would make them wait for it (shared vmcnt)
   }
   // combine the EPW edge groups (butterfly: every group ends with the totals)
 #pragma unroll
@@ -329,6 +329,7 @@ __global__ void __launch_bounds__(256) edge_forward_kernel(EdgeFwdArgs g) {
       g.out[n * g.out_ld + f] = epilogue(sum * inv_nh + (g.bias ? g.bias[f] : 0.f), g, n, f);
     }
   }
+  if (lane < HS) g.den[n * NH + h0 + lane] = den_lds[lane];
 }
 
 // ------------------------------------------------------------------ weights

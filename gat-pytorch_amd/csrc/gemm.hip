@@ -310,10 +310,42 @@ int choose_tail_split(int64_t tiles, int64_t K, int64_t slots, const Kind& kd, i
 }
 
 
+// dst[c][r] = src[r][c] through a 64 x 65 LDS tile (coalesced on both sides).
+__global__ void __launch_bounds__(256) transpose_kernel(const float* __restrict__ src,
+                                                        int64_t rows, int64_t cols, int64_t lds_,
+                                                        float* __restrict__ dst, int64_t ldd) {
+  __shared__ float t[64][65];
+  const int64_t r0 = blockIdx.y * 64ll, c0 = blockIdx.x * 64ll;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = ty; i < 64; i += 4) {
+    const int64_t r = r0 + i, c = c0 + tx;
+    t[i][tx] = (r < rows && c < cols) ? src[r * lds_ + c] : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = ty; i < 64; i += 4) {
+    const int64_t c = c0 + i, r = r0 + tx;
+    if (c < cols && r < rows) dst[c * ldd + r] = t[tx][i];
+  }
+}
+
 }  // namespace
 }  // namespace gatx
 
 using namespace gatx;
+
+extern "C" int gatx_transpose_f32(int64_t rows, int64_t cols, const float* src, int64_t ld_src,
+                                  float* dst, int64_t ld_dst, gatx_stream_t s) {
+  GATX_REQUIRE(rows >= 0 && cols >= 0 && ld_src >= cols && ld_dst >= rows,
+               "transpose: bad shape");
+  if (rows == 0 || cols == 0) return 0;
+  GATX_REQUIRE(ceil_div(rows, 64) < 65536, "transpose: too many rows");
+  dim3 grid((unsigned)ceil_div(cols, 64), (unsigned)ceil_div(rows, 64));
+  transpose_kernel<<<grid, 256, 0, (hipStream_t)s>>>(src, rows, cols, ld_src, dst, ld_dst);
+  GATX_LAUNCH_CHECK("transpose");
+  return 0;
+}
 
 static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A, int64_t sam,
                      int64_t sak, int64_t a_bs, const float* B, int64_t sbk, int64_t sbn,

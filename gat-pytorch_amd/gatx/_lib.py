@@ -40,6 +40,7 @@ SIGNATURES = {
     "gatx_gemm_f32": (c_i, [c_i64, c_i64, c_i64, P, c_i64, c_i64, P, c_i64, c_i64, P, c_i64,
                             c_i64, P, c_i64, c_i, P, c_sz, P]),
     "gatx_gemm_workspace_bytes": (c_sz, [c_i64, c_i64, c_i64]),
+    "gatx_transpose_f32": (c_i, [c_i64, c_i64, P, c_i64, P, c_i64, P]),
     "gatx_gemm_f32_batched": (c_i, [c_i64, c_i64, c_i64, c_i64, P, c_i64, c_i64, c_i64, P,
                                     c_i64, c_i64, c_i64, P, c_i64, c_i64, c_i, P, c_i64, P, c_i64,
                                     c_i64, c_i, P]),

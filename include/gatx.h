@@ -90,6 +90,10 @@ int gatx_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t sam, 
                   const float* B, int64_t sbk, int64_t sbn, float* C0, int64_t ldc0,
                   int64_t n_split, float* C1, int64_t ldc1, int accumulate, void* workspace,
                   size_t workspace_bytes, gatx_stream_t stream);
+/* dst[c * ld_dst + r] = src[r * ld_src + c] for r < rows, c < cols (the backward's k-contiguous
+ * copy of W_aug, so g_x = G_aug W_aug runs with both operands k-contiguous). */
+int gatx_transpose_f32(int64_t rows, int64_t cols, const float* src, int64_t ld_src, float* dst,
+                       int64_t ld_dst, gatx_stream_t stream);
 /* Arithmetic of every gatx GEMM (process-wide; env GATX_GEMM=f32|x3 sets the initial value):
  * 1 = "x3" (default): each fp32 operand split exactly into three bf16 planes, the six partial
  *     products above fp32 resolution on v_mfma_f32_32x32x16_bf16 with f32 accumulation — fp32
