@@ -14,7 +14,8 @@ backward and an RCCL gradient all-reduce, DDP-style).
 
 value = (sum over ranks of 3 layers x E' edges per step) / step time (max over ranks).
 roofline = the dominant kernel's algorithmic bytes (or flops) per launch / its average launch time,
-measured with HIP events on the launch stream during the timed steps. cpu_baseline = the numpy
+measured with HIP events on the launch stream over the same number of steps run right after the
+timed region (event records cost ~10 us each, so the timed region itself carries none). cpu_baseline = the numpy
 oracle (oracle/gat_oracle.py, the reference's dataflow restated) on a bounded sample, rank 0, N=1.
 """
 from __future__ import annotations
@@ -53,6 +54,41 @@ def gemm_roof():
                            "dense bf16 2500 TF / 6)")
     return dict(mode="f32", peak=FP32_MFMA_PEAK_TFS, prefix="gemm_f32_kernel<true, true, true, 0,",
                 kernel="gemm_f32_kernel (v_mfma_f32_32x32x2_f32)")
+
+
+def run_timed(step, steps, world, dev):
+    """The timed region: barrier + synchronize on both sides, max over ranks. No HIP events
+    inside it: each timed event record costs the stream ~10 us (measured in rocprof traces:
+    14-16 extra inter-kernel gaps per PPI step when every launch was bracketed)."""
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
+def run_instrumented(step, steps):
+    """The same number of steps again, right after the timed region, with every gatx launch
+    bracketed by HIP events on its stream: per-kernel durations for `kernels` / `roofline`."""
+    from gatx.functional import KernelTimer, set_kernel_timer
+    timer = KernelTimer()
+    set_kernel_timer(timer)
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    set_kernel_timer(None)
+    return timer.summary()
 
 
 def layer_dims(cfg):
@@ -152,7 +188,6 @@ def run_rmat(args, world, rank, dev):
     no sharding: with --gpus N each rank runs an independent replica (value sums them)."""
     from gatx import GATLayer, clear_graph_cache
     from gatx import data as gd
-    from gatx.functional import KernelTimer, set_kernel_timer
     NH, F, FIN = 8, 64, 512
     N, E = args.rmat_nodes, args.rmat_edges
     torch.manual_seed(0)
@@ -172,27 +207,10 @@ def run_rmat(args, world, rank, dev):
     torch.cuda.synchronize()
     from gatx.graph import graph_cache
     E2 = graph_cache.get(ei, N, True).num_edges
-    timer = KernelTimer()
-    set_kernel_timer(timer)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    set_kernel_timer(None)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64,
-                         device=dev if dist.get_backend() == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = run_timed(step, args.steps, world, dev)
+    summ = run_instrumented(step, args.steps)
     ms = elapsed / args.steps * 1e3
     alg = algorithmic(N, E2, FIN, NH, F, True)
-    summ = timer.summary()
     kern = {}
     for phase, recs in summ.items():
         tot = sum(t for _, t in recs)
@@ -293,7 +311,6 @@ def main():
     from gatx import data as gd
     from gatx.config import data_config
     from gatx.distributed import allreduce_gradients
-    from gatx.functional import KernelTimer, set_kernel_timer
 
     ds = "PATTERN" if args.workload == "pattern" else "PPI"
     if args.graphs is None:
@@ -354,24 +371,8 @@ def main():
     N = b.num_nodes
     dims = layer_dims(cfg)
 
-    timer = KernelTimer()
-    set_kernel_timer(timer)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    set_kernel_timer(None)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64,
-                         device=dev if dist.get_backend() == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = run_timed(step, args.steps, world, dev)
+    summ = run_instrumented(step, args.steps)
     ms = elapsed / args.steps * 1e3
 
     layer_edges = len(dims) * E2
@@ -379,8 +380,7 @@ def main():
     bytes_step = sum(a["b_gemm"] + a["b_edge"] for a in alg)
     value = layer_edges * world / (elapsed / args.steps)
 
-    # live per-kernel timing (HIP events on the launch stream) over the timed steps
-    summ = timer.summary()
+    # per-kernel timing: HIP events on the launch stream over the instrumented steps
     kern = {}
     for phase, recs in summ.items():
         tot = sum(t for _, t in recs)
