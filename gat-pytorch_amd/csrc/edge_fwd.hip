@@ -101,7 +101,7 @@ __device__ inline int64_t xcd_contiguous(int64_t b, int64_t nb) {
 
 __device__ inline float epilogue(float v, const EdgeFwdArgs& g, int64_t n, int64_t col) {
   if (g.resid) v += g.resid[n * g.resid_ld + col];
-  if (g.elu) v = v > 0.f ? v : expm1f(v);
+  if (g.elu) v = elu_act(v);
   return v;
 }
 
@@ -302,10 +302,10 @@ __global__ void __launch_bounds__(256) edge_forward_kernel(EdgeFwdArgs g) {
             r.x += rv[0]; r.y += rv[1]; r.z += rv[2]; r.w += rv[3];
           }
           if (g.elu) {
-            r.x = r.x > 0.f ? r.x : expm1f(r.x);
-            r.y = r.y > 0.f ? r.y : expm1f(r.y);
-            r.z = r.z > 0.f ? r.z : expm1f(r.z);
-            r.w = r.w > 0.f ? r.w : expm1f(r.w);
+            r.x = elu_act(r.x);
+            r.y = elu_act(r.y);
+            r.z = elu_act(r.z);
+            r.w = elu_act(r.w);
           }
           const f4v ov = {r.x, r.y, r.z, r.w};
           __builtin_nontemporal_store(ov, (f4v*)(orow + cb));

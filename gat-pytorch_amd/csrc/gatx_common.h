@@ -68,6 +68,17 @@ __device__ inline bool dropout_keep(uint64_t seed, int64_t idx, float p) {
 // exp of the reference's shifted, LeakyReLU'd logit: 0.01 * (raw - M) (raw - M <= 0 always).
 __device__ inline float att_exp(float raw, float M) { return __expf(kLeakySlope * (raw - M)); }
 
+// ELU (GATModel's activation, nn.ELU(alpha=1)) for the fused epilogues: v > 0 ? v : expm1(v),
+// with expm1 as a degree-5 Taylor polynomial above -1/16 (relative error < 1e-8) and
+// exp2(v log2 e) - 1 below (v_exp_f32; the result is then >= 0.06 in magnitude, error ~1e-7).
+// About ten VALU operations per element against ocml's expm1f, which made the ELU epilogue of
+// the first layer's output projection VALU-bound (46 M elements per PPI step).
+__device__ inline float elu_act(float v) {
+  const float p = v * (1.f + v * (0.5f + v * (1.f / 6.f + v * (1.f / 24.f + v * (1.f / 120.f)))));
+  const float e = __builtin_amdgcn_exp2f(v * 1.44269504088896341f) - 1.f;
+  return v > 0.f ? v : (v > -0.0625f ? p : e);
+}
+
 __device__ inline float4 operator*(float4 a, float s) {
   return make_float4(a.x * s, a.y * s, a.z * s, a.w * s);
 }

@@ -109,7 +109,7 @@ __device__ inline void store_out(const GemmArgs& g, int64_t b, int64_t row, int6
   if (first) {
     if (g.bias) v += g.bias[b * g.bias_bs + c];
     if (g.resid) v += g.resid[b * g.resid_bs + row * g.resid_ld + c];
-    if (g.elu) v = v > 0.f ? v : expm1f(v);
+    if (g.elu) v = elu_act(v);
   }
   *p = v;
 }
@@ -145,7 +145,7 @@ __device__ inline void store_block(const GemmArgs& g, int64_t b, int64_t row0, i
     if (g.accumulate) v += *p;   // the order of store_out: ((acc + C) + bias) + resid
     if (has_bias) v += bias;
     if (rp) v += rp[row * g.resid_ld];
-    if (elu) v = v > 0.f ? v : expm1f(v);
+    if (elu) v = elu_act(v);
     *p = v;
   }
 }

@@ -163,7 +163,7 @@ __global__ void __launch_bounds__(64 * SK_WAVES, 1) gemm_smallk_kernel(GemmArgs 
           const int64_t row = row0 + (r & 3) + 8 * (r >> 2);
           if (!full && row >= M) continue;
           float v = acc[i][r] + bv;
-          if (g.elu) v = v > 0.f ? v : expm1f(v);
+          if (g.elu) v = elu_act(v);
           base[row * g.ldc0] = v;
         }
       }
