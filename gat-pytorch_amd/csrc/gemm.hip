@@ -162,7 +162,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN, MINB) gemm_f32_kernel(GemmArgs
     __syncthreads();
   }
 
-  write_tile<MB, NB>(g, acc, tail_z, tail_ti, m0, n0, wm, wn, lane);
+  write_tile<MB, NB, BM, BN, false>(g, acc, tail_z, tail_ti, m0, n0, wm, wn, lane);
 }
 
 // GEMM arithmetic, env GATX_GEMM (or gatx_set_gemm_mode): "x3" (default) = the split-bf16

@@ -119,11 +119,12 @@ __device__ inline void store_out(const GemmArgs& g, int64_t b, int64_t row, int6
 // terms are resolved once per block instead of per element (the per-element 64-bit index
 // arithmetic of store_out cost the projection GEMMs ~3% of their time), and the column's bias
 // comes in from the caller, loaded before any store: on gfx9 loads and stores share the vmcnt
-// counter, so a load issued after a block's stores waits for all of them to reach memory
-// (the accumulate / residual loads still do; no forward projection uses them).
+// counter, so a load issued after a block's stores waits for all of them to reach memory.
 __device__ inline float block_bias(const GemmArgs& g, int64_t b, int64_t col) {
   return (g.bias && col < g.N && col < g.n_split) ? g.bias[b * g.bias_bs + col] : 0.f;
 }
+// PRE = false keeps the per-element form (no extra registers: the f32 kernel's 128-VGPR cap).
+template <bool PRE = true>
 __device__ inline void store_block(const GemmArgs& g, int64_t b, int64_t row0, int64_t col,
                                    const floatx16& acc, float bias) {
   if (col >= g.N) return;
@@ -136,17 +137,47 @@ __device__ inline void store_block(const GemmArgs& g, int64_t b, int64_t row0, i
   const float* rp = (first && g.resid) ? g.resid + b * g.resid_bs + col : nullptr;
   const bool elu = first && g.elu;
   const bool full = row0 + 27 < g.M;
+  if (!PRE || (!g.accumulate && !rp)) {
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int64_t row = row0 + (r & 3) + 8 * (r >> 2);
-    if (!full && row >= g.M) continue;
-    float* p = base + row * ldc;
-    float v = acc[r];
-    if (g.accumulate) v += *p;   // the order of store_out: ((acc + C) + bias) + resid
-    if (has_bias) v += bias;
-    if (rp) v += rp[row * g.resid_ld];
-    if (elu) v = elu_act(v);
-    *p = v;
+    for (int r = 0; r < 16; ++r) {
+      const int64_t row = row0 + (r & 3) + 8 * (r >> 2);
+      if (!full && row >= g.M) continue;
+      float* p = base + row * ldc;
+      float v = acc[r];
+      if (!PRE && g.accumulate) v += *p;
+      if (has_bias) v += bias;
+      if (!PRE && rp) v += rp[row * g.resid_ld];
+      if (elu) v = elu_act(v);
+      *p = v;
+    }
+    return;
+  }
+  // accumulate / residual: each half-block's 8 loads are issued before its 8 stores, so a load
+  // waits on at most one half-block of stores (per element it waited on every earlier store;
+  // that doubled the PPI L1 g_x GEMM, whose epilogue accumulates the identity-skip gradient)
+#pragma unroll
+  for (int hb = 0; hb < 2; ++hb) {
+    float cv[8], rv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = hb * 8 + i;
+      const int64_t row = row0 + (r & 3) + 8 * (r >> 2);
+      const bool ok = full || row < g.M;
+      cv[i] = (g.accumulate && ok) ? base[row * ldc] : 0.f;
+      rv[i] = (rp && ok) ? rp[row * g.resid_ld] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = hb * 8 + i;
+      const int64_t row = row0 + (r & 3) + 8 * (r >> 2);
+      if (!full && row >= g.M) continue;
+      float v = acc[r];
+      if (g.accumulate) v += cv[i];   // the order of store_out: ((acc + C) + bias) + resid
+      if (has_bias) v += bias;
+      if (rp) v += rv[i];
+      if (elu) v = elu_act(v);
+      base[row * ldc] = v;
+    }
   }
 }
 
@@ -163,7 +194,7 @@ __device__ inline void tile_of(int64_t b, int64_t T, int64_t tiles_n, int64_t& t
 
 // Epilogue shared by both kernels. C/D map of a 32x32 f32 MFMA block: col = lane&31,
 // row = (r&3) + 8*(r>>2) + 4*(lane>>5).
-template <int MB, int NB, int TBM = BM, int TBN = BN>
+template <int MB, int NB, int TBM = BM, int TBN = BN, bool PRE = true>
 __device__ inline void write_tile(const GemmArgs& g, floatx16 (&acc)[MB][NB], int tail_z,
                                   int64_t tail_ti, int64_t m0, int64_t n0, int wm, int wn,
                                   int lane) {
@@ -200,7 +231,7 @@ __device__ inline void write_tile(const GemmArgs& g, floatx16 (&acc)[MB][NB], in
         }
         continue;
       }
-      store_block(g, blockIdx.y, m0 + wm * (MB * 32) + mi * 32 + 4 * (lane >> 5), col,
+      store_block<PRE>(g, blockIdx.y, m0 + wm * (MB * 32) + mi * 32 + 4 * (lane >> 5), col,
                   acc[mi][ni], bias[ni]);
     }
 }
