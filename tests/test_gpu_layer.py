@@ -292,30 +292,48 @@ def test_gemm_tail_split(device):
             assert (outs[0] - outs[2]).abs().max().item() < 2e-4 * K ** 0.5
 
 
-def test_graph_build_matches_oracle(device):
+@pytest.mark.parametrize("variant", ["counting", "hubs", "no_rewrite", "degree_64"])
+def test_graph_build_matches_oracle(variant, device):
+    """edge_index' and both CSRs against the oracle's rewrite and numpy stable sorts: random
+    graphs with self-loops, duplicates and isolated nodes, hub nodes of degree 300 (one wave per
+    segment must loop over many 64-edge batches), with and without the self-loop rewrite."""
     gatx = _gatx()
     from gatx import data as gd
     b = gd.uniform_graph_batch(3, 500, 4000, 4)
+    N = b.num_nodes + 7                 # trailing isolated nodes too
     ei = b.edge_index.copy()
     ei[:, :50] = ei[0, :50]            # some self-loops
     ei = np.concatenate([ei, ei[:, :100]], 1)   # duplicates
+    if variant == "hubs":              # in-degree of node 3 and out-degree of node 5 > 64
+        r = np.arange(10, 310)
+        ei = np.concatenate([ei, np.stack([r, np.full_like(r, 3)]),
+                             np.stack([np.full_like(r, 5), r])], 1)
+    if variant == "degree_64":         # top node 1400 up to exactly 64 in edge_index'
+        have = np.bincount(orc.add_remaining_self_loops(ei)[1], minlength=N)[1400]
+        r = np.arange(600, 600 + 64 - have)
+        ei = np.concatenate([ei, np.stack([r, np.full_like(r, 1400)])], 1)
+    rewrite = variant != "no_rewrite"
     t = torch.from_numpy(ei).to(device)
-    g = gatx.Graph(t, b.num_nodes + 7, True)   # trailing isolated nodes too
-    ref = orc.add_remaining_self_loops(ei)
+    g = gatx.Graph(t, N, rewrite)
+    ref = orc.add_remaining_self_loops(ei) if rewrite else ei
+    dst = ref[1]
+    counts = np.bincount(dst, minlength=N)
+    assert (counts.max() > 64) == (variant == "hubs")
+    if variant == "degree_64":
+        assert counts.max() == 64
     np.testing.assert_array_equal(g.edge_index.cpu().numpy(), ref)
     rowptr, col, perm = (v.numpy() for v in g.csr_host())
-    dst = ref[1]
     order = np.argsort(dst, kind="stable")
     np.testing.assert_array_equal(perm, order)
     np.testing.assert_array_equal(col, ref[0][order])
-    counts = np.bincount(dst, minlength=b.num_nodes + 7)
+    np.testing.assert_array_equal(g.rowidx[:g.num_edges].cpu().numpy(), dst[order])
     np.testing.assert_array_equal(np.diff(rowptr), counts)
     g.ensure_transpose()
     srow = g.srowptr.cpu().numpy()
     scol = g.scol[:g.num_edges].cpu().numpy()
     seid = g.seid[:g.num_edges].cpu().numpy()
-    np.testing.assert_array_equal(np.diff(srow), np.bincount(ref[0], minlength=b.num_nodes + 7))
-    np.testing.assert_array_equal(col[seid], np.sort(ref[0], kind="stable"))
+    np.testing.assert_array_equal(np.diff(srow), np.bincount(ref[0], minlength=N))
+    np.testing.assert_array_equal(seid, np.argsort(col, kind="stable"))
     np.testing.assert_array_equal(scol, dst[order][seid])
 
 
