@@ -588,6 +588,57 @@ __global__ void __launch_bounds__(256) attention_alpha_kernel(
   }
 }
 
+// The same in edge_index' order: thread p reads edge p's (src, dst) from edge_index' itself
+// (coalesced) and writes alpha[p] (coalesced): the CSR-order kernel above scatters its writes
+// through perm (each 4*NH-byte row a separate partial granule). Tied argmax entries are
+// recorded by CSR slot as above, found by a scan of dst's segment (ties are rare).
+template <int NHC, typename I>
+__global__ void __launch_bounds__(256) attention_alpha_ei_kernel(
+    const I* __restrict__ ei, int64_t ld, int64_t E2, const float* __restrict__ S,
+    const uint32_t* __restrict__ M_ord, const float* __restrict__ den, int NH_rt, int const_att,
+    const int32_t* __restrict__ rowptr, const int32_t* __restrict__ perm,
+    float* __restrict__ alpha, long long* __restrict__ argmax) {
+  constexpr int VEC = (NHC % 4 == 0) ? 4 : ((NHC % 2 == 0) ? 2 : 1);
+  const int NH = NHC > 0 ? NHC : NH_rt, S2 = 2 * NH;
+  const float M = const_att ? 0.f : ord_to_float(*M_ord);
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < E2;
+       p += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = (int64_t)ei[p], d = (int64_t)ei[ld + p];
+    float* out = alpha + p * NH;
+    bool hit = false;
+    if constexpr (NHC > 0) {
+      float a[NHC];
+#pragma unroll
+      for (int h = 0; h < NHC; ++h) {
+        const float raw = S[s * S2 + h] + S[d * S2 + NHC + h];
+        hit |= (!const_att && raw == M);
+        a[h] = (const_att ? 1.f : att_exp(raw, M)) / (den[d * NHC + h] + kSoftmaxEps);
+      }
+#pragma unroll
+      for (int h = 0; h < NHC; h += VEC) {
+        if constexpr (VEC == 4) *(float4*)(out + h) = make_float4(a[h], a[h + 1], a[h + 2], a[h + 3]);
+        else if constexpr (VEC == 2) *(float2*)(out + h) = make_float2(a[h], a[h + 1]);
+        else out[h] = a[h];
+      }
+    } else {
+      for (int h = 0; h < NH; ++h) {
+        const float raw = S[s * S2 + h] + S[d * S2 + NH + h];
+        hit |= (!const_att && raw == M);
+        out[h] = (const_att ? 1.f : att_exp(raw, M)) / (den[d * NH + h] + kSoftmaxEps);
+      }
+    }
+    if (hit) {   // rare: record every tied argmax (CSR slot, head) for max()'s gradient
+      int64_t e = rowptr[d];
+      while (perm[e] != (int32_t)p) ++e;
+      for (int h = 0; h < NH; ++h)
+        if (S[s * S2 + h] + S[d * S2 + NH + h] == M) {
+          unsigned long long k = atomicAdd((unsigned long long*)argmax, 1ull);
+          if (k < GATX_ARGMAX_CAP) argmax[1 + k] = (long long)e * NH + h;
+        }
+    }
+  }
+}
+
 inline unsigned grid_for(int64_t n, int block = 256, int64_t cap = 16384) {
   int64_t g = ceil_div(n > 0 ? n : 1, block);
   return (unsigned)(g < cap ? g : cap);
@@ -690,6 +741,30 @@ extern "C" int gatx_attention_alpha(const int32_t* col, const int32_t* rowidx,
   }
 #undef GATX_AL
   GATX_LAUNCH_CHECK("attention_alpha");
+  return 0;
+}
+
+extern "C" int gatx_attention_alpha_ei(const void* edge_index, int is64, int64_t ld, int64_t E2,
+                                       const float* S, const uint32_t* M_ord, const float* den,
+                                       int NH, int const_att, const int32_t* rowptr,
+                                       const int32_t* perm, float* alpha, int64_t* argmax,
+                                       gatx_stream_t s) {
+  if (E2 == 0) return 0;
+  hipStream_t st = (hipStream_t)s;
+  const unsigned grid = grid_for(E2, 256, 8192);
+#define GATX_AE(C, I)                                                                          \
+  attention_alpha_ei_kernel<C, I><<<grid, 256, 0, st>>>((const I*)edge_index, ld, E2, S, M_ord, \
+                                                        den, NH, const_att, rowptr, perm, alpha, \
+                                                        (long long*)argmax)
+#define GATX_AEI(I)                                                                            \
+  switch (NH) {                                                                                \
+    case 1: GATX_AE(1, I); break; case 2: GATX_AE(2, I); break; case 4: GATX_AE(4, I); break;  \
+    case 6: GATX_AE(6, I); break; case 8: GATX_AE(8, I); break; default: GATX_AE(0, I); break; \
+  }
+  if (is64) { GATX_AEI(int64_t) } else { GATX_AEI(int32_t) }
+#undef GATX_AEI
+#undef GATX_AE
+  GATX_LAUNCH_CHECK("attention_alpha_ei");
   return 0;
 }
 

@@ -61,6 +61,7 @@ SIGNATURES = {
     "gatx_edge_forward": (c_i, [P, P, P, P, P, P, P, c_i64, c_i64, c_i, c_i, c_i, c_i, P, c_f,
                                 c_u64, P, P, P, P, P]),
     "gatx_attention_alpha": (c_i, [P, P, P, c_i64, P, P, P, c_i, c_i, P, P, P]),
+    "gatx_attention_alpha_ei": (c_i, [P, c_i, c_i64, c_i64, P, P, P, c_i, c_i, P, P, P, P, P]),
     "gatx_prepare_go": (c_i, [P, P, c_i64, c_i, c_i, c_i, c_i, P, P, P]),
     "gatx_edge_backward_dst": (c_i, [P, P, P, P, P, P, P, c_i64, c_i64, c_i, c_i, c_i, c_f, c_u64,
                                      P, P, P, P, P, c_i64, P]),

@@ -163,6 +163,22 @@ def augmented_weight(W, a, sh: "LayerShape"):
     return W_aug
 
 
+def _attention_alpha(graph: Graph, S, M_ord, den, sh: "LayerShape", alpha, argmax, s):
+    """alpha in edge_index' order (models/gat_layer.py:106-110): iterates edge_index' itself, so
+    both its reads and the alpha writes are coalesced (GATX_ALPHA_CSR=1: the CSR-order kernel,
+    whose writes scatter through perm)."""
+    import os
+    ei = graph.edge_index
+    if os.environ.get("GATX_ALPHA_CSR") == "1":
+        call("gatx_attention_alpha", ptr(graph.col), ptr(graph.rowidx), ptr(graph.perm),
+             graph.num_edges, ptr(S), ptr(M_ord), ptr(den), sh.NH, int(sh.const), ptr(alpha),
+             ptr(argmax), s)
+        return
+    call("gatx_attention_alpha_ei", ptr(ei), int(ei.dtype == torch.int64), ei.stride(0),
+         graph.num_edges, ptr(S), ptr(M_ord), ptr(den), sh.NH, int(sh.const), ptr(graph.rowptr),
+         ptr(graph.perm), ptr(alpha), ptr(argmax), s)
+
+
 def _env_int(name: str, default: int) -> int:
     import os
     v = os.environ.get(name)
@@ -248,8 +264,7 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
                  int(sh.const), None, float(p), seed, ptr(Z), sh.NH * Fin_p, None, 0, 0,
                  ptr(den), chunk, s)
         with _span("attention_alpha", (E2, sh.NH)):
-            call("gatx_attention_alpha", ptr(graph.col), ptr(graph.rowidx), ptr(graph.perm), E2,
-                 ptr(S), ptr(M_ord), ptr(den), sh.NH, int(sh.const), ptr(alpha), ptr(argmax), s)
+            _attention_alpha(graph, S, M_ord, den, sh, alpha, argmax, s)
         Wp = padded_weight(W, Fin_p)   # float4-readable rows
         with _span("gemm_out", (N, sh.F, sh.F_in, sh.NH)):
             call("gatx_gemm_f32_batched", sh.NH, N, sh.F, sh.F_in, ptr(Z), sh.NH * Fin_p, 1,
@@ -281,8 +296,7 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
              edge_heads_per_item(sh), int(sh.concat), int(sh.const), ptr(bias), float(p), seed,
              ptr(out), sh.out_cols, resid_p, sh.out_cols, int(elu), ptr(den), chunk, s)
     with _span("attention_alpha", (E2, sh.NH)):
-        call("gatx_attention_alpha", ptr(graph.col), ptr(graph.rowidx), ptr(graph.perm), E2,
-             ptr(S), ptr(M_ord), ptr(den), sh.NH, int(sh.const), ptr(alpha), ptr(argmax), s)
+        _attention_alpha(graph, S, M_ord, den, sh, alpha, argmax, s)
     saved.update(Wh=Wh, S=S, reassoc=False)
     return out, alpha, saved
 

@@ -191,6 +191,13 @@ int gatx_attention_alpha(const int32_t* col, const int32_t* rowidx, const int32_
                          int64_t E2, const float* S, const uint32_t* M_ord, const float* den,
                          int NH, int const_attention, float* alpha, int64_t* argmax,
                          gatx_stream_t stream);
+/* gatx_attention_alpha iterating edge_index' itself (int64 or int32, row stride ld): reads each
+ * edge's (src, dst) and writes alpha[p] in order (coalesced both ways); rowptr / perm (the CSR)
+ * are only read to record a tied argmax by CSR slot, as gatx_attention_alpha does. */
+int gatx_attention_alpha_ei(const void* edge_index, int index_is_int64, int64_t ld, int64_t E2,
+                            const float* S, const uint32_t* M_ord, const float* den, int NH,
+                            int const_att, const int32_t* rowptr, const int32_t* perm,
+                            float* alpha, int64_t* argmax, gatx_stream_t stream);
 
 /* S [N][2NH] = (Wh . A_src^T | Wh . A_dst^T) from Wh [N][Dp] and a.weight — the reference's own
  * association of the logit GEMV (gat_layer.py:76-82), used when folding the scores into the
