@@ -237,7 +237,8 @@ int launch_gemm(const GemmArgs& g0, bool a_kc, bool b_kc, int batch, hipStream_t
 
 // Kernel kind for an M x N output: 0 = f32 MFMA (128 x 128 tiles); 1 = x3, 128 x 128 tiles;
 // 2 = x3, 256 x 256 tiles (one 8-wave workgroup per CU: half the LDS staging per MFMA) when the
-// output is large and the bigger tiles cover it with at most 5% more padding.
+// output is large and the bigger tiles cover it with at most 15% more padding (PPI L1's 1032 x 1024
+// weight gradient: 11% more padding, still faster than 128 x 128 tiles; train step -0.03 ms).
 struct Kind {
   int id, bm, bn;
 };
@@ -250,7 +251,11 @@ Kind choose_kind(int64_t M, int64_t N) {
   if (force == 128) return {1, 128, 128};
   const int64_t small_area = round_up(M, 128) * round_up(N, 128);
   const int64_t big_area = round_up(M, 256) * round_up(N, 256);
-  if (force == 256 || (M >= 256 && N >= 256 && big_area * 100 <= small_area * 105))
+  static const int tol = [] {   // tuning only: GATX_X3_BIGTOL=percent padding accepted
+    const char* e = getenv("GATX_X3_BIGTOL");
+    return e ? atoi(e) : 115;
+  }();
+  if (force == 256 || (M >= 256 && N >= 256 && big_area * 100 <= small_area * tol))
     return {2, 256, 256};
   return {1, 128, 128};
 }
