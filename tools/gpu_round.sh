@@ -14,7 +14,7 @@ step tests timeout -k 10 600 python -m pytest "$R/tests" -m gpu -x -q -p no:cach
 tail -2 "$OUT/gpu_tests.log"
 step bench timeout -k 10 300 python "$R/bench.py" > "$OUT/bench.json" 2> "$OUT/bench.err"
 step bench_train timeout -k 10 300 python "$R/bench.py" --mode train --no-cpu-baseline > "$OUT/bench_train.json" 2> "$OUT/bench_train.err"
-step bench_rmat timeout -k 10 400 python "$R/bench.py" --workload rmat --steps 5 --warmup 1 > "$OUT/bench_rmat.json" 2> "$OUT/bench_rmat.err"
+step bench_rmat timeout -k 10 400 python "$R/bench.py" --workload rmat --steps 5 --warmup 2 > "$OUT/bench_rmat.json" 2> "$OUT/bench_rmat.err"
 cd /tmp && export TMPDIR=/tmp
 step prof_fwd timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_fwd" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/prof_fwd.log" 2>&1
 step prof_train timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_train" -o run --output-format csv -- python3 "$R/bench.py" --mode train --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/prof_train.log" 2>&1
