@@ -231,6 +231,17 @@ def run_rmat(args, world, rank, dev):
                       "frac": round(tfs / gr["peak"], 4), "traffic": None,
                       "gemm_mode": gr["mode"], "flops_per_launch": fl, "avg_launch_ms": ms_,
                       "_ms": ms_})
+    pmc = os.path.join(ROOT, "profiles", "pmc_rmat.json")   # tools/gpu_pmc_rmat.sh
+    if os.path.exists(pmc):
+        pm = json.load(open(pmc))
+        for r in roofs:
+            pre = "edge_forward_kernel" if r["bound"] == "hbm" else "gemm_x3_kernel<true, true, true, 0,"
+            ks = [v for k, v in pm["kernels"].items() if k.startswith(pre)]
+            if ks:
+                n = sum(v["launches"] for v in ks)
+                r["traffic"] = sum((v["hbm_read_bytes"] + v["hbm_write_bytes"]) * v["launches"]
+                                   for v in ks) / n
+                r["traffic_source"] = f"profiles/pmc_rmat.json ({pm.get('source', '')})"
     roofs.sort(key=lambda r: -r["_ms"])
     for r in roofs:
         r.pop("_ms")

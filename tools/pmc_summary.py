@@ -30,7 +30,8 @@ for f in sorted(glob.glob(os.path.join(base + "_p*", "**", "*counter_collection.
             seen.add(key)
             acc[name]["_dur_us"].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 import json
-out_json = {"source": "rocprofv3 --pmc, bench.py --steps 3 --warmup 1: " + os.path.basename(base.rstrip("/").rsplit("/pmc", 1)[0]), "kernels": {}}
+label = os.environ.get("PMC_SOURCE", "bench.py --steps 3 --warmup 1")
+out_json = {"source": "rocprofv3 --pmc, " + label + ": " + os.path.basename(base.rstrip("/").rsplit("/pmc", 1)[0]), "kernels": {}}
 for n, cs in acc.items():
     d = {k: sum(v) / len(v) for k, v in cs.items()}
     out_json["kernels"][n] = {
