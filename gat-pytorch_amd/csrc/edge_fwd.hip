@@ -44,6 +44,58 @@ __global__ void __launch_bounds__(256) attention_max_kernel(const int32_t* __res
     part[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
 }
 
+// The same with the head count known: each thread takes 4 edges per round with every index and
+// score load of the round issued before any max (the plain loop keeps one edge's dependent
+// col -> S chain in flight per thread), score rows as float4 / float2 loads.
+template <int NHC>
+__global__ void __launch_bounds__(256) attention_max_vec_kernel(const int32_t* __restrict__ col,
+                                                                const int32_t* __restrict__ rowidx,
+                                                                int64_t E2,
+                                                                const float* __restrict__ S,
+                                                                float* __restrict__ part) {
+  constexpr int S2 = 2 * NHC, UE = 4;
+  constexpr int VEC = (NHC % 4 == 0) ? 4 : ((NHC % 2 == 0) ? 2 : 1);
+  float m = -INFINITY;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e0 < E2; e0 += UE * stride) {
+    int64_t sv[UE], dv[UE];
+#pragma unroll
+    for (int u = 0; u < UE; ++u) {
+      const int64_t e = min(e0 + u * stride, E2 - 1);   // clamped: a repeat cannot raise the max
+      sv[u] = col[e];
+      dv[u] = rowidx[e];
+    }
+    float a[UE][NHC], b[UE][NHC];
+#pragma unroll
+    for (int u = 0; u < UE; ++u)
+#pragma unroll
+      for (int h = 0; h < NHC; h += VEC) {
+        const float* ps = S + sv[u] * S2 + h;
+        const float* pd = S + dv[u] * S2 + NHC + h;
+        if constexpr (VEC == 4) {
+          const float4 x = *(const float4*)ps, y = *(const float4*)pd;
+          a[u][h] = x.x; a[u][h + 1] = x.y; a[u][h + 2] = x.z; a[u][h + 3] = x.w;
+          b[u][h] = y.x; b[u][h + 1] = y.y; b[u][h + 2] = y.z; b[u][h + 3] = y.w;
+        } else if constexpr (VEC == 2) {
+          const float2 x = *(const float2*)ps, y = *(const float2*)pd;
+          a[u][h] = x.x; a[u][h + 1] = x.y; b[u][h] = y.x; b[u][h + 1] = y.y;
+        } else {
+          a[u][h] = *ps; b[u][h] = *pd;
+        }
+      }
+#pragma unroll
+    for (int u = 0; u < UE; ++u)
+#pragma unroll
+      for (int h = 0; h < NHC; ++h) m = fmaxf(m, a[u][h] + b[u][h]);
+  }
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    part[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
 __global__ void __launch_bounds__(256) max_final_kernel(const float* __restrict__ part, int nb,
                                                         uint32_t* __restrict__ M_ord,
                                                         long long* __restrict__ argmax) {
@@ -784,7 +836,14 @@ extern "C" int gatx_attention_max(const int32_t* col, const int32_t* rowidx, int
   hipStream_t st = (hipStream_t)s;
   const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(E2, 256), kMaxBlocks));
   float* part = (float*)workspace;
-  attention_max_kernel<<<nb, 256, 0, st>>>(col, rowidx, E2, S, NH, part);
+  // S rows are float4/float2-aligned when 2*NH is a multiple of the vector width
+  const bool al = ((uintptr_t)S % 16) == 0;
+  if (E2 > 0 && al && NH == 4) attention_max_vec_kernel<4><<<nb, 256, 0, st>>>(col, rowidx, E2, S, part);
+  else if (E2 > 0 && al && NH == 8) attention_max_vec_kernel<8><<<nb, 256, 0, st>>>(col, rowidx, E2, S, part);
+  else if (E2 > 0 && al && NH == 6) attention_max_vec_kernel<6><<<nb, 256, 0, st>>>(col, rowidx, E2, S, part);
+  else if (E2 > 0 && al && NH == 2) attention_max_vec_kernel<2><<<nb, 256, 0, st>>>(col, rowidx, E2, S, part);
+  else if (E2 > 0 && NH == 1) attention_max_vec_kernel<1><<<nb, 256, 0, st>>>(col, rowidx, E2, S, part);
+  else attention_max_kernel<<<nb, 256, 0, st>>>(col, rowidx, E2, S, NH, part);
   GATX_LAUNCH_CHECK("attention_max");
   max_final_kernel<<<1, 256, 0, st>>>(part, nb, M_ord, (long long*)argmax);
   GATX_LAUNCH_CHECK("attention_max_final");
