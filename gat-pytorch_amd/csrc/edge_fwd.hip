@@ -651,42 +651,75 @@ __global__ void __launch_bounds__(256) attention_alpha_ei_kernel(
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ perm,
     float* __restrict__ alpha, long long* __restrict__ argmax) {
   constexpr int VEC = (NHC % 4 == 0) ? 4 : ((NHC % 2 == 0) ? 2 : 1);
+  constexpr int UE = NHC > 0 ? 4 : 1;   // edges per thread per round, all loads issued first
+  constexpr int NHA = NHC > 0 ? NHC : 1;
   const int NH = NHC > 0 ? NHC : NH_rt, S2 = 2 * NH;
   const float M = const_att ? 0.f : ord_to_float(*M_ord);
-  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < E2;
-       p += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t s = (int64_t)ei[p], d = (int64_t)ei[ld + p];
-    float* out = alpha + p * NH;
-    bool hit = false;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t p0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p0 < E2; p0 += UE * stride) {
     if constexpr (NHC > 0) {
-      float a[NHC];
+      int64_t sv[UE], dv[UE];
 #pragma unroll
-      for (int h = 0; h < NHC; ++h) {
-        const float raw = S[s * S2 + h] + S[d * S2 + NHC + h];
-        hit |= (!const_att && raw == M);
-        a[h] = (const_att ? 1.f : att_exp(raw, M)) / (den[d * NHC + h] + kSoftmaxEps);
+      for (int u = 0; u < UE; ++u) {
+        const int64_t p = min(p0 + u * stride, E2 - 1);
+        sv[u] = (int64_t)ei[p];
+        dv[u] = (int64_t)ei[ld + p];
       }
+      float a[UE][NHA], dn[UE][NHA];
 #pragma unroll
-      for (int h = 0; h < NHC; h += VEC) {
-        if constexpr (VEC == 4) *(float4*)(out + h) = make_float4(a[h], a[h + 1], a[h + 2], a[h + 3]);
-        else if constexpr (VEC == 2) *(float2*)(out + h) = make_float2(a[h], a[h + 1]);
-        else out[h] = a[h];
+      for (int u = 0; u < UE; ++u)
+#pragma unroll
+        for (int h = 0; h < NHC; ++h) {
+          a[u][h] = S[sv[u] * S2 + h] + S[dv[u] * S2 + NHC + h];
+          dn[u][h] = den[dv[u] * NHC + h];
+        }
+#pragma unroll
+      for (int u = 0; u < UE; ++u) {
+        const int64_t p = p0 + u * stride;
+        if (p >= E2) break;
+        float* out = alpha + p * NHC;
+        bool hit = false;
+        float r[NHA];
+#pragma unroll
+        for (int h = 0; h < NHC; ++h) {
+          hit |= (!const_att && a[u][h] == M);
+          r[h] = (const_att ? 1.f : att_exp(a[u][h], M)) / (dn[u][h] + kSoftmaxEps);
+        }
+#pragma unroll
+        for (int h = 0; h < NHC; h += VEC) {
+          if constexpr (VEC == 4) *(float4*)(out + h) = make_float4(r[h], r[h + 1], r[h + 2], r[h + 3]);
+          else if constexpr (VEC == 2) *(float2*)(out + h) = make_float2(r[h], r[h + 1]);
+          else out[h] = r[h];
+        }
+        if (hit) {   // rare: record every tied argmax (CSR slot, head) for max()'s gradient
+          int64_t e = rowptr[dv[u]];
+          while (perm[e] != (int32_t)p) ++e;
+          for (int h = 0; h < NHC; ++h)
+            if (a[u][h] == M) {
+              unsigned long long k = atomicAdd((unsigned long long*)argmax, 1ull);
+              if (k < GATX_ARGMAX_CAP) argmax[1 + k] = (long long)e * NHC + h;
+            }
+        }
       }
     } else {
+      const int64_t p = p0;
+      const int64_t s = (int64_t)ei[p], d = (int64_t)ei[ld + p];
+      float* out = alpha + p * NH;
+      bool hit = false;
       for (int h = 0; h < NH; ++h) {
         const float raw = S[s * S2 + h] + S[d * S2 + NH + h];
         hit |= (!const_att && raw == M);
         out[h] = (const_att ? 1.f : att_exp(raw, M)) / (den[d * NH + h] + kSoftmaxEps);
       }
-    }
-    if (hit) {   // rare: record every tied argmax (CSR slot, head) for max()'s gradient
-      int64_t e = rowptr[d];
-      while (perm[e] != (int32_t)p) ++e;
-      for (int h = 0; h < NH; ++h)
-        if (S[s * S2 + h] + S[d * S2 + NH + h] == M) {
-          unsigned long long k = atomicAdd((unsigned long long*)argmax, 1ull);
-          if (k < GATX_ARGMAX_CAP) argmax[1 + k] = (long long)e * NH + h;
-        }
+      if (hit) {
+        int64_t e = rowptr[d];
+        while (perm[e] != (int32_t)p) ++e;
+        for (int h = 0; h < NH; ++h)
+          if (S[s * S2 + h] + S[d * S2 + NH + h] == M) {
+            unsigned long long k = atomicAdd((unsigned long long*)argmax, 1ull);
+            if (k < GATX_ARGMAX_CAP) argmax[1 + k] = (long long)e * NH + h;
+          }
+      }
     }
   }
 }
@@ -803,7 +836,7 @@ extern "C" int gatx_attention_alpha_ei(const void* edge_index, int is64, int64_t
                                        gatx_stream_t s) {
   if (E2 == 0) return 0;
   hipStream_t st = (hipStream_t)s;
-  const unsigned grid = grid_for(E2, 256, 8192);
+  const unsigned grid = grid_for(ceil_div(E2, 4), 256, 8192);   // 4 edges per thread
 #define GATX_AE(C, I)                                                                          \
   attention_alpha_ei_kernel<C, I><<<grid, 256, 0, st>>>((const I*)edge_index, ld, E2, S, M_ord, \
                                                         den, NH, const_att, rowptr, perm, alpha, \
