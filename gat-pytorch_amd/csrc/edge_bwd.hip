@@ -483,6 +483,121 @@ __global__ void __launch_bounds__(256) edge_bwd_src_kernel(BwdArgs g) {
   }
 }
 
+// src pass of a head-mean layer: go is one row per node for every head (the mean's gradient
+// go / NH), so one wave per SOURCE node takes all NH heads: each go[dst] row is gathered once
+// and accumulated with the NH weights of the edge, instead of once per (source, head) item
+// (NH-fold fewer gathered bytes and NH-fold fewer items). Same per-head summation order as
+// edge_bwd_src_kernel.
+template <int LPE, int CPL>
+__global__ void __launch_bounds__(256) edge_bwd_src_mean_kernel(BwdArgs g) {
+  constexpr int EPW = 64 / LPE, NHM = 8;
+  constexpr int U = CPL <= 1 ? 8 : (CPL <= 2 ? 4 : 2);
+  const int lane = threadIdx.x & 63;
+  const int wave = uni(threadIdx.x >> 6);
+  const int grp = lane / LPE, li = lane % LPE;
+  const int64_t s = xcd_contiguous(blockIdx.x, gridDim.x) * 4 + wave;
+  if (s >= g.N) return;
+  const int NH = g.NH, Fp = g.Fp, F4 = Fp / 4, S2 = 2 * NH;
+  const int64_t Dp = (int64_t)NH * Fp, E2 = g.E2;
+  const float M = g.const_att ? 0.f : ord_to_float(*g.M_ord);
+  const bool drop = g.p_drop > 0.f;
+  const float drop_scale = drop ? 1.f / (1.f - g.p_drop) : 1.f;
+  const float4* __restrict__ go4 = (const float4*)g.go;
+  __shared__ int src_sh[4][64];
+  __shared__ float w_sh[4][NHM][64];
+  int* src_lds = src_sh[wave];
+  float (*w_lds)[64] = w_sh[wave];
+
+  int off4[CPL];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int q = c * LPE + li;
+    off4[c] = q < F4 ? q : 0;
+  }
+  float ssrc[NHM], gs[NHM];
+  float4 acc[NHM][CPL];
+#pragma unroll
+  for (int h = 0; h < NHM; ++h) {
+    ssrc[h] = (h < NH && !g.const_att) ? g.S[s * S2 + h] : 0.f;
+    gs[h] = 0.f;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) acc[h][c] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const float* __restrict__ graw = g.g_raw;
+
+  const int beg = uni(g.rowptr[s]), end = uni(g.rowptr[s + 1]);
+  for (int base = beg; base < end; base += 64) {
+    const int cnt = min(64, end - base);
+    const bool valid = lane < cnt;
+    const int j = base + min(lane, cnt - 1);
+    const int d = g.col[j];
+    const int e = g.seid[j];
+    const int64_t ep = drop ? (int64_t)g.perm[e] : 0;
+#pragma unroll
+    for (int h = 0; h < NHM; ++h) {
+      if (h >= NH) break;
+      float w = 0.f;
+      if (valid) {
+        const float ex = g.const_att ? 1.f : att_exp(ssrc[h] + g.S[(int64_t)d * S2 + NH + h], M);
+        w = ex / (g.den[(int64_t)d * NH + h] + kSoftmaxEps);
+        if (drop) w = dropout_keep(g.seed, ep * NH + h, g.p_drop) ? w * drop_scale : 0.f;
+        if (graw) gs[h] += graw[(int64_t)h * E2 + e];
+      }
+      w_lds[h][lane] = w;
+    }
+    src_lds[lane] = d;
+    wave_lds_sync();
+    for (int j0 = grp; j0 < cnt; j0 += EPW * U) {
+      float4 v[U][CPL];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const float4* rp = go4 + (int64_t)src_lds[min(j0 + u * EPW, cnt - 1)] * g.go_stride4;
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) v[u][c] = rp[off4[c]];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int jr = j0 + u * EPW;
+        const bool live = jr < cnt;
+        const int jc = live ? jr : 0;
+#pragma unroll
+        for (int h = 0; h < NHM; ++h) {
+          if (h >= NH) break;
+          const float wv = live ? w_lds[h][jc] : 0.f;
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) acc[h][c] = fma4(wv, v[u][c], acc[h][c]);
+        }
+      }
+    }
+    wave_lds_sync();
+  }
+  float* row = g.G_aug + s * g.ldg;
+#pragma unroll
+  for (int h = 0; h < NHM; ++h) {
+    if (h >= NH) break;
+#pragma unroll
+    for (int off = LPE; off < 64; off <<= 1) {
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) acc[h][c] = add4(acc[h][c], shfl_xor4(acc[h][c], off));
+    }
+    if (grp == 0) {
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) {
+        const int q = c * LPE + li;
+        if (q < F4) *(float4*)(row + (int64_t)h * Fp + 4 * q) = acc[h][c];
+      }
+    }
+  }
+  if (!g.const_att) {
+#pragma unroll
+    for (int h = 0; h < NHM; ++h) {
+      if (h >= NH) break;
+      const float v = group_sum<64>(gs[h]);
+      if (lane == 0) row[Dp + h] = v + (g.g_corr ? g.g_corr[s * NH + h] : 0.f);
+    }
+  }
+}
+
 // g_W[c][i] = gW_aug[pad(c)][i] + sum_h2 A2[h2][c] * gW_aug[Dp + h2][i]
 __global__ void __launch_bounds__(256) gw_kernel(const float* __restrict__ gW_aug,
                                                  const float* __restrict__ a, int NH, int F,
@@ -731,6 +846,16 @@ extern "C" int gatx_edge_backward_src(const float* S, const uint32_t* M_ord, con
   a.p_drop = p; a.seed = seed; a.g_raw = const_att ? nullptr : (float*)g_raw;
   a.g_corr = g_corr_src; a.G_aug = G_aug; a.ldg = ldg;
   a.chunk = kChunk;
+  static const bool per_head = [] {   // A/B switch: GATX_SRC_MEAN=0 keeps per-head items
+    const char* e = getenv("GATX_SRC_MEAN");
+    return e && e[0] == '0';
+  }();
+  if (!concat && NH <= 8 && !per_head) {   // head-mean: one item per source, all heads
+    const unsigned grid = (unsigned)ceil_div(N, 4);
+    GATX_DISPATCH_HEAD(gm, edge_bwd_src_mean_kernel, grid, a);
+    GATX_LAUNCH_CHECK("edge_bwd_src_mean");
+    return 0;
+  }
   a.n_items = ceil_div(N, kChunk) * kChunk * NH;
   const unsigned grid = (unsigned)ceil_div(a.n_items, 4);
   GATX_DISPATCH_HEAD(gm, edge_bwd_src_kernel, grid, a);
