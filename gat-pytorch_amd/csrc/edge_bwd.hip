@@ -12,7 +12,9 @@
 //   max bwd     g_M = -sum g_raw' (= -sum g_s_dst), split evenly over the argmax entries.
 //   src pass    one wave per (source s, head h): the message gradient sum alpha~ go[dst] (go rows
 //               gathered like the forward gathers Wh rows) and g_s_src = sum g_raw' + max share,
-//               written as one row of G_aug = [g_Wh | g_s_src | g_s_dst].
+//               written as one row of G_aug = [g_Wh | g_s_src | g_s_dst]. Head-mean layers
+//               (go one row per node, shared by every head) use one wave per source for all
+//               heads, so each go[dst] row is gathered once per edge instead of NH times.
 // The weight/input gradients then come from two MFMA GEMMs on G_aug (gemm.hip) and
 // gatx_weight_grads. No float atomics on the data path: every sum has a fixed order (bitwise
 // reproducible), except the tie-split of max()'s gradient when several argmax entries share a node.
