@@ -118,6 +118,12 @@ def ptr(t) -> int | None:
     return t.data_ptr()
 
 
+def version(t) -> int:
+    """In-place version counter of a tensor for cache keys. Inference tensors (made under
+    torch.inference_mode) track none and cannot be modified in place outside it: 0."""
+    return 0 if t.is_inference() else t._version
+
+
 def stream() -> int:
     return torch.cuda.current_stream().cuda_stream
 

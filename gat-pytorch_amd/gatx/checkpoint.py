@@ -138,6 +138,22 @@ def _as_tensor_spec(v):
     return key, dtype, int(offset), tuple(size), tuple(stride)
 
 
+def _check_view(name, numel: int, offset: int, size, stride):
+    """Bounds of a (offset, size, stride) view of a storage of `numel` elements, checked before
+    as_strided touches memory: a malformed or hostile pickle must not read outside the buffer."""
+    if len(size) != len(stride):
+        raise ValueError(f"{name}: size {size} and stride {stride} differ in rank")
+    if offset < 0 or any(s < 0 for s in size) or any(st < 0 for st in stride):
+        raise ValueError(f"{name}: negative offset/size/stride ({offset}, {size}, {stride})")
+    if any(s == 0 for s in size):
+        if offset > numel:
+            raise ValueError(f"{name}: offset {offset} past storage of {numel} elements")
+        return
+    last = offset + sum((s - 1) * st for s, st in zip(size, stride))
+    if last >= numel:
+        raise ValueError(f"{name}: view reaches element {last}, storage holds {numel}")
+
+
 def read_state_dict(path: str) -> dict:
     """{name: np.ndarray} for every tensor in the checkpoint's `state_dict` (copies, C-order)."""
     with zipfile.ZipFile(path) as zf:
@@ -158,7 +174,9 @@ def read_state_dict(path: str) -> dict:
             key, dtype, offset, size, stride = spec
             raw = np.frombuffer(zf.read(f"{root}/data/{key}"), dtype=dtype)
             itemsize = np.dtype(dtype).itemsize
+            _check_view(name, raw.size, offset, size, stride)
             arr = np.lib.stride_tricks.as_strided(
-                raw[offset:], shape=size, strides=tuple(s * itemsize for s in stride))
+                raw[offset:], shape=size, strides=tuple(s * itemsize for s in stride),
+                writeable=False)
             out[name] = np.ascontiguousarray(arr)
         return out

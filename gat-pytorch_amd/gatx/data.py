@@ -107,47 +107,75 @@ def uniform_graph_batch(num_graphs: int, nodes_per_graph: int, edges_per_graph: 
                       node_offsets=np.arange(G + 1, dtype=np.int64) * n)
 
 
-def rmat_edges(num_nodes: int, num_edges: int, seed: int = 42,
-               abcd=(0.57, 0.19, 0.19, 0.05)) -> np.ndarray:
-    """Graph500 R-MAT edge list (2, E') int64: ids drawn on a 2^scale grid, ids >= num_nodes
-    rejected, then vertex ids randomly permuted (SURVEY.md §8(d) "RMAT"). E' <= num_edges."""
-    scale = int(np.ceil(np.log2(max(num_nodes, 2))))
+def _rmat_draw(seed: int, n: int, scale: int, abcd):
+    """n raw R-MAT (src, dst) pairs on a 2^scale grid (Graph500 recursive quadrant choice)."""
     a, b, c, _ = abcd
-    src = np.zeros(num_edges, dtype=np.int64)
-    dst = np.zeros(num_edges, dtype=np.int64)
+    src = np.zeros(n, dtype=np.int64)
+    dst = np.zeros(n, dtype=np.int64)
     for lvl in range(scale):
-        u = uniform01(seed + 1000 * (lvl + 1), num_edges)
+        u = uniform01(seed + 1000 * (lvl + 1), n)
         right = (u >= a) & ((u < a + b) | (u >= a + b + c))   # quadrants b or d
         down = u >= a + b                                    # quadrants c or d
         src |= down.astype(np.int64) << lvl
         dst |= right.astype(np.int64) << lvl
-    keep = (src < num_nodes) & (dst < num_nodes)
-    src, dst = src[keep], dst[keep]
+    return src, dst
+
+
+def rmat_edges(num_nodes: int, num_edges: int, seed: int = 42,
+               abcd=(0.57, 0.19, 0.19, 0.05)) -> np.ndarray:
+    """Graph500 R-MAT edge list (2, num_edges) int64: ids drawn on a 2^scale grid, pairs with an
+    id >= num_nodes redrawn (fresh rounds of draws until exactly num_edges pairs remain), then
+    vertex ids randomly permuted (SURVEY.md §8(d) "RMAT")."""
+    scale = int(np.ceil(np.log2(max(num_nodes, 2))))
+    srcs, dsts, have, rnd = [], [], 0, 0
+    while have < num_edges:
+        need = num_edges - have
+        # oversample by the observed rejection rate so few rounds are needed
+        n = need if rnd == 0 else int(need * 1.3) + 64
+        src, dst = _rmat_draw(seed + 7919 * rnd, n, scale, abcd)
+        keep = (src < num_nodes) & (dst < num_nodes)
+        src, dst = src[keep][:need], dst[keep][:need]
+        srcs.append(src)
+        dsts.append(dst)
+        have += src.size
+        rnd += 1
+    src, dst = np.concatenate(srcs), np.concatenate(dsts)
     perm = np.argsort(splitmix64(seed ^ 0xA5A5A5A5, num_nodes), kind="stable")
     return np.stack([perm[src], perm[dst]])
 
 
 def rmat_edges_device(num_nodes: int, num_edges: int, seed: int = 42, device="cuda",
                       abcd=(0.57, 0.19, 0.19, 0.05)):
-    """rmat_edges on the device with torch's generator (same R-MAT recipe, not the same
-    draws): the full-size config (1e7 nodes, 1.6e8 edges) in well under a second. Returns a
-    (2, E') int64 device tensor."""
+    """rmat_edges on the device with torch's generator (same R-MAT recipe, including the redraw
+    of rejected pairs, not the same draws): the full-size config (1e7 nodes, exactly 1.6e8
+    edges) in about a second. Returns a (2, num_edges) int64 device tensor."""
     import torch
     scale = int(np.ceil(np.log2(max(num_nodes, 2))))
     a, b, c, _ = abcd
     g = torch.Generator(device=device)
     g.manual_seed(seed)
-    src = torch.zeros(num_edges, dtype=torch.int64, device=device)
-    dst = torch.zeros(num_edges, dtype=torch.int64, device=device)
-    for lvl in range(scale):
-        u = torch.rand(num_edges, generator=g, device=device)
-        right = (u >= a) & ((u < a + b) | (u >= a + b + c))
-        down = u >= a + b
-        src |= down.to(torch.int64) << lvl
-        dst |= right.to(torch.int64) << lvl
-        del u, right, down
-    keep = (src < num_nodes) & (dst < num_nodes)
-    src, dst = src[keep], dst[keep]
+    srcs, dsts, have, rnd = [], [], 0, 0
+    while have < num_edges:
+        need = num_edges - have
+        n = need if rnd == 0 else int(need * 1.3) + 64
+        src = torch.zeros(n, dtype=torch.int64, device=device)
+        dst = torch.zeros(n, dtype=torch.int64, device=device)
+        for lvl in range(scale):
+            u = torch.rand(n, generator=g, device=device)
+            right = (u >= a) & ((u < a + b) | (u >= a + b + c))
+            down = u >= a + b
+            src |= down.to(torch.int64) << lvl
+            dst |= right.to(torch.int64) << lvl
+            del u, right, down
+        keep = (src < num_nodes) & (dst < num_nodes)
+        src, dst = src[keep][:need], dst[keep][:need]
+        srcs.append(src)
+        dsts.append(dst)
+        have += int(src.numel())
+        rnd += 1
+    src = torch.cat(srcs) if len(srcs) > 1 else srcs[0]
+    dst = torch.cat(dsts) if len(dsts) > 1 else dsts[0]
+    del srcs, dsts
     perm = torch.randperm(num_nodes, generator=g, device=device)
     return torch.stack([perm[src], perm[dst]])
 

@@ -10,7 +10,7 @@ from __future__ import annotations
 
 import torch
 
-from ._lib import ARGMAX_CAP, call, lib, ptr, stream
+from ._lib import ARGMAX_CAP, call, lib, ptr, stream, version
 from .graph import Graph
 
 
@@ -116,40 +116,65 @@ def gemm_workspace(M: int, N: int, K: int, dev):
 _WPAD_CACHE: "OrderedDict" = None
 
 
+def _cacheable(*params) -> bool:
+    """Derived-weight caches are used only when no gradient flows to the weights (eval /
+    no_grad / inference): a training step rebuilds them from the live parameters every forward,
+    so in-place updates that bypass the version counter (`p.data.mul_()`, EMA / weight averaging
+    through `.data`) can never leave a stale copy in the gradient path. In no-grad use the key is
+    (storage, version counter): such a `.data` update between two eval forwards is not seen —
+    call `clear_weight_cache()` after one (load_state_dict and optimizer steps bump the version
+    and are seen)."""
+    if torch.is_grad_enabled() and any(p is not None and p.requires_grad for p in params):
+        return False
+    return True
+
+
+def clear_weight_cache():
+    """Drop every cached derived weight (W_aug, padded W); see _cacheable."""
+    if _WAUG_CACHE is not None:
+        _WAUG_CACHE.clear()
+    if _WPAD_CACHE is not None:
+        _WPAD_CACHE.clear()
+
+
 def padded_weight(W, ld: int):
     """W (rows x F_in) copied into rows of `ld` floats (zero tail, gatx_pad_rows) so GEMMs can
-    read it as float4 rows; cached on the parameter's identity and version."""
+    read it as float4 rows; cached on the parameter's identity and version (see _cacheable)."""
     global _WPAD_CACHE
     from collections import OrderedDict
     if W.size(1) == ld:
         return W
     if _WPAD_CACHE is None:
         _WPAD_CACHE = OrderedDict()
-    key = (W.data_ptr(), W._version, tuple(W.shape), W.device, ld)
-    hit = _WPAD_CACHE.get(key)
+    use_cache = _cacheable(W)
+    key = (W.data_ptr(), version(W), tuple(W.shape), W.device, ld)
+    hit = _WPAD_CACHE.get(key) if use_cache else None
     if hit is not None:
         _WPAD_CACHE.move_to_end(key)
         return hit[1]
     Wp = torch.empty((W.size(0), ld), dtype=torch.float32, device=W.device)
     call("gatx_pad_rows", ptr(W), W.size(0), W.size(1), W.size(1), ptr(Wp), ld, stream())
-    _WPAD_CACHE[key] = (W, Wp)
-    while len(_WPAD_CACHE) > 16:
-        _WPAD_CACHE.popitem(last=False)
+    if use_cache:
+        _WPAD_CACHE[key] = (W, Wp)
+        while len(_WPAD_CACHE) > 16:
+            _WPAD_CACHE.popitem(last=False)
     return Wp
 
 
 def augmented_weight(W, a, sh: "LayerShape"):
-    """W_aug = [W padded per head; A_src W; A_dst W] (gatx_prepare_weights). Cached on the
-    parameters' identity and version counters, so inference reuses it across steps while any
-    in-place update (optimizer step, load_state_dict) rebuilds it."""
+    """W_aug = [W padded per head; A_src W; A_dst W] (gatx_prepare_weights). Rebuilt every
+    training forward; in no-grad use cached on the parameters' identity and version counters,
+    so inference reuses it across steps while load_state_dict / optimizer steps rebuild it (see
+    _cacheable for the `.data` caveat)."""
     global _WAUG_CACHE
     from collections import OrderedDict
     if _WAUG_CACHE is None:
         _WAUG_CACHE = OrderedDict()
-    key = (W.data_ptr(), W._version, tuple(W.shape), W.device,
-           a.data_ptr() if a is not None else 0, a._version if a is not None else -1,
+    use_cache = _cacheable(W, a)
+    key = (W.data_ptr(), version(W), tuple(W.shape), W.device,
+           a.data_ptr() if a is not None else 0, version(a) if a is not None else -1,
            sh.NH, sh.F)
-    hit = _WAUG_CACHE.get(key)
+    hit = _WAUG_CACHE.get(key) if use_cache else None
     if hit is not None:
         _WAUG_CACHE.move_to_end(key)
         return hit[2]
@@ -157,9 +182,10 @@ def augmented_weight(W, a, sh: "LayerShape"):
     W_aug = torch.empty(waug_floats, dtype=torch.float32, device=W.device)
     with _span("prepare_weights", (sh.NH, sh.F, sh.F_in)):
         call("gatx_prepare_weights", ptr(W), ptr(a), sh.NH, sh.F, sh.F_in, ptr(W_aug), stream())
-    _WAUG_CACHE[key] = (W, a, W_aug)   # holding W / a pins their storage (no pointer reuse)
-    while len(_WAUG_CACHE) > 16:
-        _WAUG_CACHE.popitem(last=False)
+    if use_cache:
+        _WAUG_CACHE[key] = (W, a, W_aug)   # holding W / a pins their storage (no pointer reuse)
+        while len(_WAUG_CACHE) > 16:
+            _WAUG_CACHE.popitem(last=False)
     return W_aug
 
 
@@ -218,7 +244,15 @@ def use_reassociation(sh: LayerShape) -> bool:
     out_h = (sum alpha~ x[src]) W_h^T == sum alpha~ (x[src] W_h^T)."""
     if _env_int("GATX_REASSOC", 1) == 0:
         return False
-    return sh.concat and 2 * _round4(sh.F_in) <= sh.Dp
+    return sh.concat and 2 * _round4(sh.F_in) <= sh.Dp and reassoc_heads_per_item(sh) > 0
+
+
+def reassoc_heads_per_item(sh: LayerShape) -> int:
+    """Heads sharing one gathered x row in the reassociated edge pass: the largest divisor of NH
+    up to 8 whose HS * round4(F_in) row fits the edge kernel's 2048-float item (0: none fits)."""
+    Fin_p = _round4(sh.F_in)
+    fits = [d for d in range(1, 9) if sh.NH % d == 0 and d * Fin_p <= 2048]
+    return max(fits) if fits else 0
 
 
 def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: int,
@@ -258,7 +292,7 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
                      sh.NH, ptr(M_ord), ptr(argmax), ptr(_max_ws(dev)), s)
         Z = torch.empty((N, sh.NH * Fin_p), **f32)
         with _span("edge_forward", (N, E2, sh.NH, Fin_p, "x")):
-            hs_x = max(d for d in range(1, 9) if sh.NH % d == 0)   # heads sharing one x row
+            hs_x = reassoc_heads_per_item(sh)   # heads sharing one x row
             call("gatx_edge_forward_ex", ptr(x_rows), Fin_p, 0, ptr(S), ptr(M_ord),
                  ptr(graph.rowptr), ptr(graph.col), ptr(graph.perm), N, sh.NH, Fin_p, hs_x, 1,
                  int(sh.const), None, float(p), seed, ptr(Z), sh.NH * Fin_p, None, 0, 0,

@@ -15,7 +15,7 @@ from collections import OrderedDict
 import torch
 
 from . import _lib
-from ._lib import call, ptr, stream
+from ._lib import call, ptr, stream, version
 
 
 class Graph:
@@ -113,7 +113,7 @@ class GraphCache:
 
     @staticmethod
     def _key(t: torch.Tensor, num_nodes: int, add_self_loops: bool):
-        return (t.data_ptr(), t._version, tuple(t.shape), tuple(t.stride()), t.dtype,
+        return (t.data_ptr(), version(t), tuple(t.shape), tuple(t.stride()), t.dtype,
                 t.device, num_nodes, add_self_loops)
 
     def get(self, edge_index: torch.Tensor, num_nodes: int, add_self_loops: bool) -> Graph:
@@ -135,7 +135,7 @@ class GraphCache:
         for t, g in reversed(self._d.values()):
             ei = g.edge_index
             if ei is edge_index or (ei.data_ptr() == edge_index.data_ptr()
-                                    and ei._version == edge_index._version
+                                    and version(ei) == version(edge_index)
                                     and ei.shape == edge_index.shape
                                     and ei.stride() == edge_index.stride()
                                     and ei.dtype == edge_index.dtype):

@@ -407,7 +407,8 @@ def test_errors_mirror_reference(device):
 
 @pytest.mark.parametrize("x_grad", [True, False])
 @pytest.mark.parametrize("reassoc", ["0", "1"])
-@pytest.mark.parametrize("fin,NH,F", [(50, 4, 256), (3, 4, 12), (13, 2, 40), (8, 8, 30)])
+@pytest.mark.parametrize("fin,NH,F", [(50, 4, 256), (3, 4, 12), (13, 2, 40), (8, 8, 30),
+                                      (300, 8, 128)])
 def test_reassociation_paths(reassoc, fin, NH, F, x_grad, device, monkeypatch):
     """First-layer reassociation (aggregate x rows, then project per head) vs the direct path;
     both against the oracle, forward and backward. Without an input gradient the reassociated
