@@ -1,6 +1,7 @@
 """Benchmark: GAT-layer edges/s + achieved HBM GB/s, PPI 3-layer forward (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--graphs G] [--mode fwd|train]
+                    [--workload ppi|pattern|rmat]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
 Workload: per rank a synthetic PPI-shaped batch of G graphs (2245 nodes and 61318
@@ -10,13 +11,24 @@ layer 1, ELU between layers) with random (xavier) weights, eval mode. One step =
 preprocessing of a fresh batch (self-loop rewrite + CSR build, as every reference forward does
 per layer) + the 3-layer forward. Weak scaling: each rank processes its own G graphs; the forward
 has no exchange step, so there is no collective in the timed region (--mode train adds the
-backward and an RCCL gradient all-reduce, DDP-style).
+backward and the overlapped RCCL gradient all-reduce, gatx.distributed.GradientAllReducer).
 
-value = (sum over ranks of 3 layers x E' edges per step) / step time (max over ranks).
-roofline = the dominant kernel's algorithmic bytes (or flops) per launch / its average launch time,
-measured with HIP events on the launch stream over the last steps // 10 steps of the timed region
-(only those carry events: each record costs the stream ~10 us). cpu_baseline = the numpy
-oracle (oracle/gat_oracle.py, the reference's dataflow restated) on a bounded sample, rank 0, N=1.
+value = (sum over ranks of layers x E' edges per step) / step time (max over ranks).
+Byte accounting (all per step, all reported):
+  unique_GBps        - the dataflow actually run, every array read/written once (gathered rows
+                       once per node): the HBM-compulsory traffic / step time
+  roofline_time_frac - sum over kernels of max(unique bytes / 8 TB/s, flops / GEMM peak) over the
+                       step time (<= 1 by construction when the clock is honest)
+  hbm_measured       - rocprofv3 PMC bytes (FETCH_SIZE x 2 + WRITE_SIZE) per step from the
+                       committed profiles/pmc_*.json summary, over this run's step time
+  l2_gather_GBps     - SURVEY.md §8d's formula (one Wh row per EDGE, no reuse credited): the
+                       gather rate the caches serve, NOT an HBM figure
+roofline = the dominant kernel's flops (GEMM) or unique bytes (edge pass) per launch / its
+average launch time, measured with HIP events on the launch stream over the last steps // 10
+steps of the timed region (only those carry events: each record costs the stream ~10 us).
+cpu_baseline = the reference dataflow restated in torch eager (oracle/torch_dataflow.py) on a
+bounded sample, every available host core, rank 0, N=1 (the reference itself is timed in the
+build container: bench/cpu_reference_baseline.json).
 """
 from __future__ import annotations
 
@@ -93,94 +105,226 @@ def layer_dims(cfg):
             for i in range(cfg["num_layers"])]
 
 
-def algorithmic(N, E2, F_in, NH, F, concat):
-    """SURVEY.md §8(d) per-layer algorithmic bytes / flops (fp32 = 4 B, int32 indices)."""
+def _r4(v):
+    return (v + 3) // 4 * 4
+
+
+def survey_bytes(N, E2, F_in, NH, F, concat):
+    """SURVEY.md §8(d)'s per-layer formulas (fp32 = 4 B, int32 indices): B_gemm, FLOP_gemm and
+    B_edge, which prices one Wh[src] row gather PER EDGE (no cache reuse credited). That is the
+    traffic an L2-less machine would move, not HBM bytes: reported as `l2_gather_GBps` only."""
     b_gemm = 4 * (N * F_in + F_in * NH * F + N * NH * F + 2 * N * NH)
     f_gemm = 2 * N * F_in * NH * F + 4 * N * NH * NH * F
-    # edge_forward alone: rowptr + col + perm + s_src gathers + s_dst + Wh[src] rows + alpha
-    # write + den write + output write
-    b_edge_fwd = 4 * ((N + 1) + 2 * E2 + E2 * NH + N * NH + E2 * NH * F + E2 * NH + N * NH
-                      + (N * NH * F if concat else N * F))
-    # attention_max alone: col + rowidx + s gathers
-    b_max = 4 * (2 * E2 + 2 * E2 * NH)
-    b_edge_survey = 4 * (2 * (E2 + N + 1) + 2 * (E2 * NH + N * NH) + E2 * NH * F + E2 * NH
-                         + (N * NH * F if concat else N * F))
-    return dict(b_gemm=b_gemm, f_gemm=f_gemm, b_edge_fwd=b_edge_fwd, b_max=b_max,
-                b_edge=b_edge_survey)
+    b_edge = 4 * (2 * (E2 + N + 1) + 2 * (E2 * NH + N * NH) + E2 * NH * F + E2 * NH
+                  + (N * NH * F if concat else N * F))
+    return b_gemm, f_gemm, b_edge
 
 
-def cpu_baseline(model_np, cfg, budget_s=20.0):
-    """Time the numpy oracle (reference dataflow) on one PPI graph, 3-layer forward."""
-    from oracle import gat_oracle as orc
+def layer_dataflow(N, E2, F_in, NH, F, concat, resid):
+    """Per-kernel UNIQUE bytes (each array read or written once: the HBM-compulsory traffic) and
+    flops of one gatx layer forward, following the dataflow the library actually runs
+    (gatx.functional.layer_forward): the reassociated first layer gathers 4*round4(F_in)-byte x
+    rows, the others 4*NH*Fp-byte Wh rows; gathered rows are counted once per node, not per edge.
+    Returns [(kernel, bytes, flops)]."""
+    from gatx.functional import LayerShape, fold_scores_into_gemm, use_reassociation
+    sh = LayerShape(NH, F, F_in, concat, False)
+    H2, Fp, Dp = 2 * NH, sh.Fp, sh.Dp
+    oc = sh.out_cols
+    r = oc if resid else 0
+    mx = ("attention_max", 4 * (2 * E2 + N * H2), 0)
+    alpha = ("attention_alpha", 16 * E2 + 4 * (N * H2 + N * NH + E2 * NH), 0)
+    if use_reassociation(sh):
+        Fin_p = _r4(F_in)
+        return [
+            ("gemm_scores", 4 * (N * F_in + H2 * F_in + N * H2), 2 * N * F_in * H2),
+            mx,
+            ("edge_forward", 4 * ((N + 1) + E2 + N * H2 + N * Fin_p + N * NH * Fin_p + N * NH), 0),
+            alpha,
+            ("gemm_out", 4 * (N * NH * Fin_p + NH * F * Fin_p + N * oc + N * r),
+             2 * N * Fin_p * NH * F),
+        ]
+    out = []
+    if fold_scores_into_gemm(sh):
+        out.append(("gemm", 4 * (N * F_in + (Dp + H2) * F_in + N * Dp + N * H2),
+                    2 * N * F_in * (NH * F + H2)))
+    else:
+        out.append(("gemm", 4 * (N * F_in + Dp * F_in + N * Dp), 2 * N * F_in * NH * F))
+        out.append(("node_scores", 4 * (N * Dp + N * H2), 2 * N * Dp * H2))
+    out += [mx,
+            ("edge_forward", 4 * ((N + 1) + E2 + N * H2 + N * Dp + N * NH + N * oc + N * r), 0),
+            alpha]
+    return out
+
+
+def graph_build_bytes(E, E2, N):
+    """Compulsory bytes of the per-step graph preprocessing: read edge_index (int64), write
+    edge_index' (int64) and the int32 CSR (col, rowidx, perm, rowptr)."""
+    return 16 * E + 16 * E2 + 12 * E2 + 4 * (N + 1)
+
+
+def pmc_step_bytes(pm_path, step_ms):
+    """L2->fabric bytes per step measured by rocprofv3 (FETCH_SIZE x 2 + WRITE_SIZE, the
+    MI355X_MICROARCH.md gfx950 correction; Infinity-Cache hits are included, so this bounds HBM
+    traffic from above), summed over the kernels of the profiled steps (kernels launched at least
+    once per step; one-off setup kernels excluded)."""
+    if not os.path.exists(pm_path):
+        return None
+    pm = json.load(open(pm_path))
+    steps = pm.get("steps", 4)
+    tot = 0.0
+    for v in pm["kernels"].values():
+        if v["launches"] >= steps:
+            tot += (v["hbm_read_bytes"] + v["hbm_write_bytes"]) * v["launches"]
+    per_step = tot / steps
+    gbs = per_step / (step_ms * 1e-3) / 1e9
+    return {"bytes_per_step": per_step, "GBps": round(gbs, 1),
+            "frac_of_peak": round(gbs / HBM_PEAK_GBS, 4),
+            "source": f"{os.path.relpath(pm_path, ROOT)} ({pm.get('source', '')}); step time of "
+                      "this run",
+            "note": "rocprofv3 FETCH_SIZE x2 + WRITE_SIZE (gfx950 correction); counts "
+                    "Infinity-Cache hits, so an upper bound on HBM bytes"}
+
+
+def available_cores():
+    """Host cores this process may use: the affinity set, capped by a cgroup CPU quota if one is
+    set (the GPU box grants each job a share of a larger machine)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = max(1, min(n, int(int(q) // int(per))))
+    except Exception:
+        pass
+    return n
+
+
+def _cpu_timer(fn, budget_s):
+    times = []
+    t_start = time.perf_counter()
+    fn()   # warm-up
+    while True:
+        t0 = time.perf_counter()
+        fn()
+        times.append(time.perf_counter() - t0)
+        if time.perf_counter() - t_start > budget_s or len(times) >= 3:
+            break
+    return min(times), len(times)
+
+
+def cpu_baseline(model, cfg, ds, graphs, budget_s=20.0):
+    """The reference's CPU dataflow restated in torch eager (oracle/torch_dataflow.py: index,
+    cat, mm through `a`, max, exp, scatter_add_, exactly the ops of models/gat_layer.py:64-127)
+    on `graphs` graphs of the same workload, every available host core."""
+    from oracle import torch_dataflow as td
     from gatx import data as gd
-    try:
-        from threadpoolctl import threadpool_limits
-    except Exception:  # pragma: no cover
-        threadpool_limits = None
-    cores = min(16, len(os.sched_getaffinity(0)))
-    b = gd.dataset_batch("PPI", 1, graph_seed=4242)
+    cores = available_cores()
+    torch.set_num_threads(cores)
+    b = gd.dataset_batch(ds, graphs, graph_seed=4242)
     dims = layer_dims(cfg)
-    ctx = threadpool_limits(limits=cores) if threadpool_limits else None
-    times, e_tot = [], 0
-    try:
-        t_start = time.perf_counter()
-        while True:
-            t0 = time.perf_counter()
-            out, ei, alphas = orc.gat_model_forward(
-                b.x, b.edge_index, model_np["layers"], model_np["skips"],
-                cfg["num_heads_per_layer"], [d[2] for d in dims], cfg["heads_concat_per_layer"],
-                cfg["add_skip_connection"])
-            times.append(time.perf_counter() - t0)
-            e_tot = sum(a.shape[0] for a in alphas)
-            if time.perf_counter() - t_start > budget_s or len(times) >= 3:
-                break
-    finally:
-        if ctx is not None:
-            ctx.__exit__(None, None, None)
-    best = min(times)
-    return {"value": e_tot / best, "unit": "layer-edges/s", "cores": cores, "kind": "port",
-            "sample": f"numpy oracle (reference dataflow), PPI 3-layer fwd on 1 graph "
-                      f"(N={b.num_nodes}, sum E'={e_tot}), best of {len(times)}: {best:.2f} s"}
+    layers = [(l.W.weight.detach().cpu(), l.a.weight.detach().cpu()) for l in model.gat_layer_list]
+    skips = [None if isinstance(s, torch.nn.Identity) else s.weight.detach().cpu()
+             for s in model.skip_layer_list]
+    x = torch.from_numpy(b.x)
+    ei = torch.from_numpy(b.edge_index)
+    res = {}
+
+    def run():
+        with torch.no_grad():
+            res["o"] = td.model_forward(x, ei, layers, skips, cfg["num_heads_per_layer"],
+                                        [d[2] for d in dims], cfg["heads_concat_per_layer"],
+                                        cfg["add_skip_connection"])
+    best, n = _cpu_timer(run, budget_s)
+    e_tot = sum(a.shape[0] for a in res["o"][2])
+    return {"value": e_tot / best, "unit": "layer-edges/s", "cores": cores, "kind": "restatement",
+            "sample": f"torch-eager restatement of the reference dataflow (oracle/torch_dataflow.py),"
+                      f" {ds} {len(dims)}-layer fwd on {graphs} graph(s) (N={b.num_nodes}, sum "
+                      f"E'={e_tot}), {cores} threads, best of {n}: {best:.3f} s; the reference "
+                      "itself, timed in the build container: bench/cpu_reference_baseline.json"}
 
 
 def cpu_baseline_rmat(W, a, NH, F, budget_s=20.0):
-    """The numpy oracle on a scaled RMAT (1e5 nodes / 1.6e6 edges, SURVEY.md §8d 'RMAT on CPU'),
-    one GATLayer forward (F_in 512 -> 8 x 64 concat)."""
-    from oracle import gat_oracle as orc
+    """The torch restatement on a scaled RMAT (1e5 nodes / 1.6e6 edges, SURVEY.md §8d 'RMAT on
+    CPU'), one GATLayer forward (F_in 512 -> 8 x 64 concat)."""
+    from oracle import torch_dataflow as td
     from gatx import data as gd
-    try:
-        from threadpoolctl import threadpool_limits
-    except Exception:  # pragma: no cover
-        threadpool_limits = None
-    cores = min(16, len(os.sched_getaffinity(0)))
+    cores = available_cores()
+    torch.set_num_threads(cores)
     n, e = 100_000, 1_600_000
-    ei = gd.rmat_edges(n, e, seed=4242)
-    x = gd.normal(7, n * W.shape[1]).reshape(n, W.shape[1])
-    ctx = threadpool_limits(limits=cores) if threadpool_limits else None
-    times, E2 = [], 0
-    try:
-        t_start = time.perf_counter()
-        while True:
-            t0 = time.perf_counter()
-            out, ei2, alpha, _ = orc.gat_layer_forward(x, ei, W, a, NH, F, True)
-            times.append(time.perf_counter() - t0)
-            E2 = alpha.shape[0]
-            if time.perf_counter() - t_start > budget_s or len(times) >= 3:
-                break
-    finally:
-        if ctx is not None:
-            ctx.__exit__(None, None, None)
-    best = min(times)
-    return {"value": E2 / best, "unit": "layer-edges/s", "cores": cores, "kind": "port",
-            "sample": f"numpy oracle (reference dataflow), 1 GATLayer fwd on a SCALED RMAT "
-                      f"(N={n}, E'={E2}; the full 1e7/1.6e8 graph is infeasible on CPU), best of "
-                      f"{len(times)}: {best:.2f} s"}
+    ei = torch.from_numpy(gd.rmat_edges(n, e, seed=4242))
+    x = torch.from_numpy(gd.normal(7, n * W.shape[1]).reshape(n, W.shape[1]))
+    Wt, at = torch.from_numpy(W), torch.from_numpy(a)
+    res = {}
+
+    def run():
+        with torch.no_grad():
+            res["o"] = td.layer_forward(x, ei, Wt, at, NH, F, True)
+    best, k = _cpu_timer(run, budget_s)
+    E2 = res["o"][2].shape[0]
+    return {"value": E2 / best, "unit": "layer-edges/s", "cores": cores, "kind": "restatement",
+            "sample": f"torch-eager restatement of the reference dataflow, 1 GATLayer fwd on a "
+                      f"SCALED RMAT (N={n}, E'={E2}; the full 1e7/1.6e8 graph is infeasible on "
+                      f"CPU), {cores} threads, best of {k}: {best:.3f} s"}
+
+
+def kernel_summary(summ, n_instr):
+    kern = {}
+    for phase, recs in summ.items():
+        tot = sum(t for _, t in recs)
+        kern[phase] = {"launches": len(recs), "avg_ms": tot / len(recs),
+                       "total_ms_per_step": tot / n_instr}
+    return kern
+
+
+def roofline_objects(summ, unique_edge_bytes, pmc_path):
+    """The two roofline objects (projection GEMM: MFMA-bound; edge pass: HBM-bound), each priced
+    per launch from the live HIP-event durations, the GEMM by its flops, the edge pass by its
+    UNIQUE bytes (the gathered rows once, CSR, scores, output). `traffic` = the PMC-measured
+    L2->fabric bytes per launch of the same kernel when a summary is committed."""
+    roofs = {}
+    gem = summ.get("gemm", [])
+    if gem:
+        fl = sum(2.0 * n * fin * (nh * f + 2 * nh) for (n, _, fin, nh, f), _ in gem)
+        ms_ = sum(t for _, t in gem)
+        tfs = fl / (ms_ * 1e-3) / 1e12
+        gr = gemm_roof()
+        roofs["gemm"] = {"bound": "mfma", "kernel": gr["kernel"] + ", projection x.W_aug^T",
+                         "achieved": round(tfs, 2), "peak": round(gr["peak"], 1),
+                         "unit": "TFLOP/s", "frac": round(tfs / gr["peak"], 4), "traffic": None,
+                         "gemm_mode": gr["mode"], "flops_per_launch": fl / len(gem),
+                         "avg_launch_ms": ms_ / len(gem), "_prefix": gr["prefix"], "_ms": ms_}
+    edg = summ.get("edge_forward", [])
+    if edg:
+        by = sum(unique_edge_bytes(info) for info, _ in edg)
+        ms_ = sum(t for _, t in edg)
+        gbs = by / (ms_ * 1e-3) / 1e9
+        roofs["edge_forward"] = {"bound": "hbm", "kernel": "edge_forward_kernel<*> (all layers)",
+                                 "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                                 "bytes_per_launch": by / len(edg),
+                                 "bytes_basis": "unique bytes: gathered rows once per node, CSR, "
+                                                "scores, den, output (+ residual)",
+                                 "avg_launch_ms": ms_ / len(edg),
+                                 "_prefix": "edge_forward_kernel", "_ms": ms_}
+    if os.path.exists(pmc_path):
+        pm = json.load(open(pmc_path))
+        for r in roofs.values():
+            ks = [v for k, v in pm["kernels"].items() if k.startswith(r["_prefix"])]
+            if ks:
+                n = sum(v["launches"] for v in ks)
+                r["traffic"] = sum((v["hbm_read_bytes"] + v["hbm_write_bytes"]) * v["launches"]
+                                   for v in ks) / n
+                r["traffic_source"] = f"{os.path.relpath(pmc_path, ROOT)} ({pm.get('source', '')})"
+    ordered = sorted(roofs.values(), key=lambda r: -r["_ms"])
+    for r in ordered:
+        r.pop("_prefix")
+        r.pop("_ms")
+    return ordered
 
 
 def run_rmat(args, world, rank, dev):
     """BASELINE config 5: one GATLayer (F_in 512 -> 8 heads x 64, concat, self-loops) forward on
-    a synthetic R-MAT graph (1e7 nodes, 1.6e8 edges), eval mode, CSR built per step. One graph,
-    no sharding: with --gpus N each rank runs an independent replica (value sums them)."""
+    a synthetic R-MAT graph (1e7 nodes, exactly 1.6e8 edges), eval mode, CSR built per step. One
+    graph, no sharding: with --gpus N each rank runs an independent replica (value sums them)."""
     from gatx import GATLayer, clear_graph_cache
     from gatx import data as gd
     NH, F, FIN = 8, 64, 512
@@ -203,67 +347,36 @@ def run_rmat(args, world, rank, dev):
     from gatx.graph import graph_cache
     E2 = graph_cache.get(ei, N, True).num_edges
     elapsed, summ, n_instr = run_timed(step, args.steps, world, dev)
-    ms = elapsed / args.steps * 1e3
-    alg = algorithmic(N, E2, FIN, NH, F, True)
-    kern = {}
-    for phase, recs in summ.items():
-        tot = sum(t for _, t in recs)
-        kern[phase] = {"launches": len(recs), "avg_ms": tot / len(recs),
-                       "total_ms_per_step": tot / n_instr}
-    roofs = []
-    edg = summ.get("edge_forward", [])
-    if edg:
-        by = alg["b_edge_fwd"] - 4.0 * E2 * NH     # alpha is written by attention_alpha
-        ms_ = sum(t for _, t in edg) / len(edg)
-        gbs = by / (ms_ * 1e-3) / 1e9
-        roofs.append({"bound": "hbm", "kernel": "edge_forward_kernel (Wh[src] row gathers)",
-                      "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                      "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
-                      "bytes_per_launch": by, "avg_launch_ms": ms_, "_ms": ms_})
-    gem = summ.get("gemm", [])
-    if gem:
-        fl = 2.0 * N * FIN * NH * F
-        ms_ = sum(t for _, t in gem) / len(gem)
-        tfs = fl / (ms_ * 1e-3) / 1e12
-        gr = gemm_roof()
-        roofs.append({"bound": "mfma", "kernel": gr["kernel"] + ", projection x.W^T",
-                      "achieved": round(tfs, 2), "peak": round(gr["peak"], 1), "unit": "TFLOP/s",
-                      "frac": round(tfs / gr["peak"], 4), "traffic": None,
-                      "gemm_mode": gr["mode"], "flops_per_launch": fl, "avg_launch_ms": ms_,
-                      "_ms": ms_})
-    pmc = os.path.join(ROOT, "profiles", "pmc_rmat.json")   # tools/gpu_pmc_rmat.sh
-    if os.path.exists(pmc):
-        pm = json.load(open(pmc))
-        for r in roofs:
-            pre = "edge_forward_kernel" if r["bound"] == "hbm" else "gemm_x3_kernel<true, true, true, 0,"
-            ks = [v for k, v in pm["kernels"].items() if k.startswith(pre)]
-            if ks:
-                n = sum(v["launches"] for v in ks)
-                r["traffic"] = sum((v["hbm_read_bytes"] + v["hbm_write_bytes"]) * v["launches"]
-                                   for v in ks) / n
-                r["traffic_source"] = f"profiles/pmc_rmat.json ({pm.get('source', '')})"
-    roofs.sort(key=lambda r: -r["_ms"])
-    for r in roofs:
-        r.pop("_ms")
+    step_s = elapsed / args.steps
+    flow = layer_dataflow(N, E2, FIN, NH, F, True, False)
+    uniq = sum(b for _, b, _ in flow) + graph_build_bytes(E, E2, N)
+    peak = gemm_roof()["peak"] * 1e12
+    t_roof = sum(max(b / (HBM_PEAK_GBS * 1e9), f / peak) for _, b, f in flow) \
+        + graph_build_bytes(E, E2, N) / (HBM_PEAK_GBS * 1e9)
+    b_gemm, _, b_edge = survey_bytes(N, E2, FIN, NH, F, True)
+    edge_b = [b for k, b, _ in flow if k == "edge_forward"][0]
+    roofs = roofline_objects(summ, lambda info: edge_b, os.path.join(ROOT, "profiles",
+                                                                    "pmc_rmat.json"))
     result = {
         "metric": "GAT-layer edges/sec + achieved HBM GB/s, RMAT 1-layer fwd",
-        "value": round(E2 * world / (elapsed / args.steps), 1), "unit": "layer-edges/s",
-        "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
+        "value": round(E2 * world / step_s, 1), "unit": "layer-edges/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(step_s * 1e3, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
-        "data": "synthetic R-MAT (a,b,c,d)=(0.57,0.19,0.19,0.05), ids permuted, x ~ N(0,1), "
-                "xavier weights",
+        "data": "synthetic R-MAT (a,b,c,d)=(0.57,0.19,0.19,0.05), rejected ids redrawn, ids "
+                "permuted, x ~ N(0,1), xavier weights",
         "config": {"workload": f"RMAT {N} nodes / {E} edges, GATLayer 512 -> 8x64 concat, "
                                "self-loops, eval, CSR built per step",
                    "nodes": N, "edges_in": int(ei.size(1)), "edges_per_layer": E2,
                    "parallelism": "replicas" if world > 1 else "single GPU"},
-        "achieved_GBps_algorithmic_per_gpu": round((alg["b_gemm"] + alg["b_edge"])
-                                                   / (elapsed / args.steps) / 1e9, 1),
-        "roofline_time_frac": round(max((alg["b_gemm"] + alg["b_edge"]) / (HBM_PEAK_GBS * 1e9),
-                                        alg["f_gemm"] / (gemm_roof()["peak"] * 1e12))
-                                    / (ms * 1e-3), 4),
+        "unique_GBps": round(uniq / step_s / 1e9, 1),
+        "roofline_time_frac": round(t_roof / step_s, 4),
+        "l2_gather_GBps": round((b_gemm + b_edge) / step_s / 1e9, 1),
+        "hbm_measured": pmc_step_bytes(os.path.join(ROOT, "profiles", "pmc_rmat.json"),
+                                       step_s * 1e3),
         "roofline": roofs[0] if roofs else None,
         "roofline_other": roofs[1] if len(roofs) > 1 else None,
-        "kernels": kern,
+        "kernels": kernel_summary(summ, n_instr),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_rmat(layer.W.weight.detach().cpu().numpy(),
@@ -315,7 +428,7 @@ def main():
     from gatx import GATModel, clear_graph_cache
     from gatx import data as gd
     from gatx.config import data_config
-    from gatx.distributed import allreduce_gradients
+    from gatx.distributed import GradientAllReducer, count_weight
 
     ds = "PATTERN" if args.workload == "pattern" else "PPI"
     if args.graphs is None:
@@ -324,8 +437,6 @@ def main():
     torch.manual_seed(0)
     model = GATModel(**cfg).to(dev)
     model.train(args.mode == "train")
-    if args.mode == "fwd":
-        model.eval()
     b = gd.dataset_batch(ds, args.graphs, graph_seed=42 + 1000 * rank, feature_seed=1 + rank)
     x = torch.from_numpy(b.x).to(dev)
     ei = torch.from_numpy(b.edge_index).to(dev)
@@ -335,7 +446,13 @@ def main():
     if ds == "PATTERN":   # PatternGAT (models/pattern_gat.py:11-15): class-balanced BCE
         loss_fn = torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([1 / 0.1765], device=dev))
         y = y[:, 0]
-    params = [p for p in model.parameters()]
+    reducer = None
+    w_loss = 1.0
+    if args.mode == "train" and world > 1:
+        # DDP-style: buckets all-reduced (SUM) over RCCL as backward produces them; each rank's
+        # mean loss weighted by its share of the union batch's nodes
+        reducer = GradientAllReducer(model.parameters(), average=False)
+        w_loss = count_weight(b.num_nodes, device=dev if backend == "nccl" else "cpu")
 
     def step():
         if not args.cached_graph:
@@ -343,33 +460,27 @@ def main():
         if args.mode == "fwd":
             with torch.no_grad():
                 return model(x, ei)
+        opt.zero_grad(set_to_none=True)
         if ds == "PATTERN":   # PatternGAT.training_step (models/pattern_gat.py:18-25)
             out = model(x, ei).squeeze(-1)
             loss = loss_fn(out, y)
-            opt.zero_grad(set_to_none=True)
-            loss.backward()
-            if world > 1:
-                allreduce_gradients(params, world)
-            opt.step()
-            return out
-        # PPI_GAT.training_step (models/ppi_gat.py:15-33): BCE + the attention norm, computed
-        # every step (logged; added to the loss only with a non-zero attention_penalty)
-        out, ei2, atts = model.forward_and_return_attention(x, ei)
-        loss = loss_fn(out, y)
-        attention_norm = model.calc_attention_norm(ei2, atts)
-        if args.attention_penalty != 0.0:
-            loss = loss + args.attention_penalty * attention_norm
-        opt.zero_grad(set_to_none=True)
-        loss.backward()
-        if world > 1:   # one flat bucket (7.47 MB) all-reduced over RCCL
-            allreduce_gradients(params, world)
+        else:
+            # PPI_GAT.training_step (models/ppi_gat.py:15-33): BCE + the attention norm, computed
+            # every step (logged; added to the loss only with a non-zero attention_penalty)
+            out, ei2, atts = model.forward_and_return_attention(x, ei)
+            loss = loss_fn(out, y)
+            attention_norm = model.calc_attention_norm(ei2, atts)
+            if args.attention_penalty != 0.0:
+                loss = loss + args.attention_penalty * attention_norm
+        (loss * w_loss if w_loss != 1.0 else loss).backward()
+        if reducer is not None:
+            reducer.finish()
         opt.step()
         return out
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    # per-layer E' of this batch
     from gatx.graph import graph_cache
     g = graph_cache.get(ei, b.num_nodes, True)
     E2 = g.num_edges
@@ -377,63 +488,32 @@ def main():
     dims = layer_dims(cfg)
 
     elapsed, summ, n_instr = run_timed(step, args.steps, world, dev)
-    ms = elapsed / args.steps * 1e3
-
+    step_s = elapsed / args.steps
+    ms = step_s * 1e3
     layer_edges = len(dims) * E2
-    alg = [algorithmic(N, E2, fin, NH, F, cc) for (fin, NH, F, cc) in dims]
-    bytes_step = sum(a["b_gemm"] + a["b_edge"] for a in alg)
-    value = layer_edges * world / (elapsed / args.steps)
+    value = layer_edges * world / step_s
 
-    # per-kernel timing: HIP events on the launch stream over the instrumented timed steps
-    kern = {}
-    for phase, recs in summ.items():
-        tot = sum(t for _, t in recs)
-        kern[phase] = {"launches": len(recs), "avg_ms": tot / len(recs),
-                       "total_ms_per_step": tot / n_instr}
-    roofs = {}
-    gem = summ.get("gemm", [])
-    if gem:
-        fl = sum(2.0 * n * fin * nh * f + 4.0 * n * nh * nh * f for (n, _, fin, nh, f), _ in gem)
-        ms_ = sum(t for _, t in gem)
-        tfs = fl / (ms_ * 1e-3) / 1e12
-        gr = gemm_roof()
-        roofs["gemm"] = {"bound": "mfma", "kernel": gr["kernel"] + ", projection x.W_aug^T",
-                         "achieved": round(tfs, 2), "peak": round(gr["peak"], 1),
-                         "unit": "TFLOP/s", "frac": round(tfs / gr["peak"], 4), "traffic": None,
-                         "gemm_mode": gr["mode"], "flops_per_launch": fl / len(gem),
-                         "avg_launch_ms": ms_ / len(gem), "_prefix": gr["prefix"], "_ms": ms_}
-    edg = summ.get("edge_forward", [])
-    if edg:
-        by = 0.0
-        for info, _ in edg:
-            n, e2, nh, f, mode = info
-            if mode == "x":   # reassociated first layer: gathers x rows (f = padded F_in)
-                by += 4.0 * ((n + 1) + 2 * e2 + e2 * nh + n * nh + e2 * f + n * nh * f + n * nh)
-            else:
-                by += algorithmic(n, e2, 0, nh, f, mode)["b_edge_fwd"] - 4.0 * e2 * nh
-        ms_ = sum(t for _, t in edg)
-        gbs = by / (ms_ * 1e-3) / 1e9
-        roofs["edge_forward"] = {"bound": "hbm", "kernel": "edge_forward_kernel<*> (3 layers)",
-                                 "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                 "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
-                                 "bytes_per_launch": by / len(edg),
-                                 "avg_launch_ms": ms_ / len(edg),
-                                 "_prefix": "edge_forward_kernel", "_ms": ms_}
-    pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
-    if os.path.exists(pmc):
-        pm = json.load(open(pmc))
-        for r in roofs.values():
-            ks = [v for k, v in pm["kernels"].items() if k.startswith(r["_prefix"])]
-            if ks:
-                n = sum(v["launches"] for v in ks)
-                r["traffic"] = sum((v["hbm_read_bytes"] + v["hbm_write_bytes"]) * v["launches"]
-                                   for v in ks) / n
-                r["traffic_source"] = f"profiles/pmc_latest.json ({pm.get('source', '')})"
-    ordered = sorted(roofs.values(), key=lambda r: -r["_ms"])
-    for r in ordered:
-        r.pop("_prefix"); r.pop("_ms")
-    dominant = ordered[0] if ordered else None
-    other = ordered[1] if len(ordered) > 1 else None
+    # honest accounting: unique bytes of the dataflow actually run, priced against HBM
+    peak = gemm_roof()["peak"] * 1e12
+    flows = [layer_dataflow(N, E2, fin, nh, f, cc, cfg["add_skip_connection"][i])
+             for i, (fin, nh, f, cc) in enumerate(dims)]
+    gb = graph_build_bytes(b.num_edges, E2, N) if not args.cached_graph else 0
+    uniq = sum(bb for fl in flows for _, bb, _ in fl) + gb
+    t_roof = sum(max(bb / (HBM_PEAK_GBS * 1e9), ff / peak) for fl in flows for _, bb, ff in fl) \
+        + gb / (HBM_PEAK_GBS * 1e9)
+    surv = [survey_bytes(N, E2, fin, nh, f, cc) for (fin, nh, f, cc) in dims]
+    l2_gather = sum(bg + be for bg, _, be in surv)
+
+    def edge_unique(info):
+        n, e2, nh, f, mode = info
+        for (fin, nh_, f_, cc), fl in zip(dims, flows):
+            if nh_ == nh and (f_ == f or (mode == "x" and _r4(fin) == f)):
+                return [bb for k, bb, _ in fl if k == "edge_forward"][0]
+        raise KeyError(info)
+    pmc_path = os.path.join(ROOT, "profiles",
+                            "pmc_latest.json" if (ds == "PPI" and args.mode == "fwd"
+                                                  and args.graphs == 20) else "_none_")
+    ordered = roofline_objects(summ, edge_unique, pmc_path)
 
     result = {
         "metric": f"GAT-layer edges/sec + achieved HBM GB/s, {ds} {len(dims)}-layer fwd"
@@ -450,22 +530,22 @@ def main():
                                + (", CSR cached" if args.cached_graph else ", CSR built per step"),
                    "graphs_per_gpu": args.graphs, "nodes_per_gpu": N, "edges_per_layer": E2,
                    "parallelism": f"graph-batch dp{world}"},
-        "achieved_GBps_algorithmic_per_gpu": round(bytes_step / (elapsed / args.steps) / 1e9, 1),
-        "roofline_time_frac": round(sum(max((a["b_gemm"] + a["b_edge"]) / (HBM_PEAK_GBS * 1e9),
-                                            a["f_gemm"] / (gemm_roof()["peak"] * 1e12))
-                                        for a in alg) / (ms * 1e-3), 4),
-        "roofline": dominant,
-        "roofline_other": other,
-        "kernels": kern,
+        "unique_GBps": round(uniq / step_s / 1e9, 1),
+        "roofline_time_frac": round(t_roof / step_s, 4),
+        "roofline_time_basis": "sum over the forward's kernels of max(unique bytes / 8 TB/s, "
+                               "flops / GEMM peak) + graph build bytes / 8 TB/s, over step time",
+        "l2_gather_GBps": round(l2_gather / step_s / 1e9, 1),
+        "hbm_measured": pmc_step_bytes(pmc_path, ms) if args.mode == "fwd" else None,
+        "roofline": ordered[0] if ordered else None,
+        "roofline_other": ordered[1] if len(ordered) > 1 else None,
+        "kernels": kernel_summary(summ, n_instr),
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.mode == "fwd" and ds == "PPI":
-        model_np = {"layers": [(l.W.weight.detach().cpu().numpy(), l.a.weight.detach().cpu().numpy())
-                               for l in model.gat_layer_list],
-                    "skips": [None if isinstance(s, torch.nn.Identity) else s.weight.detach().cpu().numpy()
-                              for s in model.skip_layer_list]}
-        result["cpu_baseline"] = cpu_baseline(model_np, cfg)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.mode == "fwd":
+        result["cpu_baseline"] = cpu_baseline(model, cfg, ds, 1 if ds == "PPI" else 8)
     if rank == 0:
         print(json.dumps(result), flush=True)
+    if reducer is not None:
+        reducer.remove()
     if world > 1:
         dist.destroy_process_group()
 

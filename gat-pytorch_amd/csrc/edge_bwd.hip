@@ -126,7 +126,7 @@ struct BwdArgs {
   int64_t N, E2;
   int NH, F, Fp, const_att;
   float p_drop;
-  uint64_t seed;
+  const uint64_t* seed;    // device scalar
   const float* g_alpha_ret;
   float* g_raw;            // [NH][E2] head-major, dst-CSR order
   float* gsd;              // [N][NH] compact copy of g_s_dst (for max()'s gradient)
@@ -157,6 +157,7 @@ __global__ void __launch_bounds__(256) edge_bwd_dst_kernel(BwdArgs g) {
   const float M = ord_to_float(*g.M_ord);
   const bool drop = g.p_drop > 0.f;
   const float drop_scale = drop ? 1.f / (1.f - g.p_drop) : 1.f;
+  const uint64_t seed = drop ? *g.seed : 0ull;
   const float4* __restrict__ Wh4 = (const float4*)g.Wh;
   const float4* __restrict__ go4 = (const float4*)g.go;
 
@@ -227,7 +228,7 @@ __global__ void __launch_bounds__(256) edge_bwd_dst_kernel(BwdArgs g) {
     }
     if (valid) {
       float ga = my_dot;
-      if (drop) ga = dropout_keep(g.seed, (int64_t)g.perm[e] * NH + h, g.p_drop) ? ga * drop_scale : 0.f;
+      if (drop) ga = dropout_keep(seed, (int64_t)g.perm[e] * NH + h, g.p_drop) ? ga * drop_scale : 0.f;
       if (g.g_alpha_ret) ga += g.g_alpha_ret[(int64_t)g.perm[e] * NH + h];
       if (base == beg) {
         ga0 = ga;
@@ -343,13 +344,15 @@ __global__ void __launch_bounds__(256) max_bwd_scan_kernel(const float* __restri
                                                            const uint32_t* __restrict__ M_ord,
                                                            const int32_t* __restrict__ col,
                                                            const int32_t* __restrict__ rowidx,
-                                                           int64_t E2, int NH,
+                                                           int64_t E2b, const long long* e2p,
+                                                           int NH,
                                                            const long long* __restrict__ argmax,
                                                            const float* __restrict__ gm,
                                                            float* __restrict__ g_corr_src,
                                                            float* __restrict__ G_aug,
                                                            int64_t ldg, int64_t Dp) {
   if (argmax[0] <= GATX_ARGMAX_CAP) return;
+  const int64_t E2 = e2p ? min(E2b, (int64_t)*e2p) : E2b;
   const float M = ord_to_float(*M_ord), share = gm[0];
   const int S2 = 2 * NH;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < E2 * NH;
@@ -385,6 +388,7 @@ __global__ void __launch_bounds__(256) edge_bwd_src_kernel(BwdArgs g) {
   const float M = g.const_att ? 0.f : ord_to_float(*g.M_ord);
   const bool drop = g.p_drop > 0.f;
   const float drop_scale = drop ? 1.f / (1.f - g.p_drop) : 1.f;
+  const uint64_t seed = drop ? *g.seed : 0ull;
   const float4* __restrict__ go4 = (const float4*)g.go;
   __shared__ int src_sh[4][64];
   __shared__ float w_sh[4][64];
@@ -417,7 +421,7 @@ __global__ void __launch_bounds__(256) edge_bwd_src_kernel(BwdArgs g) {
     if (valid) {
       const float ex = g.const_att ? 1.f : att_exp(ssrc + g.S[(int64_t)d * S2 + NH + h], M);
       w = ex / (g.den[(int64_t)d * NH + h] + kSoftmaxEps);
-      if (drop) w = dropout_keep(g.seed, (int64_t)g.perm[e] * NH + h, g.p_drop) ? w * drop_scale : 0.f;
+      if (drop) w = dropout_keep(seed, (int64_t)g.perm[e] * NH + h, g.p_drop) ? w * drop_scale : 0.f;
       if (graw) gs += graw[e];
     }
     if (EPW > 1) {
@@ -504,6 +508,7 @@ __global__ void __launch_bounds__(256) edge_bwd_src_mean_kernel(BwdArgs g) {
   const float M = g.const_att ? 0.f : ord_to_float(*g.M_ord);
   const bool drop = g.p_drop > 0.f;
   const float drop_scale = drop ? 1.f / (1.f - g.p_drop) : 1.f;
+  const uint64_t seed = drop ? *g.seed : 0ull;
   const float4* __restrict__ go4 = (const float4*)g.go;
   __shared__ int src_sh[4][64];
   __shared__ float w_sh[4][NHM][64];
@@ -542,7 +547,7 @@ __global__ void __launch_bounds__(256) edge_bwd_src_mean_kernel(BwdArgs g) {
       if (valid) {
         const float ex = g.const_att ? 1.f : att_exp(ssrc[h] + g.S[(int64_t)d * S2 + NH + h], M);
         w = ex / (g.den[(int64_t)d * NH + h] + kSoftmaxEps);
-        if (drop) w = dropout_keep(g.seed, ep * NH + h, g.p_drop) ? w * drop_scale : 0.f;
+        if (drop) w = dropout_keep(seed, ep * NH + h, g.p_drop) ? w * drop_scale : 0.f;
         if (graw) gs[h] += graw[(int64_t)h * E2 + e];
       }
       w_lds[h][lane] = w;
@@ -741,7 +746,7 @@ extern "C" int gatx_edge_backward_dst_ex(const float* rows, int64_t row_stride,
                                          const int32_t* rowptr, const int32_t* col,
                                          const int32_t* perm, int64_t N, int64_t E2, int NH, int F,
                                          const float* go, int64_t go_stride, int64_t go_head,
-                                         float p, uint64_t seed, const float* g_alpha,
+                                         float p, const uint64_t* seed, const float* g_alpha,
                                          float* g_raw, float* gsd, float* G, int64_t ldg,
                                          int64_t gs_off, gatx_stream_t s) {
   hipStream_t st = (hipStream_t)s;
@@ -774,7 +779,7 @@ extern "C" int gatx_edge_backward_dst(const float* Wh, const float* S, const uin
                                       const float* den, const int32_t* rowptr,
                                       const int32_t* col, const int32_t* perm, int64_t N,
                                       int64_t E2, int NH, int F, int concat, float p,
-                                      uint64_t seed, const float* go, const float* g_alpha,
+                                      const uint64_t* seed, const float* go, const float* g_alpha,
                                       float* g_raw, float* gsd, float* G_aug, int64_t ldg,
                                       gatx_stream_t s) {
   const int64_t Fp = round_up(F, 4), Dp = NH * Fp;
@@ -808,8 +813,9 @@ extern "C" size_t gatx_max_backward_workspace_bytes(void) {
 
 extern "C" int gatx_max_backward(const int64_t* argmax, const float* gsd, const float* S,
                                  const uint32_t* M_ord, const int32_t* col, const int32_t* rowidx,
-                                 int64_t N, int64_t E2, int NH, float* g_corr_src, float* G_aug,
-                                 int64_t ldg, int64_t Dp, void* workspace, gatx_stream_t s) {
+                                 int64_t N, int64_t E2, const int64_t* e2, int NH,
+                                 float* g_corr_src, float* G_aug, int64_t ldg, int64_t Dp,
+                                 void* workspace, gatx_stream_t s) {
   hipStream_t st = (hipStream_t)s;
   // the g_M share is parked right after the argmax records (the buffer holds CAP + 2 int64s)
   float* gm = (float*)(argmax + 1 + GATX_ARGMAX_CAP);
@@ -821,7 +827,8 @@ extern "C" int gatx_max_backward(const int64_t* argmax, const float* gsd, const 
                                     g_corr_src, G_aug, ldg, Dp, gm);
   GATX_LAUNCH_CHECK("max_bwd");
   max_bwd_scan_kernel<<<grid_for(E2 * NH, 256, 4096), 256, 0, st>>>(
-      S, M_ord, col, rowidx, E2, NH, (const long long*)argmax, gm, g_corr_src, G_aug, ldg, Dp);
+      S, M_ord, col, rowidx, E2, (const long long*)e2, NH, (const long long*)argmax, gm,
+      g_corr_src, G_aug, ldg, Dp);
   GATX_LAUNCH_CHECK("max_bwd_scan");
   return 0;
 }
@@ -830,7 +837,7 @@ extern "C" int gatx_edge_backward_src(const float* S, const uint32_t* M_ord, con
                                       const int32_t* srowptr, const int32_t* scol,
                                       const int32_t* seid, const int32_t* perm, int64_t N,
                                       int64_t E2, int NH, int F, int concat, int const_att,
-                                      float p, uint64_t seed, const float* go,
+                                      float p, const uint64_t* seed, const float* go,
                                       const float* g_raw, const float* g_corr_src, float* G_aug,
                                       int64_t ldg, gatx_stream_t s) {
   hipStream_t st = (hipStream_t)s;

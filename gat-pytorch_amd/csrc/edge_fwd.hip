@@ -25,10 +25,11 @@ constexpr int kMaxBlocks = 2048;
 
 __global__ void __launch_bounds__(256) attention_max_kernel(const int32_t* __restrict__ col,
                                                             const int32_t* __restrict__ rowidx,
-                                                            int64_t E2,
+                                                            int64_t E2b, const long long* e2p,
                                                             const float* __restrict__ S, int NH,
                                                             float* __restrict__ part) {
   const int S2 = 2 * NH;
+  const int64_t E2 = e2p ? min(E2b, (int64_t)*e2p) : E2b;
   float m = -INFINITY;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E2;
        e += (int64_t)gridDim.x * blockDim.x) {
@@ -50,10 +51,11 @@ __global__ void __launch_bounds__(256) attention_max_kernel(const int32_t* __res
 template <int NHC>
 __global__ void __launch_bounds__(256) attention_max_vec_kernel(const int32_t* __restrict__ col,
                                                                 const int32_t* __restrict__ rowidx,
-                                                                int64_t E2,
+                                                                int64_t E2b, const long long* e2p,
                                                                 const float* __restrict__ S,
                                                                 float* __restrict__ part) {
   constexpr int S2 = 2 * NHC, UE = 4;
+  const int64_t E2 = e2p ? min(E2b, (int64_t)*e2p) : E2b;
   constexpr int VEC = (NHC % 4 == 0) ? 4 : ((NHC % 2 == 0) ? 2 : 1);
   float m = -INFINITY;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -127,7 +129,7 @@ struct EdgeFwdArgs {
   int concat, const_att;
   const float* bias;
   float p_drop;
-  uint64_t seed;
+  const uint64_t* seed;     // device scalar (torch's generator; graph-capturable)
   float* out;
   int64_t out_ld;
   const float* resid;      // fused epilogue: out = elu?(agg + bias + resid)
@@ -201,6 +203,7 @@ __global__ void __launch_bounds__(256) edge_forward_kernel(EdgeFwdArgs g) {
   const float M = g.const_att ? 0.f : ord_to_float(*g.M_ord);
   const bool drop = g.p_drop > 0.f;
   const float drop_scale = drop ? 1.f / (1.f - g.p_drop) : 1.f;
+  const uint64_t seed = drop ? *g.seed : 0ull;
   const float4* __restrict__ rows4 = (const float4*)g.rows;
   const float* __restrict__ S = g.S;
   const int32_t* __restrict__ col = g.col;
@@ -247,7 +250,7 @@ __global__ void __launch_bounds__(256) edge_forward_kernel(EdgeFwdArgs g) {
           ex = valid ? ex : 0.f;
           dnl[h] += ex;
           float w = ex;
-          if (drop) w = dropout_keep(g.seed, ep * NH + h0 + h, g.p_drop) ? ex * drop_scale : 0.f;
+          if (drop) w = dropout_keep(seed, ep * NH + h0 + h, g.p_drop) ? ex * drop_scale : 0.f;
           if (h == 0) my_w0 = w;
           if (!SCALAR_W) w_lds[h * 64 + lane] = w;
         }
@@ -646,10 +649,13 @@ __global__ void __launch_bounds__(256) attention_alpha_kernel(
 // recorded by CSR slot as above, found by a scan of dst's segment (ties are rare).
 template <int NHC, typename I>
 __global__ void __launch_bounds__(256) attention_alpha_ei_kernel(
-    const I* __restrict__ ei, int64_t ld, int64_t E2, const float* __restrict__ S,
+    const I* __restrict__ ei, int64_t ld_, int64_t E2b, const long long* e2p,
+    const float* __restrict__ S,
     const uint32_t* __restrict__ M_ord, const float* __restrict__ den, int NH_rt, int const_att,
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ perm,
     float* __restrict__ alpha, long long* __restrict__ argmax) {
+  const int64_t E2 = e2p ? min(E2b, (int64_t)*e2p) : E2b;
+  const int64_t ld = ld_ < 0 ? E2 : ld_;   // flat edge_index' of device-known size
   constexpr int VEC = (NHC % 4 == 0) ? 4 : ((NHC % 2 == 0) ? 2 : 1);
   constexpr int UE = NHC > 0 ? 4 : 1;   // edges per thread per round, all loads issued first
   constexpr int NHA = NHC > 0 ? NHC : 1;
@@ -830,17 +836,19 @@ extern "C" int gatx_attention_alpha(const int32_t* col, const int32_t* rowidx,
 }
 
 extern "C" int gatx_attention_alpha_ei(const void* edge_index, int is64, int64_t ld, int64_t E2,
-                                       const float* S, const uint32_t* M_ord, const float* den,
-                                       int NH, int const_att, const int32_t* rowptr,
-                                       const int32_t* perm, float* alpha, int64_t* argmax,
-                                       gatx_stream_t s) {
+                                       const int64_t* e2, const float* S, const uint32_t* M_ord,
+                                       const float* den, int NH, int const_att,
+                                       const int32_t* rowptr, const int32_t* perm, float* alpha,
+                                       int64_t* argmax, gatx_stream_t s) {
   if (E2 == 0) return 0;
+  GATX_REQUIRE(ld >= 0 || e2 != nullptr, "attention_alpha_ei: ld < 0 needs the device count");
   hipStream_t st = (hipStream_t)s;
   const unsigned grid = grid_for(ceil_div(E2, 4), 256, 8192);   // 4 edges per thread
+  const long long* e2p = (const long long*)e2;
 #define GATX_AE(C, I)                                                                          \
-  attention_alpha_ei_kernel<C, I><<<grid, 256, 0, st>>>((const I*)edge_index, ld, E2, S, M_ord, \
-                                                        den, NH, const_att, rowptr, perm, alpha, \
-                                                        (long long*)argmax)
+  attention_alpha_ei_kernel<C, I><<<grid, 256, 0, st>>>((const I*)edge_index, ld, E2, e2p, S,  \
+                                                        M_ord, den, NH, const_att, rowptr,     \
+                                                        perm, alpha, (long long*)argmax)
 #define GATX_AEI(I)                                                                            \
   switch (NH) {                                                                                \
     case 1: GATX_AE(1, I); break; case 2: GATX_AE(2, I); break; case 4: GATX_AE(4, I); break;  \
@@ -864,19 +872,20 @@ extern "C" int gatx_pad_rows(const float* src, int64_t rows, int64_t cols, int64
 }
 
 extern "C" int gatx_attention_max(const int32_t* col, const int32_t* rowidx, int64_t E2,
-                                  const float* S, int NH, uint32_t* M_ord, int64_t* argmax,
-                                  void* workspace, gatx_stream_t s) {
+                                  const int64_t* e2, const float* S, int NH, uint32_t* M_ord,
+                                  int64_t* argmax, void* workspace, gatx_stream_t s) {
   hipStream_t st = (hipStream_t)s;
   const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(E2, 256), kMaxBlocks));
   float* part = (float*)workspace;
+  const long long* e2p = (const long long*)e2;
   // S rows are float4/float2-aligned when 2*NH is a multiple of the vector width
   const bool al = ((uintptr_t)S % 16) == 0;
-  if (E2 > 0 && al && NH == 4) attention_max_vec_kernel<4><<<nb, 256, 0, st>>>(col, rowidx, E2, S, part);
-  else if (E2 > 0 && al && NH == 8) attention_max_vec_kernel<8><<<nb, 256, 0, st>>>(col, rowidx, E2, S, part);
-  else if (E2 > 0 && al && NH == 6) attention_max_vec_kernel<6><<<nb, 256, 0, st>>>(col, rowidx, E2, S, part);
-  else if (E2 > 0 && al && NH == 2) attention_max_vec_kernel<2><<<nb, 256, 0, st>>>(col, rowidx, E2, S, part);
-  else if (E2 > 0 && NH == 1) attention_max_vec_kernel<1><<<nb, 256, 0, st>>>(col, rowidx, E2, S, part);
-  else attention_max_kernel<<<nb, 256, 0, st>>>(col, rowidx, E2, S, NH, part);
+  if (E2 > 0 && al && NH == 4) attention_max_vec_kernel<4><<<nb, 256, 0, st>>>(col, rowidx, E2, e2p, S, part);
+  else if (E2 > 0 && al && NH == 8) attention_max_vec_kernel<8><<<nb, 256, 0, st>>>(col, rowidx, E2, e2p, S, part);
+  else if (E2 > 0 && al && NH == 6) attention_max_vec_kernel<6><<<nb, 256, 0, st>>>(col, rowidx, E2, e2p, S, part);
+  else if (E2 > 0 && al && NH == 2) attention_max_vec_kernel<2><<<nb, 256, 0, st>>>(col, rowidx, E2, e2p, S, part);
+  else if (E2 > 0 && NH == 1) attention_max_vec_kernel<1><<<nb, 256, 0, st>>>(col, rowidx, E2, e2p, S, part);
+  else attention_max_kernel<<<nb, 256, 0, st>>>(col, rowidx, E2, e2p, S, NH, part);
   GATX_LAUNCH_CHECK("attention_max");
   max_final_kernel<<<1, 256, 0, st>>>(part, nb, M_ord, (long long*)argmax);
   GATX_LAUNCH_CHECK("attention_max_final");
@@ -889,7 +898,7 @@ extern "C" int gatx_edge_forward_ex(
     const float* rows, int64_t row_stride, int64_t head_stride, const float* S,
     const uint32_t* M_ord, const int32_t* rowptr, const int32_t* col, const int32_t* perm,
     int64_t N, int NH, int F, int heads_per_item, int concat, int const_att, const float* bias,
-    float p, uint64_t seed, float* out, int64_t out_ld, const float* resid, int64_t resid_ld,
+    float p, const uint64_t* seed, float* out, int64_t out_ld, const float* resid, int64_t resid_ld,
     int elu, float* den, int64_t chunk, gatx_stream_t s) {
   hipStream_t st = (hipStream_t)s;
   GATX_REQUIRE(NH >= 1 && F >= 1, "edge_forward: bad sizes");
@@ -901,6 +910,7 @@ extern "C" int gatx_edge_forward_ex(
   GATX_REQUIRE(row_stride % 4 == 0 && head_stride % 4 == 0 && ((uintptr_t)rows % 16) == 0,
                "edge_forward: source rows must be float4-aligned");
   GATX_REQUIRE(p >= 0.f && p < 1.f, "edge_forward: dropout must be in [0, 1)");
+  GATX_REQUIRE(p == 0.f || seed != nullptr, "edge_forward: dropout needs the device seed");
   if (N == 0) return 0;
   const int Fp = (int)round_up(F, 4);
   const int64_t D4 = (int64_t)HS * Fp / 4;
@@ -946,7 +956,7 @@ extern "C" int gatx_edge_forward(const float* Wh, const float* S, const uint32_t
                                  const int32_t* rowidx, const int32_t* perm, int64_t N,
                                  int64_t E2, int NH, int F, int concat, int const_att,
                                  const float* bias, float p,
-                                 uint64_t seed, float* out, float* alpha, float* den,
+                                 const uint64_t* seed, float* out, float* alpha, float* den,
                                  int64_t* argmax, gatx_stream_t s) {
   const int64_t Fp = round_up(F, 4);
   GATX_CALL(gatx_edge_forward_ex(Wh, NH * Fp, Fp, S, M_ord, rowptr, col, perm, N, NH, F,

@@ -5,6 +5,11 @@
 // (prefix sum over the keep flags), a stable LSD radix sort by destination (rocPRIM), and
 // boundary detection for rowptr. All orders are deterministic, so CSR segments list their
 // edges in edge_index' order and per-segment float sums are bitwise reproducible.
+//
+// No host sync: |edge_index'| = E - #self-loops + max id + 1 is only known on the device, so
+// the host allocates for the bound E + num_nodes and the kernels take the exact size from the
+// device-side meta record (gatx_graph_meta). Padding slots past E' sort after every real slot
+// (key = num_nodes) and rowptr[num_nodes] = E', so nothing that walks the CSR ever sees them.
 #include <cstring>
 
 #include <rocprim/rocprim.hpp>
@@ -21,7 +26,7 @@ __device__ inline int64_t ld_idx(const void* p, int64_t i) {
 
 constexpr int kStatsBlocks = 1024;
 
-// Per-block {min, max, self-loops} partials (no 64-bit atomics), reduced by stats_final_kernel.
+// Per-block {min, max, self-loops} partials (no 64-bit atomics), reduced by graph_meta_kernel.
 template <typename I>
 __global__ void __launch_bounds__(256) edge_stats_kernel(const void* ei, int64_t E, int64_t ld,
                                                          long long* part) {
@@ -52,8 +57,13 @@ __global__ void __launch_bounds__(256) edge_stats_kernel(const void* ei, int64_t
   }
 }
 
-__global__ void __launch_bounds__(256) stats_final_kernel(const long long* part, int nb,
-                                                          long long* stats) {
+// Device-side sizing of the rewrite from the stats partials: meta = {E2, num_loops, status, min,
+// max, n_selfloops, 0, 0}. status 1 / 2 (a negative id / an id >= num_nodes) zeroes E2 and
+// num_loops, so every later kernel sees an empty graph and nothing indexes out of bounds; the
+// host raises when it reads the meta (the reference raises in index_select / scatter_add_).
+__global__ void __launch_bounds__(256) graph_meta_kernel(const long long* part, int nb, int64_t E,
+                                                         int add_loops, int64_t num_nodes,
+                                                         long long* meta) {
   long long mn = LLONG_MAX, mx = LLONG_MIN, loops = 0;
   for (int b = threadIdx.x; b < nb; b += blockDim.x) {
     mn = min(mn, part[3 * b]); mx = max(mx, part[3 * b + 1]); loops += part[3 * b + 2];
@@ -71,7 +81,15 @@ __global__ void __launch_bounds__(256) stats_final_kernel(const long long* part,
     for (int k = 1; k < (int)(blockDim.x >> 6); ++k) {
       mn = min(mn, red[0][k]); mx = max(mx, red[1][k]); loops += red[2][k];
     }
-    stats[0] = mn; stats[1] = mx; stats[2] = loops;
+    long long status = 0;
+    if (E > 0 && mn < 0) status = 1;
+    else if (E > 0 && mx >= num_nodes) status = 2;
+    long long num_loops = (add_loops && E > 0) ? mx + 1 : 0;
+    long long e2 = add_loops ? E - loops + num_loops : E;
+    if (status) { e2 = 0; num_loops = 0; }
+    meta[0] = e2; meta[1] = num_loops; meta[2] = status;
+    meta[3] = E > 0 ? mn : 0; meta[4] = E > 0 ? mx : -1; meta[5] = loops;
+    meta[6] = 0; meta[7] = 0;
   }
 }
 
@@ -86,30 +104,58 @@ struct KeepFlag {
   }
 };
 
-// Scatter kept edges to their compacted slot, append the loops (i, i), i < num_loops.
+// One thread per input edge t < E, then one per slot q = t - E < E_bound:
+//  * input edge t: if it survives, (src, dst) goes to slot pos[t] (its rank among survivors);
+//  * slot q in [E2 - num_loops, E2): the loop (i, i), i = q - (E2 - num_loops);
+//  * slot q >= E2 (padding up to the allocation bound): sorts after every real key (dst = N).
+// edge_index' is written flat with its exact size: sources at [p], destinations at [E2 + p],
+// so edge_index'[:2*E2].view(2, E2) is the reference's contiguous (2, E') tensor.
 template <typename I>
 __global__ void __launch_bounds__(256) compact_kernel(const void* ei, int64_t E, int64_t ld,
                                                        int drop_loops, const int32_t* pos,
-                                                       int64_t num_loops, int64_t E2,
-                                                       int64_t* ei_out, int32_t* src32,
-                                                       int32_t* dst32, int32_t* iota) {
-  const int64_t total = E + num_loops;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
+                                                       const long long* meta, int64_t E_bound,
+                                                       int64_t num_nodes, int64_t* ei_out,
+                                                       int32_t* src32, int32_t* dst32,
+                                                       int32_t* iota) {
+  const int64_t E2 = meta[0], num_loops = meta[1];
+  const bool ok = meta[2] == 0;
+  const int64_t total = E + E_bound;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
     int64_t s, d, p;
-    if (i < E) {
-      s = ld_idx<I>(ei, i);
-      d = ld_idx<I>(ei, ld + i);
+    if (t < E) {
+      if (!ok) continue;
+      s = ld_idx<I>(ei, t);
+      d = ld_idx<I>(ei, ld + t);
       if (drop_loops && s == d) continue;
-      p = pos[i];
+      p = drop_loops ? pos[t] : t;
     } else {
-      s = d = i - E;
-      p = E2 - num_loops + (i - E);
+      p = t - E;
+      if (p >= E2) {   // padding slot
+        src32[p] = 0;
+        dst32[p] = (int32_t)num_nodes;
+        iota[p] = (int32_t)p;
+        continue;
+      }
+      if (p < E2 - num_loops) continue;   // a surviving input edge's slot
+      s = d = p - (E2 - num_loops);
     }
     if (ei_out) { ei_out[p] = s; ei_out[E2 + p] = d; }
     src32[p] = (int32_t)s;
     dst32[p] = (int32_t)d;
     iota[p] = (int32_t)p;
+  }
+}
+
+// transpose sort keys: the source id of each dst-CSR slot, N for the padding slots
+__global__ void __launch_bounds__(256) tkeys_kernel(const int32_t* col, const long long* e2p,
+                                                    int64_t E_bound, int64_t num_nodes,
+                                                    int32_t* keys, int32_t* iota) {
+  const int64_t E2 = *e2p;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E_bound;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    keys[e] = e < E2 ? col[e] : (int32_t)num_nodes;
+    iota[e] = (int32_t)e;
   }
 }
 
@@ -159,7 +205,7 @@ size_t scan_bytes(int64_t E) {
   return bytes;
 }
 
-size_t sort_bytes(int64_t n, unsigned bits) {
+size_t sort_bytes(int64_t n, unsigned bits) {  // bits: key range [0, 2^bits)
   size_t bytes = 0;
   (void)rocprim::radix_sort_pairs(nullptr, bytes, (int32_t*)nullptr, (int32_t*)nullptr,
                             (int32_t*)nullptr, (int32_t*)nullptr, (unsigned)(n > 0 ? n : 1), 0,
@@ -168,16 +214,16 @@ size_t sort_bytes(int64_t n, unsigned bits) {
 }
 
 template <typename I>
-int graph_build_impl(const void* ei, int64_t E, int64_t ld, int add_loops, int64_t num_loops,
-                     int64_t N, int64_t E2, int64_t* ei_out, int32_t* rowptr, int32_t* col,
-                     int32_t* rowidx, int32_t* perm, void* ws, size_t ws_bytes,
+int graph_build_impl(const void* ei, int64_t E, int64_t ld, int add_loops, int64_t N,
+                     int64_t E_bound, const long long* meta, int64_t* ei_out, int32_t* rowptr,
+                     int32_t* col, int32_t* rowidx, int32_t* perm, void* ws, size_t ws_bytes,
                      hipStream_t stream) {
-  // workspace carve: pos [E] | src32 [E2] | dst32 [E2] | iota [E2] | rocprim temp
+  // workspace carve: pos [E] | src32 [Eb] | dst32 [Eb] | iota [Eb] | rocprim temp
   char* p = (char*)ws;
   int32_t* pos = (int32_t*)p;   p += align256(sizeof(int32_t) * (E > 0 ? E : 1));
-  int32_t* src32 = (int32_t*)p; p += align256(sizeof(int32_t) * (E2 > 0 ? E2 : 1));
-  int32_t* dst32 = (int32_t*)p; p += align256(sizeof(int32_t) * (E2 > 0 ? E2 : 1));
-  int32_t* iota = (int32_t*)p;  p += align256(sizeof(int32_t) * (E2 > 0 ? E2 : 1));
+  int32_t* src32 = (int32_t*)p; p += align256(sizeof(int32_t) * (E_bound > 0 ? E_bound : 1));
+  int32_t* dst32 = (int32_t*)p; p += align256(sizeof(int32_t) * (E_bound > 0 ? E_bound : 1));
+  int32_t* iota = (int32_t*)p;  p += align256(sizeof(int32_t) * (E_bound > 0 ? E_bound : 1));
   size_t used = (size_t)(p - (char*)ws);
   GATX_REQUIRE(used <= ws_bytes, "graph_build: workspace too small");
   void* tmp = p;
@@ -190,24 +236,21 @@ int graph_build_impl(const void* ei, int64_t E, int64_t ld, int add_loops, int64
     hipError_t r = rocprim::exclusive_scan(tmp, b, it, pos, 0, (size_t)E,
                                            rocprim::plus<int32_t>(), stream);
     if (r != hipSuccess) { set_error("exclusive_scan: %s", hipGetErrorString(r)); return (int)r; }
-  } else if (E > 0) {
-    iota_kernel<<<grid_for(E), 256, 0, stream>>>(E, pos);
-    GATX_LAUNCH_CHECK("iota");
   }
-  if (E + (add_loops ? num_loops : 0) > 0) {
-    compact_kernel<I><<<grid_for(E + num_loops), 256, 0, stream>>>(
-        ei, E, ld, add_loops, pos, add_loops ? num_loops : 0, E2, ei_out, src32, dst32, iota);
+  if (E + E_bound > 0) {
+    compact_kernel<I><<<grid_for(E + E_bound), 256, 0, stream>>>(
+        ei, E, ld, add_loops, pos, meta, E_bound, N, ei_out, src32, dst32, iota);
     GATX_LAUNCH_CHECK("compact");
   }
-  if (E2 > 0) {
+  if (E_bound > 0) {
     size_t b = tmp_bytes;
-    hipError_t r = rocprim::radix_sort_pairs(tmp, b, dst32, rowidx, iota, perm, (unsigned)E2, 0,
-                                             bits_for(N), stream);
+    hipError_t r = rocprim::radix_sort_pairs(tmp, b, dst32, rowidx, iota, perm,
+                                             (unsigned)E_bound, 0, bits_for(N + 1), stream);
     if (r != hipSuccess) { set_error("radix_sort: %s", hipGetErrorString(r)); return (int)r; }
-    gather_kernel<<<grid_for(E2), 256, 0, stream>>>(src32, perm, E2, col);
+    gather_kernel<<<grid_for(E_bound), 256, 0, stream>>>(src32, perm, E_bound, col);
     GATX_LAUNCH_CHECK("gather col");
   }
-  rowptr_kernel<<<grid_for(E2 + 1), 256, 0, stream>>>(rowidx, E2, N, rowptr);
+  rowptr_kernel<<<grid_for(E_bound + 1), 256, 0, stream>>>(rowidx, E_bound, N, rowptr);
   GATX_LAUNCH_CHECK("rowptr");
   return 0;
 }
@@ -217,8 +260,14 @@ int graph_build_impl(const void* ei, int64_t E, int64_t ld, int add_loops, int64
 
 using namespace gatx;
 
-extern "C" int gatx_edge_stats(const void* edge_index, int is64, int64_t E, int64_t ld,
-                               int64_t* stats, void* workspace, gatx_stream_t s) {
+extern "C" size_t gatx_graph_meta_workspace_bytes(void) {
+  return (size_t)3 * sizeof(long long) * kStatsBlocks;
+}
+
+extern "C" int gatx_graph_meta(const void* edge_index, int is64, int64_t E, int64_t ld,
+                               int add_self_loops, int64_t num_nodes, int64_t* meta,
+                               void* workspace, gatx_stream_t s) {
+  GATX_REQUIRE(E >= 0 && num_nodes >= 0, "graph_meta: negative size");
   hipStream_t stream = (hipStream_t)s;
   const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(E, 256), kStatsBlocks));
   long long* part = (long long*)workspace;
@@ -227,65 +276,67 @@ extern "C" int gatx_edge_stats(const void* edge_index, int is64, int64_t E, int6
   else
     edge_stats_kernel<int32_t><<<nb, 256, 0, stream>>>(edge_index, E, ld, part);
   GATX_LAUNCH_CHECK("edge_stats");
-  stats_final_kernel<<<1, 256, 0, stream>>>(part, nb, (long long*)stats);
-  GATX_LAUNCH_CHECK("edge_stats_final");
+  graph_meta_kernel<<<1, 256, 0, stream>>>(part, nb, E, add_self_loops, num_nodes,
+                                           (long long*)meta);
+  GATX_LAUNCH_CHECK("graph_meta");
   return 0;
 }
 
-extern "C" size_t gatx_edge_stats_workspace_bytes(void) {
-  return (size_t)3 * sizeof(long long) * kStatsBlocks;
-}
-
-extern "C" size_t gatx_graph_build_workspace_bytes(int64_t E, int64_t E2, int64_t N) {
+extern "C" size_t gatx_graph_build_workspace_bytes(int64_t E, int64_t E_bound, int64_t N) {
   size_t b = align256(sizeof(int32_t) * (E > 0 ? E : 1)) +
-             3 * align256(sizeof(int32_t) * (E2 > 0 ? E2 : 1));
-  size_t t = std::max(scan_bytes(E), sort_bytes(E2, bits_for(N)));
+             3 * align256(sizeof(int32_t) * (E_bound > 0 ? E_bound : 1));
+  size_t t = std::max(scan_bytes(E), sort_bytes(E_bound, bits_for(N + 1)));
   return b + align256(t) + 256;
 }
 
 extern "C" int gatx_graph_build(const void* edge_index, int is64, int64_t E, int64_t ld,
-                                int add_self_loops, int64_t num_loops, int64_t num_nodes,
-                                int64_t E2, int64_t* edge_index_out, int32_t* rowptr,
+                                int add_self_loops, int64_t num_nodes, int64_t E_bound,
+                                const int64_t* meta, int64_t* edge_index_out, int32_t* rowptr,
                                 int32_t* col, int32_t* rowidx, int32_t* perm, void* ws,
                                 size_t ws_bytes, gatx_stream_t s) {
-  GATX_REQUIRE(num_nodes >= 0 && num_nodes < INT32_MAX && E2 < INT32_MAX && E >= 0,
+  GATX_REQUIRE(num_nodes >= 0 && num_nodes < INT32_MAX && E_bound < INT32_MAX && E >= 0,
                "graph_build: sizes out of int32 range");
-  GATX_REQUIRE(add_self_loops || E2 == E,
-               "graph_build: E2 must equal E without self-loop rewrite");
+  GATX_REQUIRE(E_bound >= (add_self_loops ? E + num_nodes : E),
+               "graph_build: E_bound below E (+ num_nodes with self-loops)");
   if (is64)
-    return graph_build_impl<int64_t>(edge_index, E, ld, add_self_loops, num_loops, num_nodes, E2,
-                                     edge_index_out, rowptr, col, rowidx, perm, ws, ws_bytes,
-                                     (hipStream_t)s);
-  return graph_build_impl<int32_t>(edge_index, E, ld, add_self_loops, num_loops, num_nodes, E2,
-                                   edge_index_out, rowptr, col, rowidx, perm, ws, ws_bytes,
-                                   (hipStream_t)s);
+    return graph_build_impl<int64_t>(edge_index, E, ld, add_self_loops, num_nodes, E_bound,
+                                     (const long long*)meta, edge_index_out, rowptr, col, rowidx,
+                                     perm, ws, ws_bytes, (hipStream_t)s);
+  return graph_build_impl<int32_t>(edge_index, E, ld, add_self_loops, num_nodes, E_bound,
+                                   (const long long*)meta, edge_index_out, rowptr, col, rowidx,
+                                   perm, ws, ws_bytes, (hipStream_t)s);
 }
 
-extern "C" size_t gatx_graph_transpose_workspace_bytes(int64_t E2, int64_t N) {
-  return 2 * align256(sizeof(int32_t) * (E2 > 0 ? E2 : 1)) + align256(sort_bytes(E2, bits_for(N))) +
-         256;
+extern "C" size_t gatx_graph_transpose_workspace_bytes(int64_t E_bound, int64_t N) {
+  return 2 * align256(sizeof(int32_t) * (E_bound > 0 ? E_bound : 1)) +
+         align256(sort_bytes(E_bound, bits_for(N + 1))) + 256;
 }
 
 extern "C" int gatx_graph_transpose(const int32_t* col, const int32_t* rowidx, int64_t N,
-                                    int64_t E2, int32_t* srowptr, int32_t* scol, int32_t* seid,
-                                    void* ws, size_t ws_bytes, gatx_stream_t s) {
+                                    int64_t E_bound, const int64_t* e2, int32_t* srowptr,
+                                    int32_t* scol, int32_t* seid, void* ws, size_t ws_bytes,
+                                    gatx_stream_t s) {
   hipStream_t stream = (hipStream_t)s;
   char* p = (char*)ws;
-  int32_t* iota = (int32_t*)p;  p += align256(sizeof(int32_t) * (E2 > 0 ? E2 : 1));
-  int32_t* skeys = (int32_t*)p; p += align256(sizeof(int32_t) * (E2 > 0 ? E2 : 1));
+  int32_t* iota = (int32_t*)p;  p += align256(sizeof(int32_t) * (E_bound > 0 ? E_bound : 1));
+  int32_t* keys = (int32_t*)p;  p += align256(sizeof(int32_t) * (E_bound > 0 ? E_bound : 1));
   size_t used = (size_t)(p - (char*)ws);
   GATX_REQUIRE(used <= ws_bytes, "graph_transpose: workspace too small");
-  if (E2 > 0) {
-    iota_kernel<<<grid_for(E2), 256, 0, stream>>>(E2, iota);
-    GATX_LAUNCH_CHECK("iota");
+  int32_t* skeys = scol;   // sorted keys land in scol first, then scol is gathered over them
+  if (E_bound > 0) {
+    tkeys_kernel<<<grid_for(E_bound), 256, 0, stream>>>(col, (const long long*)e2, E_bound, N,
+                                                        keys, iota);
+    GATX_LAUNCH_CHECK("tkeys");
     size_t b = ws_bytes - used;
-    hipError_t r = rocprim::radix_sort_pairs((void*)p, b, col, skeys, iota, seid, (unsigned)E2, 0,
-                                             bits_for(N), stream);
+    hipError_t r = rocprim::radix_sort_pairs((void*)p, b, keys, skeys, iota, seid,
+                                             (unsigned)E_bound, 0, bits_for(N + 1), stream);
     if (r != hipSuccess) { set_error("radix_sort: %s", hipGetErrorString(r)); return (int)r; }
-    gather_kernel<<<grid_for(E2), 256, 0, stream>>>(rowidx, seid, E2, scol);
+  }
+  rowptr_kernel<<<grid_for(E_bound + 1), 256, 0, stream>>>(skeys, E_bound, N, srowptr);
+  GATX_LAUNCH_CHECK("srowptr");
+  if (E_bound > 0) {
+    gather_kernel<<<grid_for(E_bound), 256, 0, stream>>>(rowidx, seid, E_bound, scol);
     GATX_LAUNCH_CHECK("gather scol");
   }
-  rowptr_kernel<<<grid_for(E2 + 1), 256, 0, stream>>>(skeys, E2, N, srowptr);
-  GATX_LAUNCH_CHECK("srowptr");
   return 0;
 }

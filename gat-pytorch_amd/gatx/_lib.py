@@ -28,13 +28,13 @@ P = ctypes.c_void_p
 SIGNATURES = {
     "gatx_last_error": (ctypes.c_char_p, []),
     "gatx_version": (c_i, []),
-    "gatx_edge_stats_workspace_bytes": (c_sz, []),
-    "gatx_edge_stats": (c_i, [P, c_i, c_i64, c_i64, P, P, P]),
+    "gatx_graph_meta_workspace_bytes": (c_sz, []),
+    "gatx_graph_meta": (c_i, [P, c_i, c_i64, c_i64, c_i, c_i64, P, P, P]),
     "gatx_graph_build_workspace_bytes": (c_sz, [c_i64, c_i64, c_i64]),
-    "gatx_graph_build": (c_i, [P, c_i, c_i64, c_i64, c_i, c_i64, c_i64, c_i64, P, P, P, P, P, P,
+    "gatx_graph_build": (c_i, [P, c_i, c_i64, c_i64, c_i, c_i64, c_i64, P, P, P, P, P, P, P,
                                c_sz, P]),
     "gatx_graph_transpose_workspace_bytes": (c_sz, [c_i64, c_i64]),
-    "gatx_graph_transpose": (c_i, [P, P, c_i64, c_i64, P, P, P, P, c_sz, P]),
+    "gatx_graph_transpose": (c_i, [P, P, c_i64, c_i64, P, P, P, P, P, c_sz, P]),
     "gatx_prepare_weights": (c_i, [P, P, c_i, c_i, c_i64, P, P]),
     "gatx_prepare_weights_floats": (c_i64, [c_i, c_i, c_i64, c_i]),
     "gatx_gemm_f32": (c_i, [c_i64, c_i64, c_i64, P, c_i64, c_i64, P, c_i64, c_i64, P, c_i64,
@@ -45,7 +45,7 @@ SIGNATURES = {
                                     c_i64, c_i64, c_i64, P, c_i64, c_i64, c_i, P, c_i64, P, c_i64,
                                     c_i64, c_i, P]),
     "gatx_edge_forward_ex": (c_i, [P, c_i64, c_i64, P, P, P, P, P, c_i64, c_i, c_i, c_i, c_i, c_i,
-                                   P, c_f, c_u64, P, c_i64, P, c_i64, c_i, P, c_i64, P]),
+                                   P, c_f, P, P, c_i64, P, c_i64, c_i, P, c_i64, P]),
     "gatx_pad_rows": (c_i, [P, c_i64, c_i64, c_i64, P, c_i64, P]),
     "gatx_projection_gemm": (c_i, [c_i64, c_i64, c_i64, P, c_i64, c_i64, P, c_i64, c_i64, P,
                                    c_i64, c_i64, P, c_i64, P, c_sz, P]),
@@ -57,16 +57,17 @@ SIGNATURES = {
                                    c_i, P, c_sz, P]),
     "gatx_node_scores": (c_i, [P, c_i64, c_i, c_i, P, P, P]),
     "gatx_attention_max_workspace_bytes": (c_sz, []),
-    "gatx_attention_max": (c_i, [P, P, c_i64, P, c_i, P, P, P, P]),
+    "gatx_attention_max": (c_i, [P, P, c_i64, P, P, c_i, P, P, P, P]),
     "gatx_edge_forward": (c_i, [P, P, P, P, P, P, P, c_i64, c_i64, c_i, c_i, c_i, c_i, P, c_f,
-                                c_u64, P, P, P, P, P]),
+                                P, P, P, P, P, P]),
     "gatx_attention_alpha": (c_i, [P, P, P, c_i64, P, P, P, c_i, c_i, P, P, P]),
-    "gatx_attention_alpha_ei": (c_i, [P, c_i, c_i64, c_i64, P, P, P, c_i, c_i, P, P, P, P, P]),
+    "gatx_attention_alpha_ei": (c_i, [P, c_i, c_i64, c_i64, P, P, P, P, c_i, c_i, P, P, P, P,
+                                      P]),
     "gatx_prepare_go": (c_i, [P, P, c_i64, c_i, c_i, c_i, c_i, P, P, P]),
-    "gatx_edge_backward_dst": (c_i, [P, P, P, P, P, P, P, c_i64, c_i64, c_i, c_i, c_i, c_f, c_u64,
+    "gatx_edge_backward_dst": (c_i, [P, P, P, P, P, P, P, c_i64, c_i64, c_i, c_i, c_i, c_f, P,
                                      P, P, P, P, P, c_i64, P]),
     "gatx_edge_backward_dst_ex": (c_i, [P, c_i64, c_i64, P, P, P, P, P, P, c_i64, c_i64, c_i,
-                                        c_i, P, c_i64, c_i64, c_f, c_u64, P, P, P, P, c_i64,
+                                        c_i, P, c_i64, c_i64, c_f, P, P, P, P, P, c_i64,
                                         c_i64, P]),
     "gatx_edge_backward_src_scores": (c_i, [P, P, c_i64, c_i64, c_i, P, P, P, c_i64, c_i64, P]),
     "gatx_gemm_splitk_batched_workspace_bytes": (c_sz, [c_i64, c_i64, c_i64, c_i64]),
@@ -74,9 +75,10 @@ SIGNATURES = {
                                            c_i64, c_i64, c_i64, P, c_i64, c_i64, c_i, P, c_sz,
                                            P]),
     "gatx_max_backward_workspace_bytes": (c_sz, []),
-    "gatx_max_backward": (c_i, [P, P, P, P, P, P, c_i64, c_i64, c_i, P, P, c_i64, c_i64, P, P]),
+    "gatx_max_backward": (c_i, [P, P, P, P, P, P, c_i64, c_i64, P, c_i, P, P, c_i64, c_i64, P,
+                                P]),
     "gatx_edge_backward_src": (c_i, [P, P, P, P, P, P, P, c_i64, c_i64, c_i, c_i, c_i, c_i, c_f,
-                                     c_u64, P, P, P, P, c_i64, P]),
+                                     P, P, P, P, P, c_i64, P]),
     "gatx_weight_grads": (c_i, [P, P, P, c_i, c_i, c_i64, P, P, P]),
     "gatx_colsum": (c_i, [P, c_i64, c_i64, c_i64, P, P]),
     "gatx_attention_norm_workspace_bytes": (c_sz, []),

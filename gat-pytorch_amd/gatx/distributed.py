@@ -2,11 +2,22 @@
 
 Inductive datasets (PPI, PATTERN) are disjoint unions of graphs, so a rank takes its own graphs
 (`shard_graphs`, DistributedSampler-equivalent) and the GAT forward needs no communication.
-Training needs exactly one exchange per step: the gradient all-reduce (`allreduce_gradients`,
-flattened into large buckets — PPI's 1.87 M parameters are one 7.47 MB bucket, which xGMI moves
-in tens of microseconds; tiny per-tensor all-reduces would be latency-bound).
+Training needs exactly one exchange per step: the gradient all-reduce. `GradientAllReducer`
+overlaps it with the backward the way DDP does: gradients are grouped into buckets in reverse
+registration order (the order backward produces them), and each bucket's all-reduce is launched
+asynchronously from a post-accumulate-grad hook the moment its last gradient is ready, while
+autograd keeps computing earlier layers' gradients. PPI's 1.87 M parameters (7.47 MB) make a few
+buckets; PATTERN's 20 k parameters (81 KB) one latency-bound bucket.
+
+Loss semantics: the reference's losses are means over nodes (BCE, `models/ppi_gat.py:11`,
+`models/pattern_gat.py:15`) or edges (`calc_attention_norm`, `models/GATModel.py:224`). With
+uneven shards a plain 1/world average of per-rank means is not the union batch's mean; scale each
+rank's loss by `count_weight(n_local)` = n_local / n_global (an all-reduce of one scalar) and SUM
+the gradients (`average=False`): the result equals one process training on the union batch.
+
 `collate_graphs` replaces PyG's `Batch` collate (`models/GATModel.py:273-287` use PyG
-DataLoaders, which are not installable here).
+DataLoaders, which are not installable here); `DeviceGraphLoader` is the sampler-driven device
+loop built on it.
 """
 from __future__ import annotations
 
@@ -23,7 +34,8 @@ def shard_graphs(num_graphs: int, rank: int, world: int) -> List[int]:
 
 def collate_graphs(graphs: Sequence[tuple]):
     """[(x_i (n_i, F), edge_index_i (2, e_i), y_i or None)] -> (x, edge_index, y, node_offsets):
-    node features concatenated, edge ids shifted by the preceding graphs' node counts."""
+    node features concatenated, edge ids shifted by the preceding graphs' node counts. Works on
+    whichever device the graphs live on (a device batch needs no host round trip)."""
     xs, eis, ys, offs = [], [], [], [0]
     for g in graphs:
         x, ei = g[0], g[1]
@@ -38,11 +50,70 @@ def collate_graphs(graphs: Sequence[tuple]):
     return x, ei, y, torch.tensor(offs, dtype=torch.int64)
 
 
+class DeviceGraphLoader:
+    """Per-rank batches of whole graphs, resident on the device: each epoch shuffles the graph ids
+    with a seed shared by every rank (DistributedSampler semantics: same permutation everywhere,
+    rank r takes every world-th id), then collates `batch_size` graphs at a time on the device.
+    `graphs` is a list of (x, edge_index, y) already on the device."""
+
+    def __init__(self, graphs, batch_size: int, rank: int = 0, world: int = 1,
+                 shuffle: bool = True, seed: int = 0, drop_last: bool = False):
+        self.graphs, self.batch_size = graphs, batch_size
+        self.rank, self.world, self.shuffle, self.seed = rank, world, shuffle, seed
+        self.drop_last = drop_last
+        self.epoch = 0
+
+    def set_epoch(self, epoch: int):
+        self.epoch = epoch
+
+    def _ids(self):
+        n = len(self.graphs)
+        if self.shuffle:
+            g = torch.Generator().manual_seed(self.seed + self.epoch)
+            order = torch.randperm(n, generator=g).tolist()
+        else:
+            order = list(range(n))
+        return [order[i] for i in shard_graphs(n, self.rank, self.world)]
+
+    def __iter__(self):
+        ids = self._ids()
+        bs = self.batch_size
+        stop = len(ids) - (len(ids) % bs if self.drop_last else 0)
+        for i in range(0, stop, bs):
+            yield collate_graphs([self.graphs[j] for j in ids[i:i + bs]])
+
+    def __len__(self):
+        n = len(self._ids())
+        return n // self.batch_size if self.drop_last else -(-n // self.batch_size)
+
+
+def count_weight(n_local: int | float, group=None, device=None) -> float:
+    """n_local / sum over ranks of n_local: the factor that turns this rank's mean loss into its
+    share of the union batch's mean (SUM the gradients afterwards)."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return 1.0
+    if device is None:
+        device = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
+    t = torch.tensor([float(n_local)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, group=group)
+    return float(n_local) / float(t.item())
+
+
+def _all_reduce_flat(flat: torch.Tensor, group, async_op: bool):
+    if flat.is_cuda and dist.get_backend(group) != "nccl":   # gloo: host staging
+        host = flat.cpu()
+        dist.all_reduce(host, group=group)
+        flat.copy_(host)
+        return None
+    return dist.all_reduce(flat, group=group, async_op=async_op)
+
+
 def allreduce_gradients(params: Iterable[torch.nn.Parameter], world: int | None = None,
-                        bucket_bytes: int = 64 << 20, group=None) -> None:
-    """Average .grad across ranks: grads flattened into <= bucket_bytes buckets, one all-reduce
-    (SUM) per bucket, scaled by 1/world, copied back. Parameters without grads are skipped (the
-    same set on every rank, as in DDP)."""
+                        bucket_bytes: int = 64 << 20, group=None, average: bool = True) -> None:
+    """Post-hoc all-reduce of .grad across ranks: grads flattened into <= bucket_bytes buckets,
+    one all-reduce (SUM) per bucket, scaled by 1/world when `average`, copied back. Parameters
+    without grads are skipped (the same set on every rank, as in DDP). GradientAllReducer is the
+    overlapped form used by training loops."""
     if world is None:
         world = dist.get_world_size(group)
     if world == 1:
@@ -56,16 +127,124 @@ def allreduce_gradients(params: Iterable[torch.nn.Parameter], world: int | None 
             continue
         if bucket:
             flat = torch.cat([b.reshape(-1) for b in bucket])
-            if flat.is_cuda and dist.get_backend(group) != "nccl":   # gloo: host staging
-                host = flat.cpu()
-                dist.all_reduce(host, group=group)
-                flat.copy_(host)
-            else:
-                dist.all_reduce(flat, group=group)
-            flat.mul_(1.0 / world)
+            _all_reduce_flat(flat, group, async_op=False)
+            if average:
+                flat.mul_(1.0 / world)
             off = 0
             for b in bucket:
                 n = b.numel()
                 b.copy_(flat[off:off + n].view_as(b))
                 off += n
         bucket, size = ([g], g.numel() * g.element_size()) if g is not None else ([], 0)
+
+
+class GradientAllReducer:
+    """DDP-style gradient all-reduce overlapped with the backward.
+
+        reducer = GradientAllReducer(model.parameters())
+        loss.backward()          # buckets are all-reduced (async) as their gradients land
+        reducer.finish()         # wait, write the reduced gradients back into .grad
+        opt.step()
+
+    Buckets hold consecutive parameters in reverse registration order (backward produces the
+    last layer's gradients first), at most `bucket_bytes` each. A bucket's flat buffer is filled
+    from the post-accumulate-grad hooks of its parameters; when the last one arrives the bucket's
+    all-reduce (SUM; then x 1/world when `average`) is issued with async_op, so RCCL moves it over
+    xGMI while autograd continues. Parameters that got no gradient this step are reduced as zeros
+    in finish() (every rank must issue the same collectives, as in DDP with
+    find_unused_parameters); they leave finish() with the reduced .grad (zeros if no rank
+    produced one)."""
+
+    def __init__(self, params: Iterable[torch.nn.Parameter], bucket_bytes: int = 4 << 20,
+                 group=None, average: bool = True):
+        self.params = [p for p in params if p.requires_grad]
+        self.group = group
+        self.average = average
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.buckets: List[dict] = []
+        cur, size = [], 0
+        for p in reversed(self.params):
+            nb = p.numel() * p.element_size()
+            if cur and size + nb > bucket_bytes:
+                self.buckets.append(self._bucket(cur))
+                cur, size = [], 0
+            cur.append(p)
+            size += nb
+        if cur:
+            self.buckets.append(self._bucket(cur))
+        self._slot = {}
+        for bi, b in enumerate(self.buckets):
+            for pi, p in enumerate(b["params"]):
+                self._slot[id(p)] = (bi, pi)
+        self._hooks = []
+        if self.world > 1:
+            for p in self.params:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+        self._reset()
+
+    def _bucket(self, params):
+        offs, o = [], 0
+        for p in params:
+            offs.append(o)
+            o += p.numel()
+        return {"params": params, "offsets": offs, "numel": o, "flat": None}
+
+    def _reset(self):
+        for b in self.buckets:
+            b["ready"] = 0
+            b["work"] = None
+            b["launched"] = False
+            b["seen"] = [False] * len(b["params"])
+
+    def _flat(self, b, like):
+        if b["flat"] is None or b["flat"].device != like.device:
+            b["flat"] = torch.zeros(b["numel"], dtype=like.dtype, device=like.device)
+        return b["flat"]
+
+    def _on_grad(self, p):
+        bi, pi = self._slot[id(p)]
+        b = self.buckets[bi]
+        flat = self._flat(b, p.grad)
+        o = b["offsets"][pi]
+        flat[o:o + p.numel()].copy_(p.grad.reshape(-1))
+        if not b["seen"][pi]:
+            b["seen"][pi] = True
+            b["ready"] += 1
+        if b["ready"] == len(b["params"]) and not b["launched"]:
+            b["launched"] = True
+            b["work"] = _all_reduce_flat(flat, self.group, async_op=True)
+
+    def finish(self):
+        """Wait for every bucket's all-reduce and write the results into .grad."""
+        if self.world == 1:
+            return
+        dev = next((p.grad.device for p in self.params if p.grad is not None), None)
+        for b in self.buckets:
+            if not b["launched"]:   # some parameters produced no gradient on this rank
+                flat = self._flat(b, torch.empty(0, device=dev) if dev is not None
+                                  else b["params"][0])
+                for pi, p in enumerate(b["params"]):
+                    if not b["seen"][pi]:
+                        o = b["offsets"][pi]
+                        flat[o:o + p.numel()].zero_()
+                b["launched"] = True
+                b["work"] = _all_reduce_flat(flat, self.group, async_op=True)
+        for b in self.buckets:
+            if b["work"] is not None:
+                b["work"].wait()
+            flat = b["flat"]
+            if self.average:
+                flat.mul_(1.0 / self.world)
+            for pi, p in enumerate(b["params"]):
+                o = b["offsets"][pi]
+                v = flat[o:o + p.numel()].view_as(p)
+                if p.grad is None:
+                    p.grad = v.clone()
+                else:
+                    p.grad.copy_(v)
+        self._reset()
+
+    def remove(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []

@@ -87,6 +87,9 @@ class LayerShape:
         self.K_aug = self.Dp + self.H2
         self.ldg = _round4(self.K_aug)
         self.out_cols = self.NH * self.F if self.concat else self.F
+        # derived weights (W_aug, padded W) may be cached: decided by gat_layer() before
+        # autograd.Function.forward, inside which grad mode is always off (see _cacheable)
+        self.cache_weights = True
 
 
 _MAX_WS = {}
@@ -137,7 +140,7 @@ def clear_weight_cache():
         _WPAD_CACHE.clear()
 
 
-def padded_weight(W, ld: int):
+def padded_weight(W, ld: int, use_cache: bool = True):
     """W (rows x F_in) copied into rows of `ld` floats (zero tail, gatx_pad_rows) so GEMMs can
     read it as float4 rows; cached on the parameter's identity and version (see _cacheable)."""
     global _WPAD_CACHE
@@ -146,7 +149,6 @@ def padded_weight(W, ld: int):
         return W
     if _WPAD_CACHE is None:
         _WPAD_CACHE = OrderedDict()
-    use_cache = _cacheable(W)
     key = (W.data_ptr(), version(W), tuple(W.shape), W.device, ld)
     hit = _WPAD_CACHE.get(key) if use_cache else None
     if hit is not None:
@@ -170,7 +172,7 @@ def augmented_weight(W, a, sh: "LayerShape"):
     from collections import OrderedDict
     if _WAUG_CACHE is None:
         _WAUG_CACHE = OrderedDict()
-    use_cache = _cacheable(W, a)
+    use_cache = sh.cache_weights
     key = (W.data_ptr(), version(W), tuple(W.shape), W.device,
            a.data_ptr() if a is not None else 0, version(a) if a is not None else -1,
            sh.NH, sh.F)
@@ -191,18 +193,11 @@ def augmented_weight(W, a, sh: "LayerShape"):
 
 def _attention_alpha(graph: Graph, S, M_ord, den, sh: "LayerShape", alpha, argmax, s):
     """alpha in edge_index' order (models/gat_layer.py:106-110): iterates edge_index' itself, so
-    both its reads and the alpha writes are coalesced (GATX_ALPHA_CSR=1: the CSR-order kernel,
-    whose writes scatter through perm)."""
-    import os
-    ei = graph.edge_index
-    if os.environ.get("GATX_ALPHA_CSR") == "1":
-        call("gatx_attention_alpha", ptr(graph.col), ptr(graph.rowidx), ptr(graph.perm),
-             graph.num_edges, ptr(S), ptr(M_ord), ptr(den), sh.NH, int(sh.const), ptr(alpha),
-             ptr(argmax), s)
-        return
-    call("gatx_attention_alpha_ei", ptr(ei), int(ei.dtype == torch.int64), ei.stride(0),
-         graph.num_edges, ptr(S), ptr(M_ord), ptr(den), sh.NH, int(sh.const), ptr(graph.rowptr),
-         ptr(graph.perm), ptr(alpha), ptr(argmax), s)
+    both its reads and the alpha writes are coalesced; |edge_index'| is read on the device."""
+    ei_p, is64, ld = graph.ei_args
+    call("gatx_attention_alpha_ei", ei_p, is64, ld, graph.edge_bound, graph.e2_ptr, ptr(S),
+         ptr(M_ord), ptr(den), sh.NH, int(sh.const), ptr(graph.rowptr), ptr(graph.perm),
+         ptr(alpha), ptr(argmax), s)
 
 
 def _env_int(name: str, default: int) -> int:
@@ -262,11 +257,11 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
     N = x.size(0)
     dev = x.device
     s = stream()
-    E2 = graph.num_edges
+    E2 = graph.edge_bound   # allocation bound; kernels read |edge_index'| on the device
     f32 = dict(dtype=torch.float32, device=dev)
     chunk = _env_int("GATX_EDGE_CHUNK", 2048)
     out = torch.empty((N, sh.out_cols), **f32)
-    alpha = torch.empty((E2, sh.NH), **f32)
+    alpha = torch.empty((max(E2, 1), sh.NH), **f32)
     den = torch.empty((N, sh.NH), **f32)
     # argmax[0] (tie count) is reset by gatx_attention_max; M_ord is written by it
     argmax = torch.empty(ARGMAX_CAP + 2, dtype=torch.int64, device=dev)
@@ -288,18 +283,18 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
                      ptr(W_aug) + 4 * sh.Dp * sh.F_in, 1, sh.F_in, ptr(S), sh.H2, sh.H2, None,
                      0, 0, *gemm_workspace(N, sh.H2, sh.F_in, dev), s)
             with _span("attention_max", (E2, sh.NH)):
-                call("gatx_attention_max", ptr(graph.col), ptr(graph.rowidx), E2, ptr(S),
-                     sh.NH, ptr(M_ord), ptr(argmax), ptr(_max_ws(dev)), s)
+                call("gatx_attention_max", ptr(graph.col), ptr(graph.rowidx), E2, graph.e2_ptr,
+                     ptr(S), sh.NH, ptr(M_ord), ptr(argmax), ptr(_max_ws(dev)), s)
         Z = torch.empty((N, sh.NH * Fin_p), **f32)
         with _span("edge_forward", (N, E2, sh.NH, Fin_p, "x")):
             hs_x = reassoc_heads_per_item(sh)   # heads sharing one x row
             call("gatx_edge_forward_ex", ptr(x_rows), Fin_p, 0, ptr(S), ptr(M_ord),
                  ptr(graph.rowptr), ptr(graph.col), ptr(graph.perm), N, sh.NH, Fin_p, hs_x, 1,
-                 int(sh.const), None, float(p), seed, ptr(Z), sh.NH * Fin_p, None, 0, 0,
+                 int(sh.const), None, float(p), ptr(seed), ptr(Z), sh.NH * Fin_p, None, 0, 0,
                  ptr(den), chunk, s)
         with _span("attention_alpha", (E2, sh.NH)):
             _attention_alpha(graph, S, M_ord, den, sh, alpha, argmax, s)
-        Wp = padded_weight(W, Fin_p)   # float4-readable rows
+        Wp = padded_weight(W, Fin_p, sh.cache_weights)   # float4-readable rows
         with _span("gemm_out", (N, sh.F, sh.F_in, sh.NH)):
             call("gatx_gemm_f32_batched", sh.NH, N, sh.F, sh.F_in, ptr(Z), sh.NH * Fin_p, 1,
                  Fin_p, ptr(Wp), 1, Fin_p, sh.F * Fin_p, ptr(out), sh.NH * sh.F, sh.F, 0,
@@ -322,12 +317,13 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
             call("gatx_node_scores", ptr(Wh), N, sh.NH, sh.F, ptr(a), ptr(S), s)
     if not sh.const:
         with _span("attention_max", (E2, sh.NH)):
-            call("gatx_attention_max", ptr(graph.col), ptr(graph.rowidx), E2, ptr(S), sh.NH,
-                 ptr(M_ord), ptr(argmax), ptr(_max_ws(dev)), s)
+            call("gatx_attention_max", ptr(graph.col), ptr(graph.rowidx), E2, graph.e2_ptr,
+                 ptr(S), sh.NH, ptr(M_ord), ptr(argmax), ptr(_max_ws(dev)), s)
     with _span("edge_forward", (N, E2, sh.NH, sh.F, sh.concat)):
         call("gatx_edge_forward_ex", ptr(Wh), sh.Dp, sh.Fp, ptr(S), ptr(M_ord),
              ptr(graph.rowptr), ptr(graph.col), ptr(graph.perm), N, sh.NH, sh.F,
-             edge_heads_per_item(sh), int(sh.concat), int(sh.const), ptr(bias), float(p), seed,
+             edge_heads_per_item(sh), int(sh.concat), int(sh.const), ptr(bias), float(p),
+             ptr(seed),
              ptr(out), sh.out_cols, resid_p, sh.out_cols, int(elu), ptr(den), chunk, s)
     with _span("attention_alpha", (E2, sh.NH)):
         _attention_alpha(graph, S, M_ord, den, sh, alpha, argmax, s)
@@ -346,7 +342,7 @@ def layer_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShape, 
     s = stream()
     f32 = dict(dtype=torch.float32, device=dev)
     g_out = g_out.contiguous()
-    E2 = graph.num_edges
+    E2 = graph.edge_bound   # g_raw row stride; kernels read |edge_index'| on the device
     graph.ensure_transpose()
     if saved.get("reassoc") and not need_x and not sh.const and sh.NH <= 8:
         return _reassoc_backward(g_out, g_alpha, x, W, a, bias, graph, sh, p, seed, saved,
@@ -372,18 +368,18 @@ def layer_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShape, 
         gsd = torch.empty((N, sh.NH), **f32)
         call("gatx_edge_backward_dst", ptr(saved["Wh"]), ptr(saved["S"]), ptr(saved["M_ord"]),
              ptr(saved["den"]), ptr(graph.rowptr), ptr(graph.col), ptr(graph.perm), N, E2,
-             sh.NH, sh.F, int(sh.concat), float(p), seed, ptr(go),
+             sh.NH, sh.F, int(sh.concat), float(p), ptr(seed), ptr(go),
              ptr(g_alpha.contiguous()) if g_alpha is not None else None, ptr(g_raw), ptr(gsd),
              ptr(G_aug), sh.ldg, s)
     call("gatx_edge_backward_src", ptr(saved["S"]), ptr(saved["M_ord"]), ptr(saved["den"]),
          ptr(graph.srowptr), ptr(graph.scol), ptr(graph.seid), ptr(graph.perm), N, E2, sh.NH,
-         sh.F, int(sh.concat), int(sh.const), float(p), seed, ptr(go), ptr(g_raw), None,
+         sh.F, int(sh.concat), int(sh.const), float(p), ptr(seed), ptr(go), ptr(g_raw), None,
          ptr(G_aug), sh.ldg, s)
     if not sh.const:   # max()'s share, added into both logit-gradient columns of G_aug
         mws = torch.empty(lib.gatx_max_backward_workspace_bytes(), dtype=torch.uint8, device=dev)
         call("gatx_max_backward", ptr(saved["argmax"]), ptr(gsd), ptr(saved["S"]),
-             ptr(saved["M_ord"]), ptr(graph.col), ptr(graph.rowidx), N, E2, sh.NH, None,
-             ptr(G_aug), sh.ldg, sh.Dp, ptr(mws), s)
+             ptr(saved["M_ord"]), ptr(graph.col), ptr(graph.rowidx), N, E2, graph.e2_ptr, sh.NH,
+             None, ptr(G_aug), sh.ldg, sh.Dp, ptr(mws), s)
     g_x = g_W = g_a = g_bias = None
     W_aug = saved["W_aug"]
     if need_bias and bias is not None:   # before g_pre may become g_x's accumulator
@@ -430,7 +426,7 @@ def _reassoc_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShap
     dev = x.device
     s = stream()
     f32 = dict(dtype=torch.float32, device=dev)
-    E2 = graph.num_edges
+    E2 = graph.edge_bound
     NH, F, Fp, F_in = sh.NH, sh.F, sh.Fp, sh.F_in
     Fin_p = _round4(F_in)
     Z, x_rows = saved["Z"], saved["x_rows"]
@@ -438,7 +434,7 @@ def _reassoc_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShap
     g_pre = torch.empty((N, sh.out_cols), **f32) if (need_resid or (need_bias and elu)) else None
     call("gatx_prepare_go", ptr(g_out), ptr(out) if elu else None, N, NH, F, 1, int(elu),
          ptr(go), ptr(g_pre), s)
-    Wp = padded_weight(W, Fin_p)                      # [NH*F][Fin_p], zero tail
+    Wp = padded_weight(W, Fin_p, sh.cache_weights)    # [NH*F][Fin_p], zero tail
     g_Z = torch.empty((N, NH * Fin_p), **f32)
     call("gatx_gemm_f32_batched", NH, N, Fin_p, F, ptr(go), sh.Dp, 1, Fp, ptr(Wp), Fin_p, 1,
          F * Fin_p, ptr(g_Z), NH * Fin_p, Fin_p, 0, None, 0, None, 0, 0, 0, s)
@@ -447,14 +443,14 @@ def _reassoc_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShap
     gsd = torch.empty((N, NH), **f32)
     call("gatx_edge_backward_dst_ex", ptr(x_rows), Fin_p, 0, ptr(saved["S"]), ptr(saved["M_ord"]),
          ptr(saved["den"]), ptr(graph.rowptr), ptr(graph.col), ptr(graph.perm), N, E2, NH, Fin_p,
-         ptr(g_Z), NH * Fin_p, Fin_p, float(p), seed,
+         ptr(g_Z), NH * Fin_p, Fin_p, float(p), ptr(seed),
          ptr(g_alpha.contiguous()) if g_alpha is not None else None, ptr(g_raw), ptr(gsd),
          ptr(G_s), 2 * NH, 0, s)
     call("gatx_edge_backward_src_scores", ptr(graph.srowptr), ptr(graph.seid), N, E2, NH,
          ptr(g_raw), None, ptr(G_s), 2 * NH, 0, s)
     mws = torch.empty(lib.gatx_max_backward_workspace_bytes(), dtype=torch.uint8, device=dev)
     call("gatx_max_backward", ptr(saved["argmax"]), ptr(gsd), ptr(saved["S"]),
-         ptr(saved["M_ord"]), ptr(graph.col), ptr(graph.rowidx), N, E2, NH, None,
+         ptr(saved["M_ord"]), ptr(graph.col), ptr(graph.rowidx), N, E2, graph.e2_ptr, NH, None,
          ptr(G_s), 2 * NH, 0, ptr(mws), s)
     g_W = g_a = g_bias = None
     if need_W or need_a:
@@ -504,10 +500,33 @@ class GATLayerFunction(torch.autograd.Function):
         return g_x, g_W, g_a, g_b, g_r, None, None, None, None, None
 
 
+def device_seed(seed, dev) -> torch.Tensor:
+    """The dropout seed as the device scalar the kernels read: an int (tests, reproducible runs)
+    is uploaded; a device int64 tensor (GATLayer draws one from torch's generator, so captured
+    graphs get a fresh one per replay) is used as is."""
+    if isinstance(seed, torch.Tensor):
+        if seed.device != dev or seed.dtype != torch.int64 or seed.numel() != 1:
+            raise RuntimeError("gatx: dropout seed must be one int64 on the layer's device")
+        return seed.reshape(1)
+    return torch.tensor([int(seed) & ((1 << 63) - 1)], dtype=torch.int64, device=dev)
+
+
 def gat_layer(x, edge_index, W, a, bias, num_heads, out_features, concat, add_self_loops,
               const_attention=False, dropout_p=0.0, seed=0, graph: Graph | None = None,
               resid=None, elu=False):
-    """Functional form of GATLayer.forward: returns (out, edge_index', alpha).
+    """Functional form of GATLayer.forward: returns (out, edge_index', alpha), the last two at
+    their exact size (reads |edge_index'| from the device: one sync per new graph)."""
+    out, graph, alpha = gat_layer_lazy(x, edge_index, W, a, bias, num_heads, out_features, concat,
+                                       add_self_loops, const_attention, dropout_p, seed, graph,
+                                       resid, elu)
+    return out, graph.edge_index, alpha[:graph.num_edges]
+
+
+def gat_layer_lazy(x, edge_index, W, a, bias, num_heads, out_features, concat, add_self_loops,
+                   const_attention=False, dropout_p=0.0, seed=0, graph: Graph | None = None,
+                   resid=None, elu=False):
+    """gat_layer without any host sync: returns (out, graph, alpha_bound) where alpha_bound is
+    (graph.edge_bound, NH) and its first graph.num_edges rows are alpha in edge_index' order.
     resid / elu fuse GATModel's skip-add and ELU into the layer's epilogue:
     out = elu?(layer(x) + resid)."""
     from .graph import graph_cache
@@ -523,12 +542,14 @@ def gat_layer(x, edge_index, W, a, bias, num_heads, out_features, concat, add_se
     W = W.contiguous()
     a = a.contiguous() if a is not None else None
     sh = LayerShape(num_heads, out_features, x.size(1), concat, const_attention)
+    sh.cache_weights = _cacheable(W, a)
     if W.shape != (num_heads * out_features, x.size(1)):
         raise RuntimeError(f"W.weight shape {tuple(W.shape)} does not match "
                            f"({num_heads * out_features}, {x.size(1)})")
     if graph is None:
         graph = graph_cache.get(edge_index, x.size(0), add_self_loops)
-    if graph.num_edges == 0 and not const_attention:
+    # E' == 0 iff E == 0 (with the rewrite an empty edge_index already raised in Graph)
+    if graph.num_input_edges == 0 and not const_attention:
         # attention_weights.max() of an empty tensor (models/gat_layer.py:85)
         raise RuntimeError("max(): Expected reduction dim to be specified for input.numel() == 0.")
     if bias is not None and not concat and num_heads != 1:
@@ -540,9 +561,10 @@ def gat_layer(x, edge_index, W, a, bias, num_heads, out_features, concat, add_se
         resid = resid.contiguous()
         if resid.shape != (x.size(0), sh.out_cols):
             raise RuntimeError(f"resid shape {tuple(resid.shape)} != {(x.size(0), sh.out_cols)}")
-    out, alpha = GATLayerFunction.apply(x, W, a, bias, resid, graph, sh, float(dropout_p),
-                                        int(seed), bool(elu))
-    return out, graph.edge_index, alpha
+    p = float(dropout_p)
+    seed_t = device_seed(seed, x.device) if p > 0 else None
+    out, alpha = GATLayerFunction.apply(x, W, a, bias, resid, graph, sh, p, seed_t, bool(elu))
+    return out, graph, alpha
 
 
 def _dst_row(graph):

@@ -4,12 +4,22 @@
 The reference rewrites self-loops inside every forward of every layer
 (`models/gat_layer.py:53-54` -> `models/utils.py:47-67`) and then scatters/gathers by raw edge
 indices. Here the rewrite and the CSR build run once per distinct edge_index on the GPU
-(`gatx_edge_stats` + `gatx_graph_build`, csrc/graph.hip) and are reused by every layer and step
-that sees the same tensor. The one host sync per new graph is the reference's own
-`int(index.max())` (`models/utils.py:70-72`), which sizes edge_index'.
+(`gatx_graph_meta` + `gatx_graph_build`, csrc/graph.hip) and are reused by every layer and step
+that sees the same tensor.
+
+No host sync: the reference's `int(index.max())` (`models/utils.py:70-72`) sizes edge_index' on
+the host; here |edge_index'| stays on the device (meta[0]) and the host allocates for the bound
+E + num_nodes. The exact count is read back only when something host-side needs it — the
+returned edge_index' / attention tensors (`num_edges`, `edge_index`) — so a forward that returns
+only the node outputs never waits for the device, and the whole step can be captured into a
+hipGraph. Invalid ids (negative, or >= num_nodes) make the device build an empty graph (nothing
+indexes out of bounds) and raise here as soon as the meta is read: at the first host-side use,
+at `Graph.poll()` (non-blocking, called by every layer on a cached graph) or at
+`gatx.graph.check_pending()` — asynchronous error reporting, as for a device-side assert.
 """
 from __future__ import annotations
 
+import weakref
 from collections import OrderedDict
 
 import torch
@@ -17,15 +27,27 @@ import torch
 from . import _lib
 from ._lib import call, ptr, stream, version
 
+_I32_LIMIT = 2 ** 31 - 2
+
+
+def _status_error(meta, N):
+    status, mn, mx = int(meta[2]), int(meta[3]), int(meta[4])
+    if status == 1:
+        return RuntimeError(f"index {mn} is out of bounds: edge_index has negative node ids")
+    if status == 2:
+        return IndexError(f"index {mx} is out of bounds for dimension 0 with size {N}")
+    return None
+
 
 class Graph:
-    """CSR of edge_index' (int32), plus the returned edge_index' tensor itself.
+    """CSR of edge_index' (int32), plus edge_index' itself.
 
-    rowptr [N+1], col [E2] (source), rowidx [E2] (destination), perm [E2] (CSR slot -> position
-    in edge_index'); srowptr / scol / seid: the source-ordered transpose, built on first use."""
+    rowptr [N+1], col [Eb] (source), rowidx [Eb] (destination), perm [Eb] (CSR slot -> position
+    in edge_index'); srowptr / scol / seid: the source-ordered transpose, built on first use.
+    Eb = `edge_bound` >= E' is the allocation; kernels read E' from `e2_ptr` (device)."""
 
     def __init__(self, edge_index: torch.Tensor, num_nodes, add_self_loops: bool):
-        """num_nodes None: size the node range from the edges (max id + 1)."""
+        """num_nodes None: size the node range from the edges (max id + 1; one host sync)."""
         if edge_index.dim() != 2 or edge_index.size(0) != 2:
             raise RuntimeError(f"edge_index must have shape (2, E), got {tuple(edge_index.shape)}")
         if edge_index.dtype not in (torch.int64, torch.int32):
@@ -37,7 +59,9 @@ class Graph:
             edge_index = edge_index.contiguous()
         self.device = dev
         self.add_self_loops = add_self_loops
+        self.source = edge_index
         E = edge_index.size(1)
+        self.num_input_edges = E
         is64 = int(edge_index.dtype == torch.int64)
         ld = edge_index.stride(0)
         if E == 0 and add_self_loops:
@@ -45,55 +69,122 @@ class Graph:
             raise RuntimeError("max(): Expected reduction dim to be specified for input.numel() == 0. "
                                "Specify the reduction dim with the 'dim' argument.")
         s = stream()
-        stats = torch.empty(3, dtype=torch.int64, device=dev)
-        sws = torch.empty(_lib.lib.gatx_edge_stats_workspace_bytes(), dtype=torch.uint8,
-                          device=dev)
-        call("gatx_edge_stats", ptr(edge_index), is64, E, ld, ptr(stats), ptr(sws), s)
-        mn, mx, nloops = (int(v) for v in stats.cpu())   # the one host sync per new graph
-        if num_nodes is None:
-            num_nodes = mx + 1 if E else 0
+        self.meta = torch.empty(8, dtype=torch.int64, device=dev)
+        ws = _meta_ws(dev)
+        if num_nodes is None:   # sized by the edges themselves: the one case that must sync
+            call("gatx_graph_meta", ptr(edge_index), is64, E, ld, int(add_self_loops),
+                 _I32_LIMIT, ptr(self.meta), ptr(ws), s)
+            m = self.meta.cpu()
+            err = _status_error(m, _I32_LIMIT)
+            if err is not None:
+                raise err
+            num_nodes = int(m[4]) + 1 if E else 0
         self.num_nodes = N = int(num_nodes)
-        if E and mn < 0:
-            raise RuntimeError(f"index {mn} is out of bounds: edge_index has negative node ids")
-        if E and mx >= N:
-            raise IndexError(f"index {mx} is out of bounds for dimension 0 with size {N}")
-        if add_self_loops:
-            num_loops = mx + 1
-            E2 = E - nloops + num_loops
-        else:
-            num_loops = 0
-            E2 = E
-        self.num_edges = E2
+        call("gatx_graph_meta", ptr(edge_index), is64, E, ld, int(add_self_loops), N,
+             ptr(self.meta), ptr(ws), s)
+        Eb = E + N if add_self_loops else E
+        if Eb >= 2 ** 31 - 1 or N >= 2 ** 31 - 1:
+            raise RuntimeError("gatx: graphs are limited to 2^31-1 nodes / edges")
+        self.edge_bound = Eb
         i32 = dict(dtype=torch.int32, device=dev)
         self.rowptr = torch.empty(N + 1, **i32)
-        self.col = torch.empty(max(E2, 1), **i32)
-        self.rowidx = torch.empty(max(E2, 1), **i32)
-        self.perm = torch.empty(max(E2, 1), **i32)
+        self.col = torch.empty(max(Eb, 1), **i32)
+        self.rowidx = torch.empty(max(Eb, 1), **i32)
+        self.perm = torch.empty(max(Eb, 1), **i32)
         if add_self_loops:
-            self.edge_index = torch.empty((2, E2), dtype=torch.int64, device=dev)
-            ei_out = ptr(self.edge_index)
+            self._ei_flat = torch.empty(max(2 * Eb, 2), dtype=torch.int64, device=dev)
+            ei_out = ptr(self._ei_flat)
         else:
-            self.edge_index = edge_index   # the reference returns its input unchanged
+            self._ei_flat = None   # the reference returns its input unchanged
             ei_out = None
-        ws_bytes = _lib.lib.gatx_graph_build_workspace_bytes(E, E2, N)
-        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
-        call("gatx_graph_build", ptr(edge_index), is64, E, ld, int(add_self_loops), num_loops, N,
-             E2, ei_out, ptr(self.rowptr), ptr(self.col), ptr(self.rowidx), ptr(self.perm),
-             ptr(ws), ws_bytes, s)
+        ws_bytes = _lib.lib.gatx_graph_build_workspace_bytes(E, Eb, N)
+        bws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        call("gatx_graph_build", ptr(edge_index), is64, E, ld, int(add_self_loops), N, Eb,
+             ptr(self.meta), ei_out, ptr(self.rowptr), ptr(self.col), ptr(self.rowidx),
+             ptr(self.perm), ptr(bws), ws_bytes, s)
         self.srowptr = self.scol = self.seid = None
+        self._E2 = None
+        self._error = None
+        self._edge_index = None
+        # non-blocking validation: the meta lands in pinned memory behind an event
+        self._meta_host = None
+        self._event = None
+        if not torch.cuda.is_current_stream_capturing():
+            self._meta_host = torch.empty(8, dtype=torch.int64, pin_memory=True)
+            self._meta_host.copy_(self.meta, non_blocking=True)
+            self._event = torch.cuda.Event()
+            self._event.record()
+            check_pending(block=False)   # surfaces errors of earlier graphs that have landed
+            _PENDING.append(weakref.ref(self))
+
+    # ---- device-side sizes
+    @property
+    def e2_ptr(self) -> int:
+        """Device address of |edge_index'| (int64), for the kernels' edge-count argument."""
+        return ptr(self.meta)
+
+    @property
+    def ei_args(self):
+        """(pointer, is64, ld) of edge_index' for gatx_attention_alpha_ei: the flat (2, E')
+        buffer (ld < 0: taken from the device count) or the untouched input."""
+        if self._ei_flat is not None:
+            return ptr(self._ei_flat), 1, -1
+        t = self.source
+        return ptr(t), int(t.dtype == torch.int64), t.stride(0)
+
+    def _validate(self, m):
+        err = _status_error(m, self.num_nodes)
+        if err is not None:
+            self._error = err   # every later use of this graph raises it again
+            raise err
+        self._E2 = int(m[0])
+
+    def poll(self):
+        """Validate without blocking if the device has produced the meta (raises on bad ids)."""
+        if self._error is not None:
+            raise self._error
+        if self._E2 is None and self._event is not None and self._event.query():
+            self._validate(self._meta_host)
+
+    # ---- host-side sizes (synchronise on first use)
+    @property
+    def num_edges(self) -> int:
+        """|edge_index'| (reads the device meta once: a sync if it is not there yet)."""
+        if self._error is not None:
+            raise self._error
+        if self._E2 is None:
+            if self._event is not None:
+                self._event.synchronize()
+                self._validate(self._meta_host)
+            else:
+                self._validate(self.meta.cpu())
+        return self._E2
+
+    @property
+    def edge_index(self) -> torch.Tensor:
+        """edge_index' as the reference returns it: a contiguous int64 (2, E') tensor (the input
+        itself without the rewrite)."""
+        if self._edge_index is None:
+            E2 = self.num_edges
+            if self._ei_flat is None:
+                self._edge_index = self.source
+            else:
+                self._edge_index = self._ei_flat[:2 * E2].view(2, E2)
+                graph_cache.alias(self._edge_index, self)
+        return self._edge_index
 
     def ensure_transpose(self):
         if self.srowptr is not None:
             return
-        N, E2, dev = self.num_nodes, self.num_edges, self.device
+        N, Eb, dev = self.num_nodes, self.edge_bound, self.device
         i32 = dict(dtype=torch.int32, device=dev)
         self.srowptr = torch.empty(N + 1, **i32)
-        self.scol = torch.empty(max(E2, 1), **i32)
-        self.seid = torch.empty(max(E2, 1), **i32)
-        ws_bytes = _lib.lib.gatx_graph_transpose_workspace_bytes(E2, N)
+        self.scol = torch.empty(max(Eb, 1), **i32)
+        self.seid = torch.empty(max(Eb, 1), **i32)
+        ws_bytes = _lib.lib.gatx_graph_transpose_workspace_bytes(Eb, N)
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
-        call("gatx_graph_transpose", ptr(self.col), ptr(self.rowidx), N, E2, ptr(self.srowptr),
-             ptr(self.scol), ptr(self.seid), ptr(ws), ws_bytes, stream())
+        call("gatx_graph_transpose", ptr(self.col), ptr(self.rowidx), N, Eb, self.e2_ptr,
+             ptr(self.srowptr), ptr(self.scol), ptr(self.seid), ptr(ws), ws_bytes, stream())
 
     def csr_host(self):
         """(rowptr, col, perm) as CPU tensors — for tests."""
@@ -101,18 +192,53 @@ class Graph:
         return self.rowptr.cpu(), self.col[:E2].cpu(), self.perm[:E2].cpu()
 
 
+_META_WS = {}
+_PENDING: list = []
+
+
+def _meta_ws(dev):
+    t = _META_WS.get(dev)
+    if t is None:
+        t = torch.empty(_lib.lib.gatx_graph_meta_workspace_bytes(), dtype=torch.uint8, device=dev)
+        _META_WS[dev] = t
+    return t
+
+
+def check_pending(block: bool = True):
+    """Validate every live graph whose meta has not been read yet (blocking by default): raises
+    the first bad-index error, like torch.cuda.synchronize() surfacing a device assert. Called
+    non-blocking by every Graph construction."""
+    global _PENDING
+    pending, _PENDING = _PENDING, []
+    for i, r in enumerate(pending):
+        g = r()
+        if g is None or g._E2 is not None or g._error is not None:
+            continue   # gone, validated, or its error already raised
+        try:
+            if block:
+                _ = g.num_edges
+            else:
+                g.poll()
+        except Exception:
+            _PENDING.extend(x for x in pending[i + 1:] if x() is not None)
+            raise
+        if g._E2 is None:
+            _PENDING.append(r)
+
+
 class GraphCache:
     """Small LRU of Graphs keyed on the edge_index tensor's identity and version. Entries hold a
     reference to their key tensor, so a cached data_ptr can never be recycled under them. A
-    Graph built with add_self_loops also answers for its own output edge_index' (the rewrite is
-    idempotent, so GATModel.forward_and_return_attention's chaining of layers hits the cache)."""
+    Graph built with add_self_loops also answers for its own output edge_index' once that is
+    materialised (the rewrite is idempotent, so GATModel.forward_and_return_attention's chaining
+    of layers hits the cache)."""
 
     def __init__(self, capacity: int = 8):
         self.capacity = capacity
         self._d: OrderedDict = OrderedDict()
 
     @staticmethod
-    def _key(t: torch.Tensor, num_nodes: int, add_self_loops: bool):
+    def _key(t: torch.Tensor, num_nodes, add_self_loops: bool):
         return (t.data_ptr(), version(t), tuple(t.shape), tuple(t.stride()), t.dtype,
                 t.device, num_nodes, add_self_loops)
 
@@ -121,19 +247,26 @@ class GraphCache:
         hit = self._d.get(k)
         if hit is not None:
             self._d.move_to_end(k)
-            return hit[1]
+            g = hit[1]
+            g.poll()
+            return g
         g = Graph(edge_index, num_nodes, add_self_loops)
         self._put(k, edge_index, g)
-        if add_self_loops:
-            self._put(self._key(g.edge_index, num_nodes, True), g.edge_index, g)
         return g
+
+    def alias(self, ei2: torch.Tensor, g: Graph):
+        """Register a graph's materialised edge_index' as a key of the same graph."""
+        if g.add_self_loops:
+            self._put(self._key(ei2, g.num_nodes, True), ei2, g)
 
     def for_edges(self, edge_index: torch.Tensor) -> Graph:
         """The Graph whose edge_index' IS this tensor (what a layer returned), else a CSR of it
         as given (no rewrite), sized by its max id — for consumers of a layer's output edges
         such as the attention-norm regulariser."""
         for t, g in reversed(self._d.values()):
-            ei = g.edge_index
+            ei = g._edge_index
+            if ei is None:
+                continue
             if ei is edge_index or (ei.data_ptr() == edge_index.data_ptr()
                                     and version(ei) == version(edge_index)
                                     and ei.shape == edge_index.shape

@@ -17,7 +17,7 @@ from __future__ import annotations
 import torch
 from torch import nn
 
-from .functional import gat_layer
+from .functional import gat_layer_lazy
 
 
 class GATLayer(nn.Module):
@@ -53,25 +53,45 @@ class GATLayer(nn.Module):
         if self.bias:
             nn.init.zeros_(self.bias_param)
 
-    def _dropout_seed(self) -> int:
-        # one 64-bit draw from torch's CPU generator per forward: follows torch.manual_seed
-        return int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+    def _dropout_seed(self, device):
+        # one 64-bit draw from torch's generator on the layer's device per forward (the
+        # reference's nn.Dropout draws there too): follows torch.cuda.manual_seed, no host sync,
+        # and a captured hipGraph draws a fresh seed on every replay
+        return torch.randint(0, 2 ** 62, (1,), dtype=torch.int64, device=device)
+
+    @property
+    def normalised_attention_coeffs(self):
+        """alpha of the last forward (`models/gat_layer.py:110`), (E', NH) in edge_index' order.
+        Kept at its allocation bound until read: the exact E' lives on the device, so the slice
+        (one host read of E') happens here, not in forward."""
+        att = self.__dict__.get("_attention")
+        if att is None or isinstance(att, torch.Tensor):
+            return att
+        graph, alpha = att
+        view = alpha[:graph.num_edges]
+        self.__dict__["_attention"] = view
+        return view
+
+    @normalised_attention_coeffs.setter
+    def normalised_attention_coeffs(self, value):
+        self.__dict__["_attention"] = value
 
     def forward(self, x, edge_index, return_attention_weights=False, *, graph=None, resid=None,
                 elu=False):
         """Reference signature (`models/gat_layer.py:42`); keyword-only extras: `graph` (a
         prebuilt gatx.Graph), `resid` / `elu` (GATModel's skip-add + ELU fused into the
-        epilogue: returns elu?(out + resid))."""
+        epilogue: returns elu?(out + resid)). Without return_attention_weights nothing waits
+        for the device (|edge_index'| is only known there)."""
         p = float(self.dropout) if (self.dropout > 0 and self.training) else 0.0
-        seed = self._dropout_seed() if p > 0 else 0
-        out, edge_index_out, alpha = gat_layer(
+        seed = self._dropout_seed(x.device) if p > 0 else 0
+        out, g, alpha = gat_layer_lazy(
             x, edge_index, self.W.weight, None if self.const_attention else self.a.weight,
             self.bias_param if self.bias else None, self.num_heads, self.out_features,
             self.concat, self.add_self_loops, self.const_attention, p, seed, graph=graph,
             resid=resid, elu=elu)
-        self.normalised_attention_coeffs = alpha
+        self.normalised_attention_coeffs = (g, alpha)
         if return_attention_weights:
-            return out, (edge_index_out, alpha)
+            return out, (g.edge_index, self.normalised_attention_coeffs)
         return out
 
     def extra_repr(self) -> str:

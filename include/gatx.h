@@ -39,36 +39,46 @@ int gatx_version(void);
 
 /* ---------------------------------------------------------------- graph (models/utils.py) */
 
-/* min / max node id and self-loop count of an edge_index (2, E) (int64 if index_is_int64 else
- * int32; rows `ld` elements apart). stats: device int64[3] = {min, max, n_selfloops}.
- * Replaces the `index.max()` of maybe_num_nodes (models/utils.py:70-72) and the `row != col`
- * mask count of add_remaining_self_loops (models/utils.py:58-60). */
-size_t gatx_edge_stats_workspace_bytes(void);
-int gatx_edge_stats(const void* edge_index, int index_is_int64, int64_t E, int64_t ld,
-                    int64_t* stats, void* workspace, gatx_stream_t stream);
+/* Device-side sizing of the self-loop rewrite, no host sync (replaces the `int(index.max())` of
+ * maybe_num_nodes, models/utils.py:70-72, and the `row != col` mask count of
+ * add_remaining_self_loops, models/utils.py:58-60). edge_index (2, E): int64 if index_is_int64
+ * else int32, rows `ld` elements apart. meta (device int64[8]) = {E2, num_loops, status, min id,
+ * max id, input self-loops, 0, 0} with num_loops = max+1 when add_self_loops, E2 = |edge_index'|.
+ * status 1 = a negative id, 2 = an id >= num_nodes: then E2 = num_loops = 0, so every later kernel
+ * sees an empty graph (no out-of-bounds access) and the host raises when it reads meta (the
+ * reference raises in index_select / scatter_add_). workspace: gatx_graph_meta_workspace_bytes(). */
+size_t gatx_graph_meta_workspace_bytes(void);
+int gatx_graph_meta(const void* edge_index, int index_is_int64, int64_t E, int64_t ld,
+                    int add_self_loops, int64_t num_nodes, int64_t* meta, void* workspace,
+                    gatx_stream_t stream);
 
-/* Self-loop rewrite + destination CSR, one pass of device kernels.
+/* Self-loop rewrite + destination CSR, one pass of device kernels, sized on the device from meta.
  * edge_index' = [edges with src != dst in input order | (i, i) for i < num_loops] when
- * add_self_loops (models/utils.py:47-67; num_loops = max+1), else edge_index unchanged.
- * Outputs (E2 = |edge_index'|): edge_index_out int64 (2, E2) (may be NULL), and the CSR of
- * edge_index' by destination over num_nodes rows, stable in edge_index' order:
- *   rowptr [num_nodes+1], col [E2] = source id, rowidx [E2] = destination id,
- *   perm [E2] = position in edge_index' of each CSR slot.
+ * add_self_loops (models/utils.py:47-67), else edge_index unchanged. The host allocates for
+ * E_bound >= E (+ num_nodes with self-loops); slots past E2 are padding that sorts after every
+ * real slot, and rowptr[num_nodes] = E2.
+ * Outputs: edge_index_out (nullable) int64[2 * E_bound] holding edge_index' contiguously as
+ * (2, E2): sources at [0, E2), destinations at [E2, 2*E2); and the CSR of edge_index' by
+ * destination over num_nodes rows, stable in edge_index' order:
+ *   rowptr [num_nodes+1], col [E_bound] = source id, rowidx [E_bound] = destination id,
+ *   perm [E_bound] = position in edge_index' of each CSR slot.
  * Replaces the per-layer `add_remaining_self_loops` call (models/gat_layer.py:53-54) and the
  * scatter/gather index plumbing of sum_over_neighbourhood / explicit_broadcast. */
-size_t gatx_graph_build_workspace_bytes(int64_t E, int64_t E2, int64_t num_nodes);
+size_t gatx_graph_build_workspace_bytes(int64_t E, int64_t E_bound, int64_t num_nodes);
 int gatx_graph_build(const void* edge_index, int index_is_int64, int64_t E, int64_t ld,
-                     int add_self_loops, int64_t num_loops, int64_t num_nodes, int64_t E2,
+                     int add_self_loops, int64_t num_nodes, int64_t E_bound, const int64_t* meta,
                      int64_t* edge_index_out, int32_t* rowptr, int32_t* col, int32_t* rowidx,
                      int32_t* perm, void* workspace, size_t workspace_bytes,
                      gatx_stream_t stream);
 
-/* Source-ordered transpose of the CSR (for the backward's scatters to source nodes):
- * srowptr [num_nodes+1], scol [E2] = destination id, seid [E2] = dst-CSR slot. */
-size_t gatx_graph_transpose_workspace_bytes(int64_t E2, int64_t num_nodes);
-int gatx_graph_transpose(const int32_t* col, const int32_t* rowidx, int64_t num_nodes, int64_t E2,
-                         int32_t* srowptr, int32_t* scol, int32_t* seid, void* workspace,
-                         size_t workspace_bytes, gatx_stream_t stream);
+/* Source-ordered transpose of the CSR (for the backward's scatters to source nodes), E2 read
+ * from the device (e2 = &meta[0]): srowptr [num_nodes+1], scol [E_bound] = destination id,
+ * seid [E_bound] = dst-CSR slot. */
+size_t gatx_graph_transpose_workspace_bytes(int64_t E_bound, int64_t num_nodes);
+int gatx_graph_transpose(const int32_t* col, const int32_t* rowidx, int64_t num_nodes,
+                         int64_t E_bound, const int64_t* e2, int32_t* srowptr, int32_t* scol,
+                         int32_t* seid, void* workspace, size_t workspace_bytes,
+                         gatx_stream_t stream);
 
 /* ---------------------------------------------------------------- projection (gat_layer.py:64) */
 
@@ -144,13 +154,15 @@ int gatx_gemm_f32_batched(int64_t batch, int64_t M, int64_t N, int64_t K, const 
 /* ---------------------------------------------------------------- attention + aggregation */
 
 /* Global max M = max_{e,h} s_src[col[e],h] + s_dst[rowidx[e],h]  (gat_layer.py:85), written as an
- * order-preserving uint32 into *M_ord (device). argmax (nullable): its tie counter argmax[0] is
- * reset to 0 for the following gatx_attention_alpha. workspace:
+ * order-preserving uint32 into *M_ord (device). Edge-count convention of every edge-parallel
+ * entry point: E2 is the host bound (grid size, strides); e2 (nullable) is the device count
+ * (&meta[0] of gatx_graph_meta), and min(E2, *e2) edges are processed. argmax (nullable): its
+ * tie counter argmax[0] is reset to 0 for the following gatx_attention_alpha*. workspace:
  * gatx_attention_max_workspace_bytes(). */
 size_t gatx_attention_max_workspace_bytes(void);
-int gatx_attention_max(const int32_t* col, const int32_t* rowidx, int64_t E2, const float* S,
-                       int NH, uint32_t* M_ord, int64_t* argmax, void* workspace,
-                       gatx_stream_t stream);
+int gatx_attention_max(const int32_t* col, const int32_t* rowidx, int64_t E2, const int64_t* e2,
+                       const float* S, int NH, uint32_t* M_ord, int64_t* argmax,
+                       void* workspace, gatx_stream_t stream);
 
 /* Fused edge pass per destination segment (gat_layer.py:85-135), then the attention output:
  *   ex = exp(0.01 * (s_src[src] + s_dst[dst] - M))   (LeakyReLU(0.01) of a non-positive value)
@@ -161,12 +173,14 @@ int gatx_attention_max(const int32_t* col, const int32_t* rowidx, int64_t E2, co
  * backward; argmax = int64[GATX_ARGMAX_CAP + 2]: count, then (csr_slot*NH + h) of raw == M
  * entries, then one scratch slot for gatx_max_backward (zeroed by the caller).
  * const_attention: ex = 1 (S, M, argmax unused). dropout_p > 0 applies the counter-based keep
- * mask dropout_keep(seed, e', h) (gatx_common.h). = gatx_edge_forward_ex + gatx_attention_alpha. */
+ * mask dropout_keep(*seed, e', h) (gatx_common.h); seed is a DEVICE uint64 (drawn from torch's
+ * generator, so a captured graph draws a fresh one per replay; unused when dropout_p == 0).
+ * = gatx_edge_forward_ex + gatx_attention_alpha (E2 exact here). */
 int gatx_edge_forward(const float* Wh, const float* S, const uint32_t* M_ord,
                       const int32_t* rowptr, const int32_t* col, const int32_t* rowidx,
                       const int32_t* perm, int64_t num_nodes, int64_t E2, int NH, int F,
                       int concat, int const_attention, const float* bias, float dropout_p,
-                      uint64_t seed, float* out, float* alpha, float* den, int64_t* argmax,
+                      const uint64_t* seed, float* out, float* alpha, float* den, int64_t* argmax,
                       gatx_stream_t stream);
 
 /* The aggregation half, generalised. Source rows are read at rows + src*row_stride +
@@ -181,7 +195,7 @@ int gatx_edge_forward_ex(const float* rows, int64_t row_stride, int64_t head_str
                          const float* S, const uint32_t* M_ord, const int32_t* rowptr,
                          const int32_t* col, const int32_t* perm, int64_t num_nodes, int NH,
                          int F, int heads_per_item, int concat, int const_attention,
-                         const float* bias, float dropout_p, uint64_t seed, float* out,
+                         const float* bias, float dropout_p, const uint64_t* seed, float* out,
                          int64_t out_ld, const float* resid, int64_t resid_ld, int elu,
                          float* den, int64_t chunk, gatx_stream_t stream);
 
@@ -191,13 +205,16 @@ int gatx_attention_alpha(const int32_t* col, const int32_t* rowidx, const int32_
                          int64_t E2, const float* S, const uint32_t* M_ord, const float* den,
                          int NH, int const_attention, float* alpha, int64_t* argmax,
                          gatx_stream_t stream);
-/* gatx_attention_alpha iterating edge_index' itself (int64 or int32, row stride ld): reads each
- * edge's (src, dst) and writes alpha[p] in order (coalesced both ways); rowptr / perm (the CSR)
- * are only read to record a tied argmax by CSR slot, as gatx_attention_alpha does. */
+/* gatx_attention_alpha iterating edge_index' itself (int64 or int32, row stride ld; ld < 0:
+ * the flat (2, E2) layout of gatx_graph_build, ld = the device count): reads each edge's
+ * (src, dst) and writes alpha[p] in order (coalesced both ways); rowptr / perm (the CSR) are only
+ * read to record a tied argmax by CSR slot, as gatx_attention_alpha does. E2 / e2: the bound and
+ * the device count (see gatx_attention_max). */
 int gatx_attention_alpha_ei(const void* edge_index, int index_is_int64, int64_t ld, int64_t E2,
-                            const float* S, const uint32_t* M_ord, const float* den, int NH,
-                            int const_att, const int32_t* rowptr, const int32_t* perm,
-                            float* alpha, int64_t* argmax, gatx_stream_t stream);
+                            const int64_t* e2, const float* S, const uint32_t* M_ord,
+                            const float* den, int NH, int const_att, const int32_t* rowptr,
+                            const int32_t* perm, float* alpha, int64_t* argmax,
+                            gatx_stream_t stream);
 
 /* S [N][2NH] = (Wh . A_src^T | Wh . A_dst^T) from Wh [N][Dp] and a.weight — the reference's own
  * association of the logit GEMV (gat_layer.py:76-82), used when folding the scores into the
@@ -225,13 +242,13 @@ int gatx_prepare_go(const float* g_out, const float* out, int64_t num_nodes, int
 /* Destination pass, one wave per (node n, head h):
  *   g_alpha~[e,h] = <go[n,h,:], Wh[src,h,:]>; g_alpha = g_alpha~ * keep/(1-p) + g_alpha_ret
  *   c[n,h] = sum_{e->n} g_alpha * alpha; g_raw'[e,h] = 0.01 * ex * (g_alpha - c) / (den + 1e-8)
- * Writes g_raw' head-major [NH][E2] in CSR order and g_s_dst = sum_e g_raw' into
+ * Writes g_raw' head-major [NH][E2] in CSR order (E2 = the row stride: the host bound) and g_s_dst = sum_e g_raw' into
  * G_aug[n][Dp+NH+h] and gsd [N][NH]. g_alpha_ret (the returned alpha's gradient, edge_index'
  * order) may be NULL. */
 int gatx_edge_backward_dst(const float* Wh, const float* S, const uint32_t* M_ord,
                            const float* den, const int32_t* rowptr, const int32_t* col,
                            const int32_t* perm, int64_t num_nodes, int64_t E2, int NH, int F,
-                           int concat, float dropout_p, uint64_t seed, const float* go,
+                           int concat, float dropout_p, const uint64_t* seed, const float* go,
                            const float* g_alpha_ret, float* g_raw, float* gsd, float* G_aug,
                            int64_t ldg, gatx_stream_t stream);
 /* The dst pass over arbitrary gathered rows: g_alpha[e,h] = <go[n, h], rows[src_e] + h *
@@ -243,7 +260,7 @@ int gatx_edge_backward_dst_ex(const float* rows, int64_t row_stride, int64_t hea
                               const float* S, const uint32_t* M_ord, const float* den,
                               const int32_t* rowptr, const int32_t* col, const int32_t* perm,
                               int64_t num_nodes, int64_t E2, int NH, int F, const float* go,
-                              int64_t go_stride, int64_t go_head, float p, uint64_t seed,
+                              int64_t go_stride, int64_t go_head, float p, const uint64_t* seed,
                               const float* g_alpha_ret, float* g_raw, float* gsd, float* G,
                               int64_t ldg, int64_t gs_off, gatx_stream_t stream);
 /* Source-side logit gradients only: G[s][gs_off + h] = sum over s's out-edges (src-CSR) of
@@ -256,13 +273,14 @@ int gatx_edge_backward_src_scores(const int32_t* srowptr, const int32_t* seid, i
  * fixed-order reduction); g_M/k is added to G_aug[dst][Dp+NH+h] and to the source side for
  * each recorded argmax entry: into g_corr_src[src,h] ([N][NH], zeroed by the caller, consumed
  * by the src pass) or, with g_corr_src NULL, straight into G_aug[src][Dp+h] (call it after the
- * src pass). Falls back to a full scan of the edges when more than GATX_ARGMAX_CAP entries
- * tie. */
+ * src pass). Falls back to a full scan of the edges (E2 bound / e2 device count, see
+ * gatx_attention_max) when more than GATX_ARGMAX_CAP entries tie. */
 size_t gatx_max_backward_workspace_bytes(void);
 int gatx_max_backward(const int64_t* argmax, const float* gsd, const float* S,
                       const uint32_t* M_ord, const int32_t* col, const int32_t* rowidx,
-                      int64_t num_nodes, int64_t E2, int NH, float* g_corr_src, float* G_aug,
-                      int64_t ldg, int64_t Dp, void* workspace, gatx_stream_t stream);
+                      int64_t num_nodes, int64_t E2, const int64_t* e2, int NH,
+                      float* g_corr_src, float* G_aug, int64_t ldg, int64_t Dp, void* workspace,
+                      gatx_stream_t stream);
 
 /* Source pass, one wave per (node s, head h): G_aug[s][h*Fp:] = sum_{e: src=s} alpha~[e,h] *
  * go[dst_e,h,:] (the message gradient), G_aug[s][Dp+h] = sum_{e: src=s} g_raw'[e,h] +
@@ -270,7 +288,7 @@ int gatx_max_backward(const int64_t* argmax, const float* gsd, const float* S,
 int gatx_edge_backward_src(const float* S, const uint32_t* M_ord, const float* den,
                            const int32_t* srowptr, const int32_t* scol, const int32_t* seid,
                            const int32_t* perm, int64_t num_nodes, int64_t E2, int NH, int F,
-                           int concat, int const_attention, float dropout_p, uint64_t seed,
+                           int concat, int const_attention, float dropout_p, const uint64_t* seed,
                            const float* go, const float* g_raw, const float* g_corr_src,
                            float* G_aug, int64_t ldg, gatx_stream_t stream);
 

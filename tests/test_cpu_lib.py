@@ -41,6 +41,39 @@ def test_ctypes_binding_covers_header(lib):
     assert set(declared_functions()) == set(SIGNATURES)
 
 
+def _declared_params():
+    """{name: [param type strings]} from the header's prototypes."""
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    out = {}
+    for m in re.finditer(r"\b(gatx_[a-z0-9_]+)\s*\(([^)]*)\)\s*;", src):
+        body = " ".join(m.group(2).split())
+        out[m.group(1)] = [] if body in ("", "void") else [p.strip() for p in body.split(",")]
+    return out
+
+
+def _ctype_of(decl: str):
+    """The ctypes class a header parameter must be bound with."""
+    import ctypes as C
+    t = decl.rsplit(" ", 1)[0] if " " in decl else decl
+    if "*" in decl or "gatx_stream_t" in t:
+        return C.c_void_p
+    return {"int": C.c_int, "int64_t": C.c_int64, "uint64_t": C.c_uint64, "float": C.c_float,
+            "size_t": C.c_size_t}[t.replace("const ", "").strip()]
+
+
+def test_ctypes_signatures_match_header_prototypes():
+    """Every binding has the header's arity and parameter types (an ABI drift here would pass
+    garbage pointers to the device)."""
+    from gatx._lib import SIGNATURES
+    params = _declared_params()
+    assert set(params) == set(SIGNATURES)
+    for name, decls in params.items():
+        got = SIGNATURES[name][1]
+        assert len(got) == len(decls), (name, len(got), len(decls))
+        for i, (d, g) in enumerate(zip(decls, got)):
+            assert _ctype_of(d) is g, (name, i, d, g)
+
+
 def test_library_is_gfx950_code_object():
     data = open(LIB, "rb").read()
     assert b"gfx950" in data

@@ -33,7 +33,7 @@ def run_gpu_layer(c, device, with_grads=True, x_grad=True):
         if m["has_bias"]:
             layer.bias_param.copy_(torch.from_numpy(c["bias"]))
     if m["dropout"] > 0:
-        layer._dropout_seed = lambda: m["seed"]
+        layer._dropout_seed = lambda *_: m["seed"]
         layer.train()
     x = torch.from_numpy(np.ascontiguousarray(c["x"])).to(device).requires_grad_(
         with_grads and x_grad)
@@ -399,8 +399,21 @@ def test_errors_mirror_reference(device):
     x = torch.randn(5, 4, device=device)
     with pytest.raises(RuntimeError):
         layer(x, torch.zeros((2, 0), dtype=torch.int64, device=device))
+    # out-of-range ids: the reference raises in index_select. Here |edge_index'| and the id
+    # check live on the device (no host sync in forward): asking for the attention weights
+    # reads them at once; otherwise the device builds an empty graph (no out-of-bounds access)
+    # and the error surfaces at the next host read -- check_pending(), or the next build
     with pytest.raises(IndexError):
-        layer(x, torch.tensor([[0, 7], [1, 2]], device=device))
+        layer(x, torch.tensor([[0, 7], [1, 2]], device=device), return_attention_weights=True)
+    with pytest.raises(RuntimeError):
+        layer(x, torch.tensor([[0, -1], [1, 2]], device=device), return_attention_weights=True)
+    from gatx.graph import check_pending, clear_graph_cache
+    check_pending()
+    out = layer(x, torch.tensor([[0, 9], [1, 2]], device=device))
+    assert out.shape == (5, 6)
+    with pytest.raises(IndexError):
+        check_pending()
+    clear_graph_cache()
     with pytest.raises(RuntimeError):
         layer(x.cpu(), torch.tensor([[0, 1], [1, 2]]))
 

@@ -31,7 +31,8 @@ for f in sorted(glob.glob(os.path.join(base + "_p*", "**", "*counter_collection.
             acc[name]["_dur_us"].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 import json
 label = os.environ.get("PMC_SOURCE", "bench.py --steps 3 --warmup 1")
-out_json = {"source": "rocprofv3 --pmc, " + label + ": " + os.path.basename(base.rstrip("/").rsplit("/pmc", 1)[0]), "kernels": {}}
+out_json = {"source": "rocprofv3 --pmc, " + label + ": " + os.path.basename(base.rstrip("/").rsplit("/pmc", 1)[0]),
+            "steps": int(os.environ.get("PMC_STEPS", "4")), "kernels": {}}
 for n, cs in acc.items():
     d = {k: sum(v) / len(v) for k, v in cs.items()}
     out_json["kernels"][n] = {
