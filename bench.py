@@ -68,13 +68,15 @@ def gemm_roof():
                 kernel="gemm_f32_kernel (v_mfma_f32_32x32x2_f32)")
 
 
-def run_timed(step, steps, world, dev):
+def run_timed(step, steps, world, dev, instr_step=None):
     """The timed region: barrier + synchronize on both sides, max over ranks. Returns (elapsed,
     per-kernel HIP-event records, instrumented step count). Only the last steps // 10 (>= 1)
     steps bracket their launches with HIP events on the launch stream: each timed event record
     costs the stream ~10 us (rocprof traces: 14-16 extra gaps per PPI step when every step was
     bracketed), so instrumenting every step would inflate the headline by 3-6%; this way the
-    kernel timings are live, inside the timed region, at < 1% cost to it."""
+    kernel timings are live, inside the timed region, at < 1% cost to it. With a captured
+    hipGraph `step`, the instrumented steps run `instr_step` (the same step, eagerly): events
+    bracket individual launches, which a graph replay does not expose."""
     from gatx.functional import KernelTimer, set_kernel_timer
     n_instr = max(1, steps // 10)
     timer = KernelTimer()
@@ -85,6 +87,8 @@ def run_timed(step, steps, world, dev):
     for i in range(steps):
         if i == steps - n_instr:
             set_kernel_timer(timer)
+            if instr_step is not None:
+                step = instr_step
         step()
     torch.cuda.synchronize()
     if world > 1:
@@ -403,6 +407,9 @@ def main():
     ap.add_argument("--rmat-edges", type=int, default=160_000_000)
     ap.add_argument("--cached-graph", action="store_true",
                     help="reuse the CSR across steps (excludes graph preprocessing)")
+    ap.add_argument("--hipgraph", choices=["auto", "on", "off"], default="auto",
+                    help="replay each step as one captured hipGraph (gatx.capture). auto: forward "
+                         "steps, and PATTERN training on one GPU")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -441,7 +448,11 @@ def main():
     x = torch.from_numpy(b.x).to(dev)
     ei = torch.from_numpy(b.edge_index).to(dev)
     y = (torch.rand(b.num_nodes, cfg["num_classes"], device=dev) > 0.5).float()
-    opt = torch.optim.Adam(model.parameters(), lr=cfg["learning_rate"])
+    use_graph = args.hipgraph == "on" or (
+        args.hipgraph == "auto" and (args.mode == "fwd" or (ds == "PATTERN" and world == 1)))
+    # a captured training step needs the optimizer's step counter on the device
+    opt = torch.optim.Adam(model.parameters(), lr=cfg["learning_rate"],
+                           capturable=use_graph and args.mode == "train")
     loss_fn = torch.nn.BCEWithLogitsLoss()
     if ds == "PATTERN":   # PatternGAT (models/pattern_gat.py:11-15): class-balanced BCE
         loss_fn = torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([1 / 0.1765], device=dev))
@@ -478,16 +489,21 @@ def main():
         opt.step()
         return out
 
+    eager_step = step
+    if use_graph:
+        from gatx.capture import CapturedStep
+        step = CapturedStep(eager_step)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     from gatx.graph import graph_cache
-    g = graph_cache.get(ei, b.num_nodes, True)
-    E2 = g.num_edges
     N = b.num_nodes
     dims = layer_dims(cfg)
 
-    elapsed, summ, n_instr = run_timed(step, args.steps, world, dev)
+    elapsed, summ, n_instr = run_timed(step, args.steps, world, dev,
+                                       eager_step if use_graph else None)
+    clear_graph_cache()
+    E2 = graph_cache.get(ei, N, True).num_edges
     step_s = elapsed / args.steps
     ms = step_s * 1e3
     layer_edges = len(dims) * E2
@@ -529,7 +545,9 @@ def main():
                                f"{args.graphs} graphs per GPU"
                                + (", CSR cached" if args.cached_graph else ", CSR built per step"),
                    "graphs_per_gpu": args.graphs, "nodes_per_gpu": N, "edges_per_layer": E2,
-                   "parallelism": f"graph-batch dp{world}"},
+                   "parallelism": f"graph-batch dp{world}",
+                   "launch": "hipGraph replay (last steps//10 eager, HIP-event instrumented)"
+                             if use_graph else "eager"},
         "unique_GBps": round(uniq / step_s / 1e9, 1),
         "roofline_time_frac": round(t_roof / step_s, 4),
         "roofline_time_basis": "sum over the forward's kernels of max(unique bytes / 8 TB/s, "

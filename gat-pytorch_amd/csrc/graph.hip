@@ -183,6 +183,77 @@ __global__ void __launch_bounds__(256) iota_kernel(int64_t n, int32_t* out) {
     out[i] = (int32_t)i;
 }
 
+// ------------------------------------------------------------------ stable LSD radix sort
+// (key, value) int32 pairs, keys in [0, 2^bits), 8-bit digits, stable: equal keys keep their
+// input order. Capturable into a hipGraph: no host-side memset or sync anywhere (rocPRIM's
+// onesweep radix sort resets its atomic block-id counter with a synchronous hipMemset on
+// gfx942/gfx950, which a captured graph never replays). Per pass:
+//  * radix_hist: block b counts the digits of its tile of kTile keys (LDS atomics) into
+//    hist[digit * nblocks + b] (digit-major, so one exclusive scan gives every (digit, block)
+//    its output base);
+//  * rocPRIM exclusive_scan (lookback scan, capture-safe) over the 256 * nblocks counts;
+//  * radix_scatter: block b walks its tile in input order, 256 keys per round (4 waves x 64):
+//    a wave ranks lanes with equal digits by 8 ballots (stable: lower lanes first), waves are
+//    ordered through per-(wave, digit) counts in LDS, rounds through running per-digit bases.
+constexpr int kRadixBits = 8, kRadix = 1 << kRadixBits;
+constexpr int kSortItems = 16, kTile = 256 * kSortItems;
+
+__global__ void __launch_bounds__(256) radix_hist_kernel(const int32_t* __restrict__ keys,
+                                                         int64_t n, int shift, int64_t nblocks,
+                                                         uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[kRadix];
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kTile;
+#pragma unroll
+  for (int i = 0; i < kSortItems; ++i) {
+    const int64_t idx = base + i * 256 + threadIdx.x;
+    if (idx < n) atomicAdd(&h[(keys[idx] >> shift) & (kRadix - 1)], 1u);
+  }
+  __syncthreads();
+  hist[(int64_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+}
+
+__global__ void __launch_bounds__(256) radix_scatter_kernel(
+    const int32_t* __restrict__ keys, const int32_t* __restrict__ vals, int64_t n, int shift,
+    int64_t nblocks, const uint32_t* __restrict__ offs, int32_t* __restrict__ keys_out,
+    int32_t* __restrict__ vals_out) {
+  __shared__ uint32_t base[kRadix];
+  __shared__ uint32_t cnt[4][kRadix];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  base[tid] = offs[(int64_t)tid * nblocks + blockIdx.x];
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const int64_t tile = (int64_t)blockIdx.x * kTile;
+  for (int r = 0; r < kSortItems; ++r) {
+    const int64_t idx = tile + r * 256 + tid;
+    const bool valid = idx < n;
+    const int32_t key = valid ? keys[idx] : 0;
+    const int32_t val = valid ? (vals ? vals[idx] : (int32_t)idx) : 0;
+    const int d = (key >> shift) & (kRadix - 1);
+#pragma unroll
+    for (int w = 0; w < 4; ++w) cnt[w][tid] = 0;
+    __syncthreads();
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < kRadixBits; ++b) {
+      const uint64_t bb = __ballot((d >> b) & 1);
+      peers &= ((d >> b) & 1) ? bb : ~bb;
+    }
+    const int rank = __popcll(peers & lt);
+    if (valid && rank == 0) cnt[wave][d] = (uint32_t)__popcll(peers);
+    __syncthreads();
+    if (valid) {
+      uint32_t pos = base[d] + rank;
+      for (int w = 0; w < wave; ++w) pos += cnt[w][d];
+      keys_out[pos] = key;
+      vals_out[pos] = val;
+    }
+    __syncthreads();
+    base[tid] += cnt[0][tid] + cnt[1][tid] + cnt[2][tid] + cnt[3][tid];
+    // the next round's cnt reset comes after a barrier this base update precedes
+  }
+}
+
 inline unsigned grid_for(int64_t n, int block = 256, int64_t cap = 16384) {
   int64_t g = ceil_div(n > 0 ? n : 1, block);
   return (unsigned)(g < cap ? g : cap);
@@ -205,12 +276,73 @@ size_t scan_bytes(int64_t E) {
   return bytes;
 }
 
-size_t sort_bytes(int64_t n, unsigned bits) {  // bits: key range [0, 2^bits)
+// ---- the radix sort's host side (workspace layout and passes)
+struct SortWs {
+  uint32_t* hist;
+  uint32_t* offs;
+  int32_t* tk;
+  int32_t* tv;
+  void* scan_tmp;
+  size_t scan_bytes;
+};
+
+size_t radix_scan_bytes(int64_t m) {
   size_t bytes = 0;
-  (void)rocprim::radix_sort_pairs(nullptr, bytes, (int32_t*)nullptr, (int32_t*)nullptr,
-                            (int32_t*)nullptr, (int32_t*)nullptr, (unsigned)(n > 0 ? n : 1), 0,
-                            bits, (hipStream_t)0);
+  (void)rocprim::exclusive_scan(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                0u, (size_t)(m > 0 ? m : 1), rocprim::plus<uint32_t>(),
+                                (hipStream_t)0);
   return bytes;
+}
+
+size_t sort_bytes(int64_t n, unsigned bits) {  // keys in [0, 2^bits)
+  (void)bits;
+  const int64_t nb = ceil_div(n > 0 ? n : 1, kTile), m = nb * kRadix;
+  return 2 * align256(sizeof(uint32_t) * m) + 2 * align256(sizeof(int32_t) * (n > 0 ? n : 1)) +
+         align256(radix_scan_bytes(m)) + 256;
+}
+
+SortWs carve_sort(void* ws, int64_t n) {
+  const int64_t nb = ceil_div(n > 0 ? n : 1, kTile), m = nb * kRadix;
+  char* p = (char*)ws;
+  SortWs w;
+  w.hist = (uint32_t*)p; p += align256(sizeof(uint32_t) * m);
+  w.offs = (uint32_t*)p; p += align256(sizeof(uint32_t) * m);
+  w.tk = (int32_t*)p; p += align256(sizeof(int32_t) * (n > 0 ? n : 1));
+  w.tv = (int32_t*)p; p += align256(sizeof(int32_t) * (n > 0 ? n : 1));
+  w.scan_tmp = p;
+  w.scan_bytes = radix_scan_bytes(m);
+  return w;
+}
+
+// keys_in -> (keys_out, vals_out) sorted stably by key; vals_in NULL = the identity (input
+// positions). Passes alternate between the output and the workspace pair so the last one lands
+// in the output.
+int sort_pairs(const int32_t* keys_in, const int32_t* vals_in, int32_t* keys_out,
+               int32_t* vals_out, int64_t n, unsigned bits, void* ws, hipStream_t stream) {
+  if (n <= 0) return 0;
+  GATX_REQUIRE(n < (1ll << 31), "sort: too many keys");
+  const SortWs w = carve_sort(ws, n);
+  const int64_t nb = ceil_div(n, kTile), m = nb * kRadix;
+  const int passes = (int)ceil_div((int64_t)(bits > 0 ? bits : 1), kRadixBits);
+  const int32_t* ck = keys_in;
+  const int32_t* cv = vals_in;
+  for (int ps = 0; ps < passes; ++ps) {
+    const bool to_out = ((passes - 1 - ps) % 2) == 0;
+    int32_t* ok = to_out ? keys_out : w.tk;
+    int32_t* ov = to_out ? vals_out : w.tv;
+    const int shift = ps * kRadixBits;
+    radix_hist_kernel<<<(unsigned)nb, 256, 0, stream>>>(ck, n, shift, nb, w.hist);
+    GATX_LAUNCH_CHECK("radix_hist");
+    size_t b = w.scan_bytes;
+    hipError_t r = rocprim::exclusive_scan(w.scan_tmp, b, w.hist, w.offs, 0u, (size_t)m,
+                                           rocprim::plus<uint32_t>(), stream);
+    if (r != hipSuccess) { set_error("radix scan: %s", hipGetErrorString(r)); return (int)r; }
+    radix_scatter_kernel<<<(unsigned)nb, 256, 0, stream>>>(ck, cv, n, shift, nb, w.offs, ok, ov);
+    GATX_LAUNCH_CHECK("radix_scatter");
+    ck = ok;
+    cv = ov;
+  }
+  return 0;
 }
 
 template <typename I>
@@ -243,10 +375,7 @@ int graph_build_impl(const void* ei, int64_t E, int64_t ld, int add_loops, int64
     GATX_LAUNCH_CHECK("compact");
   }
   if (E_bound > 0) {
-    size_t b = tmp_bytes;
-    hipError_t r = rocprim::radix_sort_pairs(tmp, b, dst32, rowidx, iota, perm,
-                                             (unsigned)E_bound, 0, bits_for(N + 1), stream);
-    if (r != hipSuccess) { set_error("radix_sort: %s", hipGetErrorString(r)); return (int)r; }
+    GATX_CALL(sort_pairs(dst32, iota, rowidx, perm, E_bound, bits_for(N + 1), tmp, stream));
     gather_kernel<<<grid_for(E_bound), 256, 0, stream>>>(src32, perm, E_bound, col);
     GATX_LAUNCH_CHECK("gather col");
   }
@@ -327,10 +456,7 @@ extern "C" int gatx_graph_transpose(const int32_t* col, const int32_t* rowidx, i
     tkeys_kernel<<<grid_for(E_bound), 256, 0, stream>>>(col, (const long long*)e2, E_bound, N,
                                                         keys, iota);
     GATX_LAUNCH_CHECK("tkeys");
-    size_t b = ws_bytes - used;
-    hipError_t r = rocprim::radix_sort_pairs((void*)p, b, keys, skeys, iota, seid,
-                                             (unsigned)E_bound, 0, bits_for(N + 1), stream);
-    if (r != hipSuccess) { set_error("radix_sort: %s", hipGetErrorString(r)); return (int)r; }
+    GATX_CALL(sort_pairs(keys, iota, skeys, seid, E_bound, bits_for(N + 1), (void*)p, stream));
   }
   rowptr_kernel<<<grid_for(E_bound + 1), 256, 0, stream>>>(skeys, E_bound, N, srowptr);
   GATX_LAUNCH_CHECK("srowptr");

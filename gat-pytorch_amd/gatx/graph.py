@@ -143,7 +143,8 @@ class Graph:
         """Validate without blocking if the device has produced the meta (raises on bad ids)."""
         if self._error is not None:
             raise self._error
-        if self._E2 is None and self._event is not None and self._event.query():
+        if (self._E2 is None and self._event is not None
+                and not torch.cuda.is_current_stream_capturing() and self._event.query()):
             self._validate(self._meta_host)
 
     # ---- host-side sizes (synchronise on first use)
