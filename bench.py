@@ -451,7 +451,10 @@ def main():
     use_graph = args.hipgraph == "on" or (
         args.hipgraph == "auto" and (args.mode == "fwd" or (ds == "PATTERN" and world == 1)))
     # a captured training step needs the optimizer's step counter on the device
-    opt = torch.optim.Adam(model.parameters(), lr=cfg["learning_rate"],
+    # torch's fused Adam (one launch for all parameters; same update rule as the reference's
+    # Adam, models/*_gat.py configure_optimizers); a captured step needs capturable state
+    opt = torch.optim.Adam(model.parameters(), lr=cfg["learning_rate"], fused=True,
+                           weight_decay=cfg["l2_reg"],
                            capturable=use_graph and args.mode == "train")
     loss_fn = torch.nn.BCEWithLogitsLoss()
     if ds == "PATTERN":   # PatternGAT (models/pattern_gat.py:11-15): class-balanced BCE

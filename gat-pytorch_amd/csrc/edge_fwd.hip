@@ -139,6 +139,10 @@ struct EdgeFwdArgs {
   int lds_row;
   int64_t chunk;           // destination nodes per (chunk, head-group) sweep
   int64_t n_items;
+  int g_begin, g_count;    // head groups [g_begin, g_begin + g_count) in this launch
+  int mean_mode;           // head mean: 0 all heads in one pass; multi-pass over head groups:
+                           // 1 first (out = group sum), 2 middle (out += group sum),
+                           // 3 last (out = epilogue((out + group sum) / NH + bias))
   int vec_out;             // concat output / resid rows float4-aligned (F % 4 == 0)
   int dbg;                 // diagnostic ablations (gatx_set_debug); 0 in production
 };
@@ -186,11 +190,12 @@ __global__ void __launch_bounds__(256) edge_forward_kernel(EdgeFwdArgs g) {
   const int grp = lane / LPE, li = lane % LPE;
   const int64_t item = xcd_contiguous(blockIdx.x, gridDim.x) * 4 + wave;
   if (item >= g.n_items) return;
-  const int NG = g.NH / g.HS;
+  const int NG = g.g_count;
   const int64_t per_chunk = g.chunk * NG;
   const int64_t ck = item / per_chunk, rem = item - ck * per_chunk;
-  const int hg = (int)(rem / g.chunk);
-  const int64_t n = ck * g.chunk + (rem - (int64_t)hg * g.chunk);
+  const int hgl = (int)(rem / g.chunk);
+  const int64_t n = ck * g.chunk + (rem - (int64_t)hgl * g.chunk);
+  const int hg = g.g_begin + hgl;
   if (n >= g.N) return;
   const int h0 = hg * g.HS, HS = g.HS;
   const int NH = g.NH, F = g.F, Fp = g.Fp, F4 = Fp / 4, S2 = 2 * NH;
@@ -376,12 +381,20 @@ __global__ void __launch_bounds__(256) edge_forward_kernel(EdgeFwdArgs g) {
     }
   }
   wave_lds_sync();
-  if (!g.concat) {   // head mean (HS == NH)
+  if (!g.concat) {   // head mean over this item's HS heads (all NH when mean_mode == 0)
     const float inv_nh = 1.f / (float)NH;
+    float* orow = g.out + n * g.out_ld;
     for (int f = lane; f < F; f += 64) {
       float sum = 0.f;
-      for (int h = 0; h < NH; ++h) sum += row_lds[h * Fp + f];
-      g.out[n * g.out_ld + f] = epilogue(sum * inv_nh + (g.bias ? g.bias[f] : 0.f), g, n, f);
+      for (int h = 0; h < HS; ++h) sum += row_lds[h * Fp + f];
+      if (g.mean_mode == 1) {
+        orow[f] = sum;
+      } else if (g.mean_mode == 2) {
+        orow[f] += sum;
+      } else {
+        if (g.mean_mode == 3) sum += orow[f];
+        orow[f] = epilogue(sum * inv_nh + (g.bias ? g.bias[f] : 0.f), g, n, f);
+      }
     }
   }
   if (lane < HS) g.den[n * NH + h0 + lane] = den_lds[lane];
@@ -897,7 +910,8 @@ extern "C" size_t gatx_attention_max_workspace_bytes(void) { return sizeof(float
 extern "C" int gatx_edge_forward_ex(
     const float* rows, int64_t row_stride, int64_t head_stride, const float* S,
     const uint32_t* M_ord, const int32_t* rowptr, const int32_t* col, const int32_t* perm,
-    int64_t N, int NH, int F, int heads_per_item, int concat, int const_att, const float* bias,
+    int64_t N, int NH, int F, int heads_per_item, int group_begin, int group_count,
+    int mean_mode, int concat, int const_att, const float* bias,
     float p, const uint64_t* seed, float* out, int64_t out_ld, const float* resid, int64_t resid_ld,
     int elu, float* den, int64_t chunk, gatx_stream_t s) {
   hipStream_t st = (hipStream_t)s;
@@ -906,7 +920,17 @@ extern "C" int gatx_edge_forward_ex(
                "edge_forward: bias with head-mean needs num_heads == 1");
   const int HS = heads_per_item <= 0 ? NH : heads_per_item;
   GATX_REQUIRE(NH % HS == 0, "edge_forward: heads_per_item must divide num_heads");
-  GATX_REQUIRE(concat || HS == NH, "edge_forward: head-mean needs all heads in one item");
+  const int NGall = NH / HS;
+  if (group_count <= 0) { group_begin = 0; group_count = NGall; }
+  GATX_REQUIRE(group_begin >= 0 && group_begin + group_count <= NGall,
+               "edge_forward: head groups out of range");
+  GATX_REQUIRE(mean_mode >= 0 && mean_mode <= 3, "edge_forward: bad mean_mode");
+  GATX_REQUIRE(concat || (mean_mode == 0 ? HS == NH : group_count == 1),
+               "edge_forward: head mean in one pass needs all heads in one item, multi-pass "
+               "one head group per launch");
+  GATX_REQUIRE(!concat || mean_mode == 0, "edge_forward: mean_mode needs concat == 0");
+  GATX_REQUIRE(mean_mode == 0 || mean_mode == 3 || (resid == nullptr && !elu && !bias),
+               "edge_forward: the epilogue belongs to the last head-mean pass");
   GATX_REQUIRE(row_stride % 4 == 0 && head_stride % 4 == 0 && ((uintptr_t)rows % 16) == 0,
                "edge_forward: source rows must be float4-aligned");
   GATX_REQUIRE(p >= 0.f && p < 1.f, "edge_forward: dropout must be in [0, 1)");
@@ -930,7 +954,8 @@ extern "C" int gatx_edge_forward_ex(
   g.lds_row = (int)round_up((int64_t)HS * Fp + HS + 64 + (int64_t)HS * 64, 4);
   g.chunk = chunk > 0 ? chunk : 2048;
   g.dbg = g_debug;
-  g.n_items = ceil_div(N, g.chunk) * g.chunk * (NH / HS);
+  g.g_begin = group_begin; g.g_count = group_count; g.mean_mode = concat ? 0 : mean_mode;
+  g.n_items = ceil_div(N, g.chunk) * g.chunk * group_count;
   const size_t lds = (size_t)4 * g.lds_row * sizeof(float);
   GATX_REQUIRE(lds <= 160 * 1024, "edge_forward: row too wide for LDS staging");
   const int64_t blocks = ceil_div(g.n_items, 4);
@@ -960,7 +985,7 @@ extern "C" int gatx_edge_forward(const float* Wh, const float* S, const uint32_t
                                  int64_t* argmax, gatx_stream_t s) {
   const int64_t Fp = round_up(F, 4);
   GATX_CALL(gatx_edge_forward_ex(Wh, NH * Fp, Fp, S, M_ord, rowptr, col, perm, N, NH, F,
-                                 concat ? 0 : NH, concat, const_att, bias, p, seed, out,
+                                 concat ? 0 : NH, 0, 0, 0, concat, const_att, bias, p, seed, out,
                                  concat ? (int64_t)NH * F : F, nullptr, 0, 0, den, 0, s));
   return gatx_attention_alpha(col, rowidx, perm, E2, S, M_ord, den, NH, const_att,
                               alpha, argmax, s);

@@ -284,15 +284,17 @@ int64_t resident_blocks(const Kind& kd) {
 
 // Split K when the output alone cannot fill the chip (g_W = G^T x: ~70 tiles, K = #nodes):
 // the most slices (<= 64) with tiles * slices still within one resident wave, each slice
-// >= 512 k, or >= 128 k when even that leaves fewer than 16 slices. A lone workgroup walking a
+// >= 512 k, or >= 128 k (64 k for <= 4 tiles) when that leaves fewer than 16 slices. A lone
+// workgroup walking a
 // long K is latency-bound: PATTERN's weight gradients (one 128 x 128 tile, K = 951 nodes) took
-// 60-74 us as one workgroup (~1 us per K-tile).
+// 60-74 us as one workgroup (~1 us per K-tile), 15 us in 6 slices of 160.
 int choose_splits(int64_t tiles, int64_t K, int64_t slots) {
   int s = 1;
   while ((s + 1) * tiles <= slots && K / (s + 1) >= 512 && s < 64) ++s;
   if (s < 16) {
+    const int64_t min_k = tiles <= 4 ? 64 : 128;
     int t = s;
-    while ((t + 1) * tiles <= slots && K / (t + 1) >= 128 && t < 16) ++t;
+    while ((t + 1) * tiles <= slots && K / (t + 1) >= min_k && t < 16) ++t;
     s = t;
   }
   return s;

@@ -188,7 +188,7 @@ __global__ void __launch_bounds__(256) iota_kernel(int64_t n, int32_t* out) {
 // input order. Capturable into a hipGraph: no host-side memset or sync anywhere (rocPRIM's
 // onesweep radix sort resets its atomic block-id counter with a synchronous hipMemset on
 // gfx942/gfx950, which a captured graph never replays). Per pass:
-//  * radix_hist: block b counts the digits of its tile of kTile keys (LDS atomics) into
+//  * radix_hist: block b counts the digits of its tile of 256 * items keys (LDS atomics) into
 //    hist[digit * nblocks + b] (digit-major, so one exclusive scan gives every (digit, block)
 //    its output base);
 //  * rocPRIM exclusive_scan (lookback scan, capture-safe) over the 256 * nblocks counts;
@@ -196,17 +196,25 @@ __global__ void __launch_bounds__(256) iota_kernel(int64_t n, int32_t* out) {
 //    a wave ranks lanes with equal digits by 8 ballots (stable: lower lanes first), waves are
 //    ordered through per-(wave, digit) counts in LDS, rounds through running per-digit bases.
 constexpr int kRadixBits = 8, kRadix = 1 << kRadixBits;
-constexpr int kSortItems = 16, kTile = 256 * kSortItems;
+constexpr int kMaxSortItems = 16;
+
+// keys per thread per block: up to 16, but at least ~256 blocks — a block walks its tile in
+// serial rounds, so small sorts (PATTERN: 50 k keys) need short tiles to fill the chip
+inline int sort_items(int64_t n) {
+  int it = kMaxSortItems;
+  while (it > 1 && ceil_div(n, 256 * it) < 256) it >>= 1;
+  return it;
+}
 
 __global__ void __launch_bounds__(256) radix_hist_kernel(const int32_t* __restrict__ keys,
-                                                         int64_t n, int shift, int64_t nblocks,
+                                                         int64_t n, int shift, int items,
+                                                         int64_t nblocks,
                                                          uint32_t* __restrict__ hist) {
   __shared__ uint32_t h[kRadix];
   h[threadIdx.x] = 0;
   __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * kTile;
-#pragma unroll
-  for (int i = 0; i < kSortItems; ++i) {
+  const int64_t base = (int64_t)blockIdx.x * 256 * items;
+  for (int i = 0; i < items; ++i) {
     const int64_t idx = base + i * 256 + threadIdx.x;
     if (idx < n) atomicAdd(&h[(keys[idx] >> shift) & (kRadix - 1)], 1u);
   }
@@ -216,15 +224,15 @@ __global__ void __launch_bounds__(256) radix_hist_kernel(const int32_t* __restri
 
 __global__ void __launch_bounds__(256) radix_scatter_kernel(
     const int32_t* __restrict__ keys, const int32_t* __restrict__ vals, int64_t n, int shift,
-    int64_t nblocks, const uint32_t* __restrict__ offs, int32_t* __restrict__ keys_out,
+    int items, int64_t nblocks, const uint32_t* __restrict__ offs, int32_t* __restrict__ keys_out,
     int32_t* __restrict__ vals_out) {
   __shared__ uint32_t base[kRadix];
   __shared__ uint32_t cnt[4][kRadix];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   base[tid] = offs[(int64_t)tid * nblocks + blockIdx.x];
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  const int64_t tile = (int64_t)blockIdx.x * kTile;
-  for (int r = 0; r < kSortItems; ++r) {
+  const int64_t tile = (int64_t)blockIdx.x * 256 * items;
+  for (int r = 0; r < items; ++r) {
     const int64_t idx = tile + r * 256 + tid;
     const bool valid = idx < n;
     const int32_t key = valid ? keys[idx] : 0;
@@ -296,13 +304,13 @@ size_t radix_scan_bytes(int64_t m) {
 
 size_t sort_bytes(int64_t n, unsigned bits) {  // keys in [0, 2^bits)
   (void)bits;
-  const int64_t nb = ceil_div(n > 0 ? n : 1, kTile), m = nb * kRadix;
+  const int64_t nb = ceil_div(n > 0 ? n : 1, 256 * sort_items(n)), m = nb * kRadix;
   return 2 * align256(sizeof(uint32_t) * m) + 2 * align256(sizeof(int32_t) * (n > 0 ? n : 1)) +
          align256(radix_scan_bytes(m)) + 256;
 }
 
 SortWs carve_sort(void* ws, int64_t n) {
-  const int64_t nb = ceil_div(n > 0 ? n : 1, kTile), m = nb * kRadix;
+  const int64_t nb = ceil_div(n > 0 ? n : 1, 256 * sort_items(n)), m = nb * kRadix;
   char* p = (char*)ws;
   SortWs w;
   w.hist = (uint32_t*)p; p += align256(sizeof(uint32_t) * m);
@@ -322,7 +330,8 @@ int sort_pairs(const int32_t* keys_in, const int32_t* vals_in, int32_t* keys_out
   if (n <= 0) return 0;
   GATX_REQUIRE(n < (1ll << 31), "sort: too many keys");
   const SortWs w = carve_sort(ws, n);
-  const int64_t nb = ceil_div(n, kTile), m = nb * kRadix;
+  const int items = sort_items(n);
+  const int64_t nb = ceil_div(n, 256 * items), m = nb * kRadix;
   const int passes = (int)ceil_div((int64_t)(bits > 0 ? bits : 1), kRadixBits);
   const int32_t* ck = keys_in;
   const int32_t* cv = vals_in;
@@ -331,13 +340,14 @@ int sort_pairs(const int32_t* keys_in, const int32_t* vals_in, int32_t* keys_out
     int32_t* ok = to_out ? keys_out : w.tk;
     int32_t* ov = to_out ? vals_out : w.tv;
     const int shift = ps * kRadixBits;
-    radix_hist_kernel<<<(unsigned)nb, 256, 0, stream>>>(ck, n, shift, nb, w.hist);
+    radix_hist_kernel<<<(unsigned)nb, 256, 0, stream>>>(ck, n, shift, items, nb, w.hist);
     GATX_LAUNCH_CHECK("radix_hist");
     size_t b = w.scan_bytes;
     hipError_t r = rocprim::exclusive_scan(w.scan_tmp, b, w.hist, w.offs, 0u, (size_t)m,
                                            rocprim::plus<uint32_t>(), stream);
     if (r != hipSuccess) { set_error("radix scan: %s", hipGetErrorString(r)); return (int)r; }
-    radix_scatter_kernel<<<(unsigned)nb, 256, 0, stream>>>(ck, cv, n, shift, nb, w.offs, ok, ov);
+    radix_scatter_kernel<<<(unsigned)nb, 256, 0, stream>>>(ck, cv, n, shift, items, nb, w.offs,
+                                                           ok, ov);
     GATX_LAUNCH_CHECK("radix_scatter");
     ck = ok;
     cv = ov;

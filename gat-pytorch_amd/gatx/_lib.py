@@ -45,7 +45,8 @@ SIGNATURES = {
                                     c_i64, c_i64, c_i64, P, c_i64, c_i64, c_i, P, c_i64, P, c_i64,
                                     c_i64, c_i, P]),
     "gatx_edge_forward_ex": (c_i, [P, c_i64, c_i64, P, P, P, P, P, c_i64, c_i, c_i, c_i, c_i, c_i,
-                                   P, c_f, P, P, c_i64, P, c_i64, c_i, P, c_i64, P]),
+                                   c_i, c_i, c_i, P, c_f, P, P, c_i64, P, c_i64, c_i, P, c_i64,
+                                   P]),
     "gatx_pad_rows": (c_i, [P, c_i64, c_i64, c_i64, P, c_i64, P]),
     "gatx_projection_gemm": (c_i, [c_i64, c_i64, c_i64, P, c_i64, c_i64, P, c_i64, c_i64, P,
                                    c_i64, c_i64, P, c_i64, P, c_sz, P]),

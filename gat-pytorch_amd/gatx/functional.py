@@ -200,26 +200,42 @@ def _attention_alpha(graph: Graph, S, M_ord, den, sh: "LayerShape", alpha, argma
          ptr(alpha), ptr(argmax), s)
 
 
+_TUNE: dict = {}
+
+
 def _env_int(name: str, default: int) -> int:
-    import os
-    v = os.environ.get(name)
-    return int(v) if v not in (None, "") else default
+    """Tuning switches (GATX_*), read from the environment once per process (the forward's
+    per-call path stays free of os.environ lookups); reset_tuning() re-reads them."""
+    v = _TUNE.get(name)
+    if v is None:
+        import os
+        e = os.environ.get(name)
+        v = _TUNE[name] = int(e) if e not in (None, "") else None
+    return default if v is None else v
+
+
+def reset_tuning():
+    _TUNE.clear()
 
 
 def edge_heads_per_item(sh: LayerShape) -> int:
-    """Heads per edge work item: one head per item when a head's row slice is >= 256 B (its
-    per-graph working set then fits one XCD's L2); otherwise the largest divisor of NH that is
-    <= 8 (the batch phase keeps the item's heads in registers). Head-mean layers need all heads
-    in one item (NH <= 8)."""
+    """Heads per edge work item: ~256+ floats of gathered row per item, so one XCD's L2 holds
+    the sweep's slice of the rows (measured inside the PPI forward: 1 head of 256 per item beats
+    2 and 4); the largest divisor of NH up to 8 (the batch phase keeps the item's heads in
+    registers). Head-mean layers use the same rule: a head group smaller than NH runs as one
+    launch per group, accumulating into the output in stream order (PPI L2: 6 heads x 124
+    floats -> 3 groups of 2, each group's per-graph slice ~2.2 MB instead of 6.7 MB)."""
     hs = _env_int("GATX_HEADS_PER_ITEM", 0)
-    if hs > 0 and sh.NH % hs == 0 and hs <= 8 and (sh.concat or hs == sh.NH):
+    if hs > 0 and sh.NH % hs == 0 and hs <= 8:
         return hs
     if not sh.concat:
-        if sh.NH > 8:
-            raise RuntimeError("gatx: head-mean layers support at most 8 heads")
-        return sh.NH
-    # ~256+ floats of row per item: one XCD's L2 holds the sweep's slice of the rows (measured
-    # inside the PPI forward: 1 head of 256 per item beats 2 and 4)
+        hm = _env_int("GATX_MEAN_HEADS", 0)
+        if hm > 0 and sh.NH % hm == 0 and hm <= 8:
+            return hm
+        # measured at PPI L2 (6 x 124 floats), edge pass per step: groups of 6 / 3 / 2 / 1
+        # heads 0.608 / 0.580 / 0.596 / 0.688 ms (the pass is bound by L2->CU gather bandwidth,
+        # ~16 TB/s, more than by HBM): ~384 floats of row per group
+        return max(d for d in range(1, 9) if sh.NH % d == 0 and d * sh.Fp <= max(384, sh.Fp))
     return max(d for d in range(1, 9) if sh.NH % d == 0 and d * sh.Fp <= max(256, sh.Fp))
 
 
@@ -289,7 +305,8 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
         with _span("edge_forward", (N, E2, sh.NH, Fin_p, "x")):
             hs_x = reassoc_heads_per_item(sh)   # heads sharing one x row
             call("gatx_edge_forward_ex", ptr(x_rows), Fin_p, 0, ptr(S), ptr(M_ord),
-                 ptr(graph.rowptr), ptr(graph.col), ptr(graph.perm), N, sh.NH, Fin_p, hs_x, 1,
+                 ptr(graph.rowptr), ptr(graph.col), ptr(graph.perm), N, sh.NH, Fin_p, hs_x,
+                 0, 0, 0, 1,
                  int(sh.const), None, float(p), ptr(seed), ptr(Z), sh.NH * Fin_p, None, 0, 0,
                  ptr(den), chunk, s)
         with _span("attention_alpha", (E2, sh.NH)):
@@ -320,11 +337,22 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
             call("gatx_attention_max", ptr(graph.col), ptr(graph.rowidx), E2, graph.e2_ptr,
                  ptr(S), sh.NH, ptr(M_ord), ptr(argmax), ptr(_max_ws(dev)), s)
     with _span("edge_forward", (N, E2, sh.NH, sh.F, sh.concat)):
-        call("gatx_edge_forward_ex", ptr(Wh), sh.Dp, sh.Fp, ptr(S), ptr(M_ord),
-             ptr(graph.rowptr), ptr(graph.col), ptr(graph.perm), N, sh.NH, sh.F,
-             edge_heads_per_item(sh), int(sh.concat), int(sh.const), ptr(bias), float(p),
-             ptr(seed),
-             ptr(out), sh.out_cols, resid_p, sh.out_cols, int(elu), ptr(den), chunk, s)
+        hs = edge_heads_per_item(sh)
+        ng = sh.NH // hs
+        if sh.concat or ng == 1:
+            call("gatx_edge_forward_ex", ptr(Wh), sh.Dp, sh.Fp, ptr(S), ptr(M_ord),
+                 ptr(graph.rowptr), ptr(graph.col), ptr(graph.perm), N, sh.NH, sh.F, hs,
+                 0, 0, 0, int(sh.concat), int(sh.const), ptr(bias), float(p), ptr(seed),
+                 ptr(out), sh.out_cols, resid_p, sh.out_cols, int(elu), ptr(den), chunk, s)
+        else:   # head mean over groups: one launch per group, accumulated in stream order
+            for gi in range(ng):
+                last = gi == ng - 1
+                mode = 1 if gi == 0 else (3 if last else 2)
+                call("gatx_edge_forward_ex", ptr(Wh), sh.Dp, sh.Fp, ptr(S), ptr(M_ord),
+                     ptr(graph.rowptr), ptr(graph.col), ptr(graph.perm), N, sh.NH, sh.F, hs,
+                     gi, 1, mode, 0, int(sh.const), ptr(bias) if last else None, float(p),
+                     ptr(seed), ptr(out), sh.out_cols, resid_p if last else None, sh.out_cols,
+                     int(elu) if last else 0, ptr(den), chunk, s)
     with _span("attention_alpha", (E2, sh.NH)):
         _attention_alpha(graph, S, M_ord, den, sh, alpha, argmax, s)
     saved.update(Wh=Wh, S=S, reassoc=False)

@@ -187,14 +187,20 @@ int gatx_edge_forward(const float* Wh, const float* S, const uint32_t* M_ord,
  * h*head_stride (+ f): row_stride = Dp, head_stride = Fp for Wh; for the reassociated first
  * layer rows = x padded to Fp = round_up(F_in, 4) with head_stride = 0, so the pass aggregates
  * Z[n,h,:] = sum alpha~ x[src,:] (F = that Fp). One work item is (node, group of heads_per_item
- * heads) (<= 0: all heads; at most 8; head-mean needs all heads); items are swept in chunks of
- * `chunk` nodes per head group (<= 0: 2048) so one XCD's L2 holds one head's slice of the rows.
+ * heads) (<= 0: all heads; at most 8); items are swept in chunks of `chunk` nodes per head group
+ * (<= 0: 2048) so one XCD's L2 holds one head group's slice of the rows. A launch covers head
+ * groups [group_begin, group_begin + group_count) (group_count <= 0: all).
+ * Head mean (concat 0): mean_mode 0 = all heads in one item (heads_per_item = NH); otherwise one
+ * head group per launch, launched in order over the groups: 1 = first (out = the group's head
+ * sum), 2 = middle (out += it), 3 = last (out = epilogue((out + it) / NH + bias)) — NH > 8, or
+ * smaller groups whose row slices stay L2-resident; each pass is deterministic, in stream order.
  * out rows are out_ld floats apart; fused epilogue out = elu?(agg + bias + resid) with resid
  * [N][resid_ld] (nullable) and elu in {0, 1} (GATModel's skip-add + ELU). Writes den. */
 int gatx_edge_forward_ex(const float* rows, int64_t row_stride, int64_t head_stride,
                          const float* S, const uint32_t* M_ord, const int32_t* rowptr,
                          const int32_t* col, const int32_t* perm, int64_t num_nodes, int NH,
-                         int F, int heads_per_item, int concat, int const_attention,
+                         int F, int heads_per_item, int group_begin, int group_count,
+                         int mean_mode, int concat, int const_attention,
                          const float* bias, float dropout_p, const uint64_t* seed, float* out,
                          int64_t out_ld, const float* resid, int64_t resid_ld, int elu,
                          float* den, int64_t chunk, gatx_stream_t stream);

@@ -20,3 +20,17 @@ def device():
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     return torch.device("cuda:0")
+
+
+@pytest.fixture(autouse=True)
+def _fresh_tuning():
+    """gatx reads its GATX_* tuning switches once per process; tests that monkeypatch them get a
+    fresh read."""
+    try:
+        from gatx import functional
+    except Exception:   # library not built: the tests that need it fail on their own
+        yield
+        return
+    functional.reset_tuning()
+    yield
+    functional.reset_tuning()

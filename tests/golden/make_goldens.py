@@ -238,7 +238,41 @@ def main(models_only=False):
     run_layer_case("edge_odd_widths", rng_x(70, 13, 81), ei, 13, 7, 5, True,
                    gdata.xavier_uniform(82, 35, 13), gdata.xavier_uniform(83, 5, 70))
 
+    extra_cases()
     model_cases(sd_pat)
+
+
+def extra_cases():
+    """Round-2 additions: head-mean layers with more than 8 heads (gat_layer.py:132 accepts any
+    NH; the HIP path runs them as head groups accumulated in stream order), and the Citeseer /
+    Pubmed trained checkpoints (data_utils.py:36-47) through the layer: Citeseer L0
+    (3703 -> 8 x 8 concat), Pubmed L0 (500 -> 8 x 8) and Pubmed's 8-head MEAN output layer
+    (64 -> 8 x 3, mean) on synthetic graphs of the datasets' sizes (PyG stats)."""
+    g = dict(G=2, n=100, e=1500, in_features=24, feature_seed=17)
+    xx, ee = gen_batch(g)
+    run_layer_case("mean_nh12", xx, ee, 24, 16, 12, False, gdata.xavier_uniform(110, 192, 24),
+                   gdata.xavier_uniform(111, 12, 12 * 32), gen=g, wgen=[110, 111])
+    g = dict(G=2, n=90, e=1400, in_features=20, feature_seed=18)
+    xx, ee = gen_batch(g)
+    run_layer_case("mean_nh16", xx, ee, 20, 9, 16, False, gdata.xavier_uniform(112, 144, 20),
+                   gdata.xavier_uniform(113, 16, 16 * 18), gen=g, wgen=[112, 113])
+    sd_cs = read_state_dict(f"{CKPT}/Citeseer-100epochs.ckpt")
+    sd_pm = read_state_dict(f"{CKPT}/Pubmed-100epochs.ckpt")
+    gen = dict(G=1, n=3327, e=9104, in_features=3703, features="bernoulli", feature_seed=19)
+    x, ei = gen_batch(gen)
+    run_layer_case("citeseer_l0_trained", x, ei, 3703, 8, 8, True,
+                   sd_cs["gat_layer_list.0.W.weight"], sd_cs["gat_layer_list.0.a.weight"],
+                   gen=gen)
+    gen = dict(G=1, n=19717, e=88648, in_features=500, feature_seed=20)
+    x, ei = gen_batch(gen)
+    run_layer_case("pubmed_l0_trained", x, ei, 500, 8, 8, True,
+                   sd_pm["gat_layer_list.0.W.weight"], sd_pm["gat_layer_list.0.a.weight"],
+                   gen=gen)
+    gen = dict(G=1, n=19717, e=88648, in_features=64, feature_seed=21)
+    x, ei = gen_batch(gen)
+    run_layer_case("pubmed_l1_mean_trained", x, ei, 64, 3, 8, False,
+                   sd_pm["gat_layer_list.1.W.weight"], sd_pm["gat_layer_list.1.a.weight"],
+                   gen=gen)
 
 
 def model_cases(sd_pat):
@@ -313,4 +347,8 @@ def model_case(name, x, ei, gen, layers, skips, dataset, wgen=None):
 
 
 if __name__ == "__main__":
-    main(models_only="--models-only" in sys.argv)
+    if "--extra-only" in sys.argv:
+        torch.set_num_threads(8)
+        extra_cases()
+    else:
+        main(models_only="--models-only" in sys.argv)
