@@ -400,9 +400,13 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--attention-penalty", type=float, default=0.0,
                     help="PPI_GAT attention_penalty (train mode)")
-    ap.add_argument("--workload", choices=["ppi", "pattern", "rmat"], default="ppi",
+    ap.add_argument("--attention-reward", type=float, default=0.0,
+                    help="PlanetoidGAT attention_reward (train mode; the norm term is always added)")
+    ap.add_argument("--workload", choices=["ppi", "pattern", "rmat", "cora", "citeseer",
+                                           "pubmed"], default="ppi",
                     help="ppi: the BASELINE metric; pattern: config 4 (batch-sharded PATTERN "
-                         "training); rmat: config 5")
+                         "training); rmat: config 5; cora/citeseer/pubmed: the transductive "
+                         "PlanetoidGAT step (one graph; with --gpus N, N replicas)")
     ap.add_argument("--rmat-nodes", type=int, default=10_000_000)
     ap.add_argument("--rmat-edges", type=int, default=160_000_000)
     ap.add_argument("--cached-graph", action="store_true",
@@ -437,7 +441,14 @@ def main():
     from gatx.config import data_config
     from gatx.distributed import GradientAllReducer, count_weight
 
-    ds = "PATTERN" if args.workload == "pattern" else "PPI"
+    ds = {"pattern": "PATTERN", "ppi": "PPI", "cora": "Cora", "citeseer": "Citeseer",
+          "pubmed": "Pubmed"}[args.workload]
+    planetoid = ds in ("Cora", "Citeseer", "Pubmed")
+    if planetoid:
+        # transductive: one graph, trained every step (models/planetoid_gat.py); the edge list
+        # never changes, so its CSR is built once and cached, as it is for any user of the layer
+        args.graphs = 1
+        args.cached_graph = True
     if args.graphs is None:
         args.graphs = 32 if ds == "PATTERN" else 20
     cfg = dict(data_config[ds])
@@ -448,8 +459,23 @@ def main():
     x = torch.from_numpy(b.x).to(dev)
     ei = torch.from_numpy(b.edge_index).to(dev)
     y = (torch.rand(b.num_nodes, cfg["num_classes"], device=dev) > 0.5).float()
+    train_mask = None
+    if planetoid:
+        # PlanetoidGAT (models/planetoid_gat.py:8-31): cross-entropy over the train split (PyG's
+        # public split: 20 labelled nodes per class) plus attention_reward x the attention norm
+        y = torch.randint(0, cfg["num_classes"], (b.num_nodes,), device=dev,
+                          generator=torch.Generator(device=dev).manual_seed(3))
+        train_mask = torch.zeros(b.num_nodes, dtype=torch.bool, device=dev)
+        train_mask[:20 * cfg["num_classes"]] = True
+        # out[mask] == out.index_select(0, mask.nonzero()): the same rows in the same order,
+        # without the host sync a boolean index costs (the step stays capturable)
+        train_idx = train_mask.nonzero().squeeze(1)
+        y_train = y.index_select(0, train_idx)
+        from gatx.graph import graph_cache as _gc
+        _ = _gc.get(ei, b.num_nodes, True).num_edges   # built and validated before any capture
     use_graph = args.hipgraph == "on" or (
-        args.hipgraph == "auto" and (args.mode == "fwd" or (ds == "PATTERN" and world == 1)))
+        args.hipgraph == "auto" and (args.mode == "fwd"
+                                     or (world == 1 and (ds == "PATTERN" or planetoid))))
     # a captured training step needs the optimizer's step counter on the device
     # torch's fused Adam (one launch for all parameters; same update rule as the reference's
     # Adam, models/*_gat.py configure_optimizers); a captured step needs capturable state
@@ -457,6 +483,8 @@ def main():
                            weight_decay=cfg["l2_reg"],
                            capturable=use_graph and args.mode == "train")
     loss_fn = torch.nn.BCEWithLogitsLoss()
+    if planetoid:
+        loss_fn = torch.nn.CrossEntropyLoss(reduction="mean")
     if ds == "PATTERN":   # PatternGAT (models/pattern_gat.py:11-15): class-balanced BCE
         loss_fn = torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([1 / 0.1765], device=dev))
         y = y[:, 0]
@@ -478,6 +506,11 @@ def main():
         if ds == "PATTERN":   # PatternGAT.training_step (models/pattern_gat.py:18-25)
             out = model(x, ei).squeeze(-1)
             loss = loss_fn(out, y)
+        elif planetoid:       # PlanetoidGAT.training_step (models/planetoid_gat.py:15-31)
+            out, ei2, atts = model.forward_and_return_attention(x, ei)
+            attention_norm = model.calc_attention_norm(ei2, atts)
+            loss = (loss_fn(out.index_select(0, train_idx), y_train)
+                    + args.attention_reward * attention_norm)
         else:
             # PPI_GAT.training_step (models/ppi_gat.py:15-33): BCE + the attention norm, computed
             # every step (logged; added to the loss only with a non-zero attention_penalty)
@@ -548,7 +581,8 @@ def main():
                                f"{args.graphs} graphs per GPU"
                                + (", CSR cached" if args.cached_graph else ", CSR built per step"),
                    "graphs_per_gpu": args.graphs, "nodes_per_gpu": N, "edges_per_layer": E2,
-                   "parallelism": f"graph-batch dp{world}",
+                   "parallelism": ("replicas" if planetoid and world > 1
+                                   else f"graph-batch dp{world}"),
                    "launch": "hipGraph replay (last steps//10 eager, HIP-event instrumented)"
                              if use_graph else "eager"},
         "unique_GBps": round(uniq / step_s / 1e9, 1),
@@ -562,7 +596,7 @@ def main():
         "kernels": kernel_summary(summ, n_instr),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.mode == "fwd":
-        result["cpu_baseline"] = cpu_baseline(model, cfg, ds, 1 if ds == "PPI" else 8)
+        result["cpu_baseline"] = cpu_baseline(model, cfg, ds, 8 if ds == "PATTERN" else 1)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if reducer is not None:

@@ -185,6 +185,8 @@ SHAPES = {
     "Cora": dict(nodes=2708, edges=10556, in_features=1433, features="bernoulli"),
     "PPI": dict(nodes=2245, edges=61318, in_features=50, features="normal"),
     "PATTERN": dict(nodes=119, edges=6099, in_features=3, features="normal"),
+    "Citeseer": dict(nodes=3327, edges=9104, in_features=3703, features="bernoulli"),
+    "Pubmed": dict(nodes=19717, edges=88648, in_features=500, features="normal"),
 }
 
 
