@@ -1,0 +1,20 @@
+#!/bin/bash
+# Copy what tools/gpu_round.sh TAG left under gpurun_out/TAG into profiles/TAG (tracked): the
+# three bench lines, the GPU test log, rocprofv3 kernel/domain stats and the PMC summaries; also
+# refresh profiles/pmc_latest.json and profiles/pmc_rmat.json, which bench.py reads.
+#   bash tools/snapshot_round.sh TAG
+set -e
+T=$1
+S=gpurun_out/$T
+D=profiles/$T
+mkdir -p "$D"
+cp "$S"/bench.json "$S"/bench_train.json "$S"/bench_rmat.json "$S"/gpu_tests.log "$D"/
+for p in fwd train rmat; do
+  cp "$S/prof_$p/run_kernel_stats.csv" "$D/${p}_kernel_stats.csv"
+  cp "$S/prof_$p/run_domain_stats.csv" "$D/${p}_domain_stats.csv" 2>/dev/null || true
+done
+PMC_STEPS=4 PMC_SOURCE="bench.py --steps 3 --warmup 1" \
+  python tools/pmc_summary.py "$S/pmc" profiles/pmc_latest.json > "$D/fwd_pmc_summary.txt"
+PMC_STEPS=3 PMC_SOURCE="bench.py --workload rmat --steps 1 --warmup 2" \
+  python tools/pmc_summary.py "$S/pmcr" profiles/pmc_rmat.json > "$D/rmat_pmc_summary.txt"
+echo "snapshot in $D"
