@@ -16,14 +16,15 @@ backward and the overlapped RCCL gradient all-reduce, gatx.distributed.GradientA
 value = (sum over ranks of layers x E' edges per step) / step time (max over ranks).
 Byte accounting (all per step, all reported):
   unique_GBps        - the dataflow actually run, every array read/written once (gathered rows
-                       once per node): the HBM-compulsory traffic / step time
+                       once per node while the gathered matrix fits the 256 MB MALL, once per
+                       edge beyond it): the HBM-compulsory traffic / step time
   roofline_time_frac - sum over kernels of max(unique bytes / 8 TB/s, flops / GEMM peak) over the
                        step time (<= 1 by construction when the clock is honest)
   hbm_measured       - rocprofv3 PMC bytes (FETCH_SIZE x 2 + WRITE_SIZE) per step from the
                        committed profiles/pmc_*.json summary, over this run's step time
   l2_gather_GBps     - SURVEY.md §8d's formula (one Wh row per EDGE, no reuse credited): the
                        gather rate the caches serve, NOT an HBM figure
-roofline = the dominant kernel's flops (GEMM) or unique bytes (edge pass) per launch / its
+roofline = the dominant kernel's flops (GEMM) or compulsory bytes (edge pass) per launch / its
 average launch time, measured with HIP events on the launch stream over the last steps // 10
 steps of the timed region (only those carry events: each record costs the stream ~10 us).
 cpu_baseline = the reference dataflow restated in torch eager (oracle/torch_dataflow.py) on a
@@ -47,6 +48,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+MALL_BYTES = 256 << 20       # Infinity Cache (MALL) capacity: the last on-chip level before HBM
 FP32_MFMA_PEAK_TFS = 157.3   # v_mfma_f32_32x32x2_f32 dense peak (same table)
 BF16_MFMA_PEAK_TFS = 2500.0  # dense bf16 MFMA peak (same table; no sparsity)
 X3_PRODUCTS = 6              # bf16 MFMA products per fp32 multiply-add in the x3 split GEMM
@@ -125,11 +127,13 @@ def survey_bytes(N, E2, F_in, NH, F, concat):
 
 
 def layer_dataflow(N, E2, F_in, NH, F, concat, resid):
-    """Per-kernel UNIQUE bytes (each array read or written once: the HBM-compulsory traffic) and
-    flops of one gatx layer forward, following the dataflow the library actually runs
-    (gatx.functional.layer_forward): the reassociated first layer gathers 4*round4(F_in)-byte x
-    rows, the others 4*NH*Fp-byte Wh rows; gathered rows are counted once per node, not per edge.
-    Returns [(kernel, bytes, flops)]."""
+    """Per-kernel COMPULSORY bytes and flops of one gatx layer forward, following the dataflow the
+    library actually runs (gatx.functional.layer_forward): the reassociated first layer gathers
+    4*round4(F_in)-byte x rows, the others 4*NH*Fp-byte Wh rows. Gathered rows count once per
+    node when the gathered matrix fits in the on-chip caches (<= the 256 MB MALL: every PPI /
+    PATTERN / Planetoid batch), and once per EDGE when it does not (RMAT: 20 GB of Wh gathered
+    in random order, so every gather is an HBM read; hub sources aside). Every other array is
+    read or written once. Returns [(kernel, bytes, flops)]."""
     from gatx.functional import LayerShape, fold_scores_into_gemm, use_reassociation
     sh = LayerShape(NH, F, F_in, concat, False)
     H2, Fp, Dp = 2 * NH, sh.Fp, sh.Dp
@@ -139,14 +143,16 @@ def layer_dataflow(N, E2, F_in, NH, F, concat, resid):
     alpha = ("attention_alpha", 16 * E2 + 4 * (N * H2 + N * NH + E2 * NH), 0)
     if use_reassociation(sh):
         Fin_p = _r4(F_in)
+        gath = N * Fin_p if N * Fin_p * 4 <= MALL_BYTES else E2 * Fin_p
         return [
             ("gemm_scores", 4 * (N * F_in + H2 * F_in + N * H2), 2 * N * F_in * H2),
             mx,
-            ("edge_forward", 4 * ((N + 1) + E2 + N * H2 + N * Fin_p + N * NH * Fin_p + N * NH), 0),
+            ("edge_forward", 4 * ((N + 1) + E2 + N * H2 + gath + N * NH * Fin_p + N * NH), 0),
             alpha,
             ("gemm_out", 4 * (N * NH * Fin_p + NH * F * Fin_p + N * oc + N * r),
              2 * N * Fin_p * NH * F),
         ]
+    gath = N * Dp if N * Dp * 4 <= MALL_BYTES else E2 * Dp
     out = []
     if fold_scores_into_gemm(sh):
         out.append(("gemm", 4 * (N * F_in + (Dp + H2) * F_in + N * Dp + N * H2),
@@ -155,7 +161,7 @@ def layer_dataflow(N, E2, F_in, NH, F, concat, resid):
         out.append(("gemm", 4 * (N * F_in + Dp * F_in + N * Dp), 2 * N * F_in * NH * F))
         out.append(("node_scores", 4 * (N * Dp + N * H2), 2 * N * Dp * H2))
     out += [mx,
-            ("edge_forward", 4 * ((N + 1) + E2 + N * H2 + N * Dp + N * NH + N * oc + N * r), 0),
+            ("edge_forward", 4 * ((N + 1) + E2 + N * H2 + gath + N * NH + N * oc + N * r), 0),
             alpha]
     return out
 
@@ -282,7 +288,7 @@ def kernel_summary(summ, n_instr):
 def roofline_objects(summ, unique_edge_bytes, pmc_path):
     """The two roofline objects (projection GEMM: MFMA-bound; edge pass: HBM-bound), each priced
     per launch from the live HIP-event durations, the GEMM by its flops, the edge pass by its
-    UNIQUE bytes (the gathered rows once, CSR, scores, output). `traffic` = the PMC-measured
+    compulsory bytes (layer_dataflow). `traffic` = the PMC-measured
     L2->fabric bytes per launch of the same kernel when a summary is committed."""
     roofs = {}
     gem = summ.get("gemm", [])
@@ -305,8 +311,10 @@ def roofline_objects(summ, unique_edge_bytes, pmc_path):
                                  "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                  "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
                                  "bytes_per_launch": by / len(edg),
-                                 "bytes_basis": "unique bytes: gathered rows once per node, CSR, "
-                                                "scores, den, output (+ residual)",
+                                 "bytes_basis": "compulsory bytes: gathered rows once per node when "
+                                                "the gathered matrix fits the 256 MB MALL, else "
+                                                "once per edge; CSR, scores, den, output (+ "
+                                                "residual) once",
                                  "avg_launch_ms": ms_ / len(edg),
                                  "_prefix": "edge_forward_kernel", "_ms": ms_}
     if os.path.exists(pmc_path):
