@@ -10,6 +10,25 @@ namespace gk {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
+// Two floats -> packed bf16 pair, round to nearest even (v_cvt_pk_bf16_f32). The empty asm keeps
+// the compiler from re-deriving each half from its own single-value conversion.
+__device__ inline uint32_t cvt_pk_bf16(float a, float b) {
+  typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+  bf2 v = {(__bf16)a, (__bf16)b};
+  uint32_t u = __builtin_bit_cast(uint32_t, v);
+  asm("" : "+v"(u));
+  return u;
+}
+
+// (x, y) -> the three bf16 planes of both, packed as pairs (x in the low half).
+__device__ inline void split_pair(float x, float y, uint32_t& h, uint32_t& m, uint32_t& l) {
+  h = cvt_pk_bf16(x, y);
+  const float rx = x - __uint_as_float(h << 16), ry = y - __uint_as_float(h & 0xffff0000u);
+  m = cvt_pk_bf16(rx, ry);
+  l = cvt_pk_bf16(rx - __uint_as_float(m << 16), ry - __uint_as_float(m & 0xffff0000u));
+}
+
+
 constexpr int BM = 128, BN = 128;
 constexpr int KSTEP = 32;   // split-K / tail slice granularity
 
