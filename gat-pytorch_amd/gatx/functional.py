@@ -550,13 +550,10 @@ def gat_layer(x, edge_index, W, a, bias, num_heads, out_features, concat, add_se
     return out, graph.edge_index, alpha[:graph.num_edges]
 
 
-def gat_layer_lazy(x, edge_index, W, a, bias, num_heads, out_features, concat, add_self_loops,
-                   const_attention=False, dropout_p=0.0, seed=0, graph: Graph | None = None,
-                   resid=None, elu=False):
-    """gat_layer without any host sync: returns (out, graph, alpha_bound) where alpha_bound is
-    (graph.edge_bound, NH) and its first graph.num_edges rows are alpha in edge_index' order.
-    resid / elu fuse GATModel's skip-add and ELU into the layer's epilogue:
-    out = elu?(layer(x) + resid)."""
+def prepare_layer(x, edge_index, W, a, bias, num_heads, out_features, concat, add_self_loops,
+                  const_attention=False, graph: Graph | None = None, resid=None):
+    """Argument checks of GATLayer.forward (the reference's own errors) and the layer's Graph:
+    returns (x, W, a, resid, LayerShape, Graph) with contiguous tensors."""
     from .graph import graph_cache
     _require(x, "x")
     _require(W, "W")
@@ -589,6 +586,19 @@ def gat_layer_lazy(x, edge_index, W, a, bias, num_heads, out_features, concat, a
         resid = resid.contiguous()
         if resid.shape != (x.size(0), sh.out_cols):
             raise RuntimeError(f"resid shape {tuple(resid.shape)} != {(x.size(0), sh.out_cols)}")
+    return x, W, a, resid, sh, graph
+
+
+def gat_layer_lazy(x, edge_index, W, a, bias, num_heads, out_features, concat, add_self_loops,
+                   const_attention=False, dropout_p=0.0, seed=0, graph: Graph | None = None,
+                   resid=None, elu=False):
+    """gat_layer without any host sync: returns (out, graph, alpha_bound) where alpha_bound is
+    (graph.edge_bound, NH) and its first graph.num_edges rows are alpha in edge_index' order.
+    resid / elu fuse GATModel's skip-add and ELU into the layer's epilogue:
+    out = elu?(layer(x) + resid)."""
+    x, W, a, resid, sh, graph = prepare_layer(x, edge_index, W, a, bias, num_heads, out_features,
+                                              concat, add_self_loops, const_attention, graph,
+                                              resid)
     p = float(dropout_p)
     seed_t = device_seed(seed, x.device) if p > 0 else None
     out, alpha = GATLayerFunction.apply(x, W, a, bias, resid, graph, sh, p, seed_t, bool(elu))

@@ -256,23 +256,26 @@ class GraphCache:
         return g
 
     def alias(self, ei2: torch.Tensor, g: Graph):
-        """Register a graph's materialised edge_index' as a key of the same graph."""
+        """Register a tensor holding a graph's edge_index' (its materialised buffer, or a copy of
+        it such as the one the registered op gatx::layer_fwd returns) as a key of the same
+        graph."""
         if g.add_self_loops:
-            self._put(self._key(ei2, g.num_nodes, True), ei2, g)
+            self._put(self._key(ei2, g.num_nodes, True), ei2, g, True)
+
+    @staticmethod
+    def _same(a: torch.Tensor, b: torch.Tensor) -> bool:
+        return a is b or (a.data_ptr() == b.data_ptr() and version(a) == version(b)
+                          and a.shape == b.shape and a.stride() == b.stride()
+                          and a.dtype == b.dtype and a.device == b.device)
 
     def for_edges(self, edge_index: torch.Tensor) -> Graph:
         """The Graph whose edge_index' IS this tensor (what a layer returned), else a CSR of it
         as given (no rewrite), sized by its max id — for consumers of a layer's output edges
         such as the attention-norm regulariser."""
-        for t, g in reversed(self._d.values()):
+        for t, g, is_alias in reversed(self._d.values()):
             ei = g._edge_index
-            if ei is None:
-                continue
-            if ei is edge_index or (ei.data_ptr() == edge_index.data_ptr()
-                                    and version(ei) == version(edge_index)
-                                    and ei.shape == edge_index.shape
-                                    and ei.stride() == edge_index.stride()
-                                    and ei.dtype == edge_index.dtype):
+            if (ei is not None and self._same(ei, edge_index)) or (
+                    is_alias and self._same(t, edge_index)):
                 return g
         k = self._key(edge_index, -1, False)
         hit = self._d.get(k)
@@ -282,8 +285,8 @@ class GraphCache:
         self._put(k, edge_index, g)
         return g
 
-    def _put(self, k, t, g):
-        self._d[k] = (t, g)
+    def _put(self, k, t, g, is_alias=False):
+        self._d[k] = (t, g, is_alias)
         self._d.move_to_end(k)
         while len(self._d) > self.capacity:
             self._d.popitem(last=False)

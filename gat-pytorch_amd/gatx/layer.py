@@ -17,6 +17,7 @@ from __future__ import annotations
 import torch
 from torch import nn
 
+from . import ops  # noqa: F401  (registers torch.ops.gatx.*)
 from .functional import gat_layer_lazy
 
 
@@ -83,6 +84,18 @@ class GATLayer(nn.Module):
         epilogue: returns elu?(out + resid)). Without return_attention_weights nothing waits
         for the device (|edge_index'| is only known there)."""
         p = float(self.dropout) if (self.dropout > 0 and self.training) else 0.0
+        if torch.compiler.is_compiling():
+            # traced by torch.compile: the registered op (gatx/ops.py), opaque to the compiler
+            if graph is not None:
+                raise RuntimeError("gatx: a prebuilt graph= is not supported under torch.compile")
+            seed_t = self._dropout_seed(x.device) if p > 0 else None
+            out, ei2, alpha, _ = torch.ops.gatx.layer_fwd(
+                x, edge_index, self.W.weight, None if self.const_attention else self.a.weight,
+                self.bias_param if self.bias else None, resid, seed_t, self.num_heads,
+                self.out_features, self.concat, self.add_self_loops, self.const_attention, p,
+                elu)
+            self.__dict__["_attention"] = alpha
+            return (out, (ei2, alpha)) if return_attention_weights else out
         seed = self._dropout_seed(x.device) if p > 0 else 0
         out, g, alpha = gat_layer_lazy(
             x, edge_index, self.W.weight, None if self.const_attention else self.a.weight,

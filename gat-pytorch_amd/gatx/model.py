@@ -92,6 +92,8 @@ class GATModel(nn.Module):
     def calc_attention_norm(edge_index, attention_list):
         """mean over layers of ||alpha * in_degree[dst] - 1||_1 / E (`models/GATModel.py:189-234`),
         fused on the device (gatx_attention_norm; degrees from the cached CSR of edge_index')."""
+        if torch.compiler.is_compiling():
+            return torch.ops.gatx.attention_norm(edge_index, list(attention_list))
         from .functional import attention_norm
         return attention_norm(edge_index, attention_list)
 
