@@ -145,6 +145,17 @@ struct EdgeFwdArgs {
                            // 3 last (out = epilogue((out + group sum) / NH + bias))
   int vec_out;             // concat output / resid rows float4-aligned (F % 4 == 0)
   int dbg;                 // diagnostic ablations (gatx_set_debug); 0 in production
+  // hub splitting (hub_T > 0): segments of more than hub_T edges are skipped by their own item
+  // and processed as pieces of hub_T edges (gatx_graph_hub_plan's list) by the items past
+  // n_items_main, each writing an unnormalised partial; edge_hub_combine_kernel sums a hub's
+  // pieces in piece order and runs the item's epilogue
+  int hub_T;
+  const int32_t* hubs;     // [hub_bound][4]: node, piece, pieces, first slot
+  const int32_t* hub_count;
+  int64_t hub_bound;
+  float* hub_part;         // [slot][g_count][HS*Fp + HS]
+  int64_t n_items_main;
+  int64_t hub_blocks;      // blocks [0, hub_blocks) run hub pieces (hub_bound * g_count waves)
 };
 
 int g_debug = 0;
@@ -171,6 +182,71 @@ __device__ inline float lane_f(float v, int j) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
 }
 
+// Normalisation and epilogue of one (node, head group) item: grp-0 lanes hold the item's
+// unnormalised sums acc (chunk q[c] of the HS * Fp row), den_lds its HS softmax denominators.
+template <int LPE, int CPL>
+__device__ inline void finish_item(const EdgeFwdArgs& g, int64_t n, int h0, int lane, int grp,
+                                   const int (&q)[CPL], const bool (&vq)[CPL],
+                                   const int (&hl)[CPL], const float4 (&acc)[CPL],
+                                   float* row_lds, const float* den_lds) {
+  const int NH = g.NH, F = g.F, Fp = g.Fp, HS = g.HS;
+  if (grp == 0) {
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      if (!vq[c]) continue;
+      const float inv = 1.f / (den_lds[hl[c]] + kSoftmaxEps);
+      const float4 o = acc[c] * inv;
+      const int h = h0 + hl[c], f0 = q[c] * 4 - hl[c] * Fp;
+      if (g.concat) {
+        float* orow = g.out + n * g.out_ld;
+        const int64_t cb = (int64_t)h * F + f0;
+        if (g.vec_out) {
+          // out / resid are streamed once: non-temporal, so they do not evict the gathered rows
+          float4 r = g.bias ? *(const float4*)(g.bias + cb) : make_float4(0.f, 0.f, 0.f, 0.f);
+          r = add4(o, r);
+          if (g.resid) {
+            const f4v rv = __builtin_nontemporal_load((const f4v*)(g.resid + n * g.resid_ld + cb));
+            r.x += rv[0]; r.y += rv[1]; r.z += rv[2]; r.w += rv[3];
+          }
+          if (g.elu) {
+            r.x = elu_act(r.x);
+            r.y = elu_act(r.y);
+            r.z = elu_act(r.z);
+            r.w = elu_act(r.w);
+          }
+          const f4v ov = {r.x, r.y, r.z, r.w};
+          __builtin_nontemporal_store(ov, (f4v*)(orow + cb));
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (f0 + j < F)
+              orow[cb + j] = epilogue(get4(o, j) + (g.bias ? g.bias[cb + j] : 0.f), g, n, cb + j);
+        }
+      } else {
+        *(float4*)(row_lds + q[c] * 4) = o;
+      }
+    }
+  }
+  wave_lds_sync();
+  if (!g.concat) {   // head mean over this item's HS heads (all NH when mean_mode == 0)
+    const float inv_nh = 1.f / (float)NH;
+    float* orow = g.out + n * g.out_ld;
+    for (int f = lane; f < F; f += 64) {
+      float sum = 0.f;
+      for (int h = 0; h < HS; ++h) sum += row_lds[h * Fp + f];
+      if (g.mean_mode == 1) {
+        orow[f] = sum;
+      } else if (g.mean_mode == 2) {
+        orow[f] += sum;
+      } else {
+        if (g.mean_mode == 3) sum += orow[f];
+        orow[f] = epilogue(sum * inv_nh + (g.bias ? g.bias[f] : 0.f), g, n, f);
+      }
+    }
+  }
+  if (lane < HS) g.den[n * NH + h0 + lane] = den_lds[lane];
+}
+
 // One wavefront per work item = (destination node n, group of HS heads). Edges are taken in
 // batches of 64: lane j loads batch edge j's source id (one coalesced load) and computes its HS
 // attention weights ex = exp(0.01 (s_src[src] + s_dst[n] - M)) (one gather of s_src per head).
@@ -188,17 +264,41 @@ __global__ void __launch_bounds__(256) edge_forward_kernel(EdgeFwdArgs g) {
   const int lane = threadIdx.x & 63;
   const int wave = uni(threadIdx.x >> 6);
   const int grp = lane / LPE, li = lane % LPE;
-  const int64_t item = xcd_contiguous(blockIdx.x, gridDim.x) * 4 + wave;
-  if (item >= g.n_items) return;
+  // the first hub_blocks blocks (a multiple of 8: dealt round-robin over the XCDs, and
+  // dispatched first, so long hub pieces start early) take the hub pieces; the rest the items
+  const int64_t hb = g.hub_blocks;
+  const bool hub_block = (int64_t)blockIdx.x < hb;
+  const int64_t item = hub_block ? g.n_items_main + (int64_t)blockIdx.x * 4 + wave
+                                 : xcd_contiguous(blockIdx.x - hb, gridDim.x - hb) * 4 + wave;
+  if (!hub_block && item >= g.n_items_main) return;
   const int NG = g.g_count;
-  const int64_t per_chunk = g.chunk * NG;
-  const int64_t ck = item / per_chunk, rem = item - ck * per_chunk;
-  const int hgl = (int)(rem / g.chunk);
-  const int64_t n = ck * g.chunk + (rem - (int64_t)hgl * g.chunk);
+  int64_t n;
+  int hgl, beg, end;
+  int64_t hub_slot = -1;   // >= 0: this wave is one piece of a hub segment
+  if (!hub_block) {
+    const int64_t per_chunk = g.chunk * NG;
+    const int64_t ck = item / per_chunk, rem = item - ck * per_chunk;
+    hgl = (int)(rem / g.chunk);
+    n = ck * g.chunk + (rem - (int64_t)hgl * g.chunk);
+    if (n >= g.N) return;
+    beg = uni(g.rowptr[n]);
+    end = uni(g.rowptr[n + 1]);
+    if (g.hub_T > 0 && end - beg > g.hub_T) return;   // done in pieces below
+  } else {
+    const int64_t hi = item - g.n_items_main;
+    hgl = (int)(hi / g.hub_bound);
+    const int64_t pc = hi - (int64_t)hgl * g.hub_bound;
+    if (hgl >= NG || pc >= uni(*g.hub_count)) return;
+    const int32_t* hp = g.hubs + 4 * pc;
+    n = uni(hp[0]);
+    const int p = uni(hp[1]);
+    hub_slot = (int64_t)uni(hp[3]) + p;
+    beg = uni(g.rowptr[n]) + p * g.hub_T;
+    end = min(uni(g.rowptr[n + 1]), beg + g.hub_T);
+  }
   const int hg = g.g_begin + hgl;
-  if (n >= g.N) return;
   const int h0 = hg * g.HS, HS = g.HS;
-  const int NH = g.NH, F = g.F, Fp = g.Fp, F4 = Fp / 4, S2 = 2 * NH;
+  const int NH = g.NH, Fp = g.Fp, F4 = Fp / 4, S2 = 2 * NH;
   const int D4 = HS * F4;
   // per-wave LDS: [HS*Fp head-mean staging][HS den][64 src ids][HS*64 edge weights]
   float* row_lds = smem + wave * g.lds_row;
@@ -233,7 +333,6 @@ __global__ void __launch_bounds__(256) edge_forward_kernel(EdgeFwdArgs g) {
 #pragma unroll
   for (int c = 0; c < CPL; ++c) acc[c] = make_float4(0.f, 0.f, 0.f, 0.f);
 
-  const int beg = uni(g.rowptr[n]), end = uni(g.rowptr[n + 1]);
   for (int base = beg; base < end; base += 64) {
     const int cnt = min(64, end - base);
     // batch phase: lane j <-> edge base + j (lanes past the segment reuse its last edge, w = 0)
@@ -343,61 +442,62 @@ __global__ void __launch_bounds__(256) edge_forward_kernel(EdgeFwdArgs g) {
     for (int c = 0; c < CPL; ++c) acc[c] = add4(acc[c], shfl_xor4(acc[c], off));
   }
   wave_lds_sync();
-  if (grp == 0) {
+  if (hub_slot >= 0) {   // one piece of a hub: its unnormalised partial, finished by the combine
+    float* part = g.hub_part + (hub_slot * NG + hgl) * (int64_t)(HS * Fp + HS);
+    if (grp == 0) {
 #pragma unroll
-    for (int c = 0; c < CPL; ++c) {
-      if (!vq[c]) continue;
-      const float inv = 1.f / (den_lds[hl[c]] + kSoftmaxEps);
-      const float4 o = acc[c] * inv;
-      const int h = h0 + hl[c], f0 = q[c] * 4 - hl[c] * Fp;
-      if (g.concat) {
-        float* orow = g.out + n * g.out_ld;
-        const int64_t cb = (int64_t)h * F + f0;
-        if (g.vec_out) {
-          // out / resid are streamed once: non-temporal, so they do not evict the gathered rows
-          float4 r = g.bias ? *(const float4*)(g.bias + cb) : make_float4(0.f, 0.f, 0.f, 0.f);
-          r = add4(o, r);
-          if (g.resid) {
-            const f4v rv = __builtin_nontemporal_load((const f4v*)(g.resid + n * g.resid_ld + cb));
-            r.x += rv[0]; r.y += rv[1]; r.z += rv[2]; r.w += rv[3];
-          }
-          if (g.elu) {
-            r.x = elu_act(r.x);
-            r.y = elu_act(r.y);
-            r.z = elu_act(r.z);
-            r.w = elu_act(r.w);
-          }
-          const f4v ov = {r.x, r.y, r.z, r.w};
-          __builtin_nontemporal_store(ov, (f4v*)(orow + cb));
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (f0 + j < F)
-              orow[cb + j] = epilogue(get4(o, j) + (g.bias ? g.bias[cb + j] : 0.f), g, n, cb + j);
-        }
-      } else {
-        *(float4*)(row_lds + q[c] * 4) = o;
-      }
+      for (int c = 0; c < CPL; ++c)
+        if (vq[c]) *(float4*)(part + q[c] * 4) = acc[c];
     }
+    if (lane < HS) part[HS * Fp + lane] = den_lds[lane];
+    return;
   }
+  finish_item<LPE, CPL>(g, n, h0, lane, grp, q, vq, hl, acc, row_lds, den_lds);
+}
+
+// Sum a hub's pieces (slots first .. first + pieces - 1, in that order) and finish the item:
+// one wave per (hub, head group), the lane layout of edge_forward_kernel<LPE, CPL>.
+template <int LPE, int CPL>
+__global__ void __launch_bounds__(256) edge_hub_combine_kernel(EdgeFwdArgs g) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = uni(threadIdx.x >> 6);
+  const int grp = lane / LPE, li = lane % LPE;
+  const int64_t hi = (int64_t)blockIdx.x * 4 + wave;
+  const int NG = g.g_count;
+  const int hgl = (int)(hi / g.hub_bound);
+  const int64_t pc = hi - (int64_t)hgl * g.hub_bound;
+  if (hgl >= NG || pc >= uni(*g.hub_count)) return;
+  const int32_t* hp = g.hubs + 4 * pc;
+  if (uni(hp[1]) != 0) return;   // one wave per hub: its first piece's entry
+  const int64_t n = uni(hp[0]);
+  const int pieces = uni(hp[2]), first = uni(hp[3]);
+  const int hg = g.g_begin + hgl;
+  const int h0 = hg * g.HS, HS = g.HS, Fp = g.Fp, F4 = Fp / 4, D4 = HS * F4;
+  float* row_lds = smem + wave * g.lds_row;
+  float* den_lds = row_lds + HS * Fp;
+  int q[CPL], hl[CPL];
+  bool vq[CPL];
+  float4 acc[CPL];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    q[c] = c * LPE + li;
+    vq[c] = q[c] < D4;
+    hl[c] = (vq[c] ? q[c] : 0) / F4;
+    acc[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  float d = 0.f;
+  const int64_t W = (int64_t)HS * Fp + HS;
+  for (int p = 0; p < pieces; ++p) {
+    const float* part = g.hub_part + ((int64_t)(first + p) * NG + hgl) * W;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c)
+      if (vq[c]) acc[c] = add4(acc[c], *(const float4*)(part + q[c] * 4));
+    if (lane < HS) d += part[HS * Fp + lane];
+  }
+  if (lane < HS) den_lds[lane] = d;
   wave_lds_sync();
-  if (!g.concat) {   // head mean over this item's HS heads (all NH when mean_mode == 0)
-    const float inv_nh = 1.f / (float)NH;
-    float* orow = g.out + n * g.out_ld;
-    for (int f = lane; f < F; f += 64) {
-      float sum = 0.f;
-      for (int h = 0; h < HS; ++h) sum += row_lds[h * Fp + f];
-      if (g.mean_mode == 1) {
-        orow[f] = sum;
-      } else if (g.mean_mode == 2) {
-        orow[f] += sum;
-      } else {
-        if (g.mean_mode == 3) sum += orow[f];
-        orow[f] = epilogue(sum * inv_nh + (g.bias ? g.bias[f] : 0.f), g, n, f);
-      }
-    }
-  }
-  if (lane < HS) g.den[n * NH + h0 + lane] = den_lds[lane];
+  finish_item<LPE, CPL>(g, n, h0, lane, grp, q, vq, hl, acc, row_lds, den_lds);
 }
 
 // ------------------------------------------------------------------ weights
@@ -758,6 +858,11 @@ int launch_edge_forward(unsigned grid, size_t lds, hipStream_t st, const EdgeFwd
   else
     edge_forward_kernel<LPE, CPL, U, false><<<grid, 256, lds, st>>>(g);
   GATX_LAUNCH_CHECK("edge_forward");
+  if (g.hub_T > 0) {
+    const int64_t waves = g.hub_bound * g.g_count;
+    edge_hub_combine_kernel<LPE, CPL><<<(unsigned)ceil_div(waves, 4), 256, lds, st>>>(g);
+    GATX_LAUNCH_CHECK("edge_hub_combine");
+  }
   return 0;
 }
 
@@ -914,6 +1019,27 @@ extern "C" int gatx_edge_forward_ex(
     int mean_mode, int concat, int const_att, const float* bias,
     float p, const uint64_t* seed, float* out, int64_t out_ld, const float* resid, int64_t resid_ld,
     int elu, float* den, int64_t chunk, gatx_stream_t s) {
+  return gatx_edge_forward_hubs(rows, row_stride, head_stride, S, M_ord, rowptr, col, perm, N,
+                                NH, F, heads_per_item, group_begin, group_count, mean_mode,
+                                concat, const_att, bias, p, seed, out, out_ld, resid, resid_ld,
+                                elu, den, chunk, 0, nullptr, nullptr, 0, nullptr, s);
+}
+
+extern "C" size_t gatx_edge_forward_hub_part_bytes(int64_t hub_bound, int NH, int F,
+                                                   int heads_per_item, int group_count) {
+  const int HS = heads_per_item <= 0 ? NH : heads_per_item;
+  const int64_t W = (int64_t)HS * round_up(F, 4) + HS;
+  return (size_t)hub_bound * (group_count > 0 ? group_count : NH / HS) * W * sizeof(float);
+}
+
+extern "C" int gatx_edge_forward_hubs(
+    const float* rows, int64_t row_stride, int64_t head_stride, const float* S,
+    const uint32_t* M_ord, const int32_t* rowptr, const int32_t* col, const int32_t* perm,
+    int64_t N, int NH, int F, int heads_per_item, int group_begin, int group_count,
+    int mean_mode, int concat, int const_att, const float* bias,
+    float p, const uint64_t* seed, float* out, int64_t out_ld, const float* resid, int64_t resid_ld,
+    int elu, float* den, int64_t chunk, int hub_edges, const int32_t* hubs,
+    const int32_t* hub_count, int64_t hub_bound, float* hub_part, gatx_stream_t s) {
   hipStream_t st = (hipStream_t)s;
   GATX_REQUIRE(NH >= 1 && F >= 1, "edge_forward: bad sizes");
   GATX_REQUIRE(concat || bias == nullptr || NH == 1,
@@ -955,10 +1081,18 @@ extern "C" int gatx_edge_forward_ex(
   g.chunk = chunk > 0 ? chunk : 2048;
   g.dbg = g_debug;
   g.g_begin = group_begin; g.g_count = group_count; g.mean_mode = concat ? 0 : mean_mode;
-  g.n_items = ceil_div(N, g.chunk) * g.chunk * group_count;
+  g.n_items_main = ceil_div(N, g.chunk) * g.chunk * group_count;
+  g.hub_T = 0; g.hubs = nullptr; g.hub_count = nullptr; g.hub_bound = 0; g.hub_part = nullptr;
+  if (hub_edges > 0 && hub_bound > 0) {
+    GATX_REQUIRE(hubs && hub_count && hub_part, "edge_forward: hub splitting needs its buffers");
+    g.hub_T = hub_edges; g.hubs = hubs; g.hub_count = hub_count; g.hub_bound = hub_bound;
+    g.hub_part = hub_part;
+  }
+  g.n_items = g.n_items_main + g.hub_bound * group_count;
+  g.hub_blocks = round_up(ceil_div(g.hub_bound * group_count, 4), 8);
   const size_t lds = (size_t)4 * g.lds_row * sizeof(float);
   GATX_REQUIRE(lds <= 160 * 1024, "edge_forward: row too wide for LDS staging");
-  const int64_t blocks = ceil_div(g.n_items, 4);
+  const int64_t blocks = g.hub_blocks + ceil_div(g.n_items_main, 4);
   GATX_REQUIRE(blocks < (1ll << 31), "edge_forward: too many work items");
   const unsigned grid = (unsigned)blocks;
 #define GATX_EF(L, C) return launch_edge_forward<L, C>(grid, lds, st, g)

@@ -394,6 +394,26 @@ int graph_build_impl(const void* ei, int64_t E, int64_t ld, int add_loops, int64
   return 0;
 }
 
+// Hub plan: every destination segment of more than T edges becomes ceil(deg / T) pieces, listed
+// as (node, piece, pieces, first slot) with the pieces of one node in consecutive slots. The
+// slot ranges are claimed with one atomic per hub (their order varies from run to run; every
+// consumer reads a hub's slots in piece order, so results do not).
+__global__ void __launch_bounds__(256) hub_plan_kernel(const int32_t* __restrict__ rowptr,
+                                                       int64_t N, int T, int32_t* __restrict__ hubs,
+                                                       int64_t bound, int32_t* __restrict__ count) {
+  for (int64_t n = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; n < N;
+       n += (int64_t)gridDim.x * blockDim.x) {
+    const int deg = rowptr[n + 1] - rowptr[n];
+    if (deg <= T) continue;
+    const int pieces = (int)ceil_div((int64_t)deg, T);
+    const int first = atomicAdd(count, pieces);
+    for (int p = 0; p < pieces && first + p < bound; ++p) {
+      int32_t* h = hubs + 4 * (int64_t)(first + p);
+      h[0] = (int32_t)n; h[1] = p; h[2] = pieces; h[3] = first;
+    }
+  }
+}
+
 }  // namespace
 }  // namespace gatx
 
@@ -474,5 +494,27 @@ extern "C" int gatx_graph_transpose(const int32_t* col, const int32_t* rowidx, i
     gather_kernel<<<grid_for(E_bound), 256, 0, stream>>>(rowidx, seid, E_bound, scol);
     GATX_LAUNCH_CHECK("gather scol");
   }
+  return 0;
+}
+
+extern "C" int64_t gatx_graph_hub_bound(int64_t E_bound, int hub_edges) {
+  // sum over hubs of ceil(deg / T) <= E'/T + #hubs <= 2 E'/T
+  return hub_edges > 0 ? 2 * ceil_div(E_bound, hub_edges) + 1 : 0;
+}
+
+extern "C" int gatx_graph_hub_plan(const int32_t* rowptr, int64_t N, int hub_edges,
+                                   int32_t* hubs, int64_t hub_bound, int32_t* hub_count,
+                                   gatx_stream_t s) {
+  GATX_REQUIRE(hub_edges > 0 && N >= 0, "graph_hub_plan: bad arguments");
+  hipStream_t st = (hipStream_t)s;
+  const hipError_t e = hipMemsetAsync(hub_count, 0, sizeof(int32_t), st);
+  if (e != hipSuccess) {
+    set_error("graph_hub_plan: %s", hipGetErrorString(e));
+    return (int)e;
+  }
+  if (N == 0) return 0;
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(N, 256), 8192);
+  hub_plan_kernel<<<grid, 256, 0, st>>>(rowptr, N, hub_edges, hubs, hub_bound, hub_count);
+  GATX_LAUNCH_CHECK("graph_hub_plan");
   return 0;
 }

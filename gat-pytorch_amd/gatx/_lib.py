@@ -47,6 +47,12 @@ SIGNATURES = {
     "gatx_edge_forward_ex": (c_i, [P, c_i64, c_i64, P, P, P, P, P, c_i64, c_i, c_i, c_i, c_i, c_i,
                                    c_i, c_i, c_i, P, c_f, P, P, c_i64, P, c_i64, c_i, P, c_i64,
                                    P]),
+    "gatx_edge_forward_hubs": (c_i, [P, c_i64, c_i64, P, P, P, P, P, c_i64, c_i, c_i, c_i, c_i,
+                                     c_i, c_i, c_i, c_i, P, c_f, P, P, c_i64, P, c_i64, c_i, P,
+                                     c_i64, c_i, P, P, c_i64, P, P]),
+    "gatx_edge_forward_hub_part_bytes": (c_sz, [c_i64, c_i, c_i, c_i, c_i]),
+    "gatx_graph_hub_bound": (c_i64, [c_i64, c_i]),
+    "gatx_graph_hub_plan": (c_i, [P, c_i64, c_i, P, c_i64, P, P]),
     "gatx_pad_rows": (c_i, [P, c_i64, c_i64, c_i64, P, c_i64, P]),
     "gatx_projection_gemm": (c_i, [c_i64, c_i64, c_i64, P, c_i64, c_i64, P, c_i64, c_i64, P,
                                    c_i64, c_i64, P, c_i64, P, c_sz, P]),

@@ -239,6 +239,21 @@ def edge_heads_per_item(sh: LayerShape) -> int:
     return max(d for d in range(1, 9) if sh.NH % d == 0 and d * sh.Fp <= max(256, sh.Fp))
 
 
+def hub_args(graph: Graph, sh: LayerShape, hs: int, group_count: int, dev):
+    """The trailing hub-splitting arguments of gatx_edge_forward_hubs: (hub_edges, hubs, count,
+    bound, partials). Segments longer than GATX_HUB_EDGES (8192) edges are aggregated in pieces
+    by parallel waves (degree skew). Engaged for graphs of more than
+    GATX_HUB_MIN_EDGES (2^22) input edges: there the plan and the combine launch cost nothing
+    next to the edge pass; a smaller graph's longest segment costs one wave at most 2^22 edges."""
+    T = _env_int("GATX_HUB_EDGES", 8192)
+    if T <= 0 or graph.num_input_edges <= _env_int("GATX_HUB_MIN_EDGES", 1 << 22):
+        return (0, None, None, 0, None)
+    hubs, count, bound = graph.hub_plan(T)
+    nb = lib.gatx_edge_forward_hub_part_bytes(bound, sh.NH, sh.F, hs, group_count)
+    part = torch.empty(max(nb, 4), dtype=torch.uint8, device=dev)
+    return (T, ptr(hubs), ptr(count), bound, ptr(part))
+
+
 def fold_scores_into_gemm(sh: LayerShape) -> bool:
     """Compute S as 2NH extra GEMM columns only when they fit the last column tile for free;
     otherwise (e.g. Dp = 1024: a whole extra 128-wide tile, +12% GEMM time) project Wh alone and
@@ -304,11 +319,13 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
         Z = torch.empty((N, sh.NH * Fin_p), **f32)
         with _span("edge_forward", (N, E2, sh.NH, Fin_p, "x")):
             hs_x = reassoc_heads_per_item(sh)   # heads sharing one x row
-            call("gatx_edge_forward_ex", ptr(x_rows), Fin_p, 0, ptr(S), ptr(M_ord),
+            hub = hub_args(graph, LayerShape(sh.NH, Fin_p, sh.F_in, True, sh.const), hs_x,
+                           sh.NH // hs_x, dev)
+            call("gatx_edge_forward_hubs", ptr(x_rows), Fin_p, 0, ptr(S), ptr(M_ord),
                  ptr(graph.rowptr), ptr(graph.col), ptr(graph.perm), N, sh.NH, Fin_p, hs_x,
                  0, 0, 0, 1,
                  int(sh.const), None, float(p), ptr(seed), ptr(Z), sh.NH * Fin_p, None, 0, 0,
-                 ptr(den), chunk, s)
+                 ptr(den), chunk, *hub, s)
         with _span("attention_alpha", (E2, sh.NH)):
             _attention_alpha(graph, S, M_ord, den, sh, alpha, argmax, s)
         Wp = padded_weight(W, Fin_p, sh.cache_weights)   # float4-readable rows
@@ -340,19 +357,21 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
         hs = edge_heads_per_item(sh)
         ng = sh.NH // hs
         if sh.concat or ng == 1:
-            call("gatx_edge_forward_ex", ptr(Wh), sh.Dp, sh.Fp, ptr(S), ptr(M_ord),
+            hub = hub_args(graph, sh, hs, ng, dev)
+            call("gatx_edge_forward_hubs", ptr(Wh), sh.Dp, sh.Fp, ptr(S), ptr(M_ord),
                  ptr(graph.rowptr), ptr(graph.col), ptr(graph.perm), N, sh.NH, sh.F, hs,
                  0, 0, 0, int(sh.concat), int(sh.const), ptr(bias), float(p), ptr(seed),
-                 ptr(out), sh.out_cols, resid_p, sh.out_cols, int(elu), ptr(den), chunk, s)
+                 ptr(out), sh.out_cols, resid_p, sh.out_cols, int(elu), ptr(den), chunk, *hub, s)
         else:   # head mean over groups: one launch per group, accumulated in stream order
+            hub = hub_args(graph, sh, hs, 1, dev)
             for gi in range(ng):
                 last = gi == ng - 1
                 mode = 1 if gi == 0 else (3 if last else 2)
-                call("gatx_edge_forward_ex", ptr(Wh), sh.Dp, sh.Fp, ptr(S), ptr(M_ord),
+                call("gatx_edge_forward_hubs", ptr(Wh), sh.Dp, sh.Fp, ptr(S), ptr(M_ord),
                      ptr(graph.rowptr), ptr(graph.col), ptr(graph.perm), N, sh.NH, sh.F, hs,
                      gi, 1, mode, 0, int(sh.const), ptr(bias) if last else None, float(p),
                      ptr(seed), ptr(out), sh.out_cols, resid_p if last else None, sh.out_cols,
-                     int(elu) if last else 0, ptr(den), chunk, s)
+                     int(elu) if last else 0, ptr(den), chunk, *hub, s)
     with _span("attention_alpha", (E2, sh.NH)):
         _attention_alpha(graph, S, M_ord, den, sh, alpha, argmax, s)
     saved.update(Wh=Wh, S=S, reassoc=False)

@@ -103,6 +103,7 @@ class Graph:
              ptr(self.meta), ei_out, ptr(self.rowptr), ptr(self.col), ptr(self.rowidx),
              ptr(self.perm), ptr(bws), ws_bytes, s)
         self.srowptr = self.scol = self.seid = None
+        self._hub_plans = {}
         self._E2 = None
         self._error = None
         self._edge_index = None
@@ -186,6 +187,19 @@ class Graph:
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
         call("gatx_graph_transpose", ptr(self.col), ptr(self.rowidx), N, Eb, self.e2_ptr,
              ptr(self.srowptr), ptr(self.scol), ptr(self.seid), ptr(ws), ws_bytes, stream())
+
+    def hub_plan(self, hub_edges: int):
+        """(hubs, hub_count, hub_bound) of gatx_graph_hub_plan for this CSR: destination segments
+        longer than hub_edges listed as pieces (device-side count; built once per graph)."""
+        plan = self._hub_plans.get(hub_edges)
+        if plan is None:
+            bound = int(_lib.lib.gatx_graph_hub_bound(self.edge_bound, hub_edges))
+            hubs = torch.empty((max(bound, 1), 4), dtype=torch.int32, device=self.device)
+            count = torch.empty(1, dtype=torch.int32, device=self.device)
+            call("gatx_graph_hub_plan", ptr(self.rowptr), self.num_nodes, hub_edges, ptr(hubs),
+                 bound, ptr(count), stream())
+            plan = self._hub_plans[hub_edges] = (hubs, count, bound)
+        return plan
 
     def csr_host(self):
         """(rowptr, col, perm) as CPU tensors — for tests."""

@@ -151,6 +151,14 @@ int gatx_gemm_f32_batched(int64_t batch, int64_t M, int64_t N, int64_t K, const 
                           int accumulate, const float* bias, int64_t bias_bs, const float* resid,
                           int64_t resid_ld, int64_t resid_bs, int elu, gatx_stream_t stream);
 
+/* Hub plan for the edge pass (SURVEY §7 "degree skew"): destination segments of more than
+ * hub_edges edges are cut into ceil(deg / hub_edges) pieces listed in hubs [hub_bound][4] =
+ * (node, piece, pieces, first slot); *hub_count (device) = the number of entries. hub_bound =
+ * gatx_graph_hub_bound(E_bound, hub_edges) always suffices. No host sync. */
+int64_t gatx_graph_hub_bound(int64_t E_bound, int hub_edges);
+int gatx_graph_hub_plan(const int32_t* rowptr, int64_t num_nodes, int hub_edges, int32_t* hubs,
+                        int64_t hub_bound, int32_t* hub_count, gatx_stream_t stream);
+
 /* ---------------------------------------------------------------- attention + aggregation */
 
 /* Global max M = max_{e,h} s_src[col[e],h] + s_dst[rowidx[e],h]  (gat_layer.py:85), written as an
@@ -204,6 +212,23 @@ int gatx_edge_forward_ex(const float* rows, int64_t row_stride, int64_t head_str
                          const float* bias, float dropout_p, const uint64_t* seed, float* out,
                          int64_t out_ld, const float* resid, int64_t resid_ld, int elu,
                          float* den, int64_t chunk, gatx_stream_t stream);
+/* gatx_edge_forward_ex with hub splitting: segments longer than hub_edges (a plan from
+ * gatx_graph_hub_plan over the same rowptr) are aggregated as pieces by their own waves into
+ * hub_part (gatx_edge_forward_hub_part_bytes), then summed in piece order and finished by a
+ * second kernel — a hub costs ceil(deg / hub_edges) waves in parallel instead of one wave walking
+ * every edge. hub_edges = 0: no splitting (exactly gatx_edge_forward_ex). */
+size_t gatx_edge_forward_hub_part_bytes(int64_t hub_bound, int num_heads, int out_features,
+                                        int heads_per_item, int group_count);
+int gatx_edge_forward_hubs(const float* rows, int64_t row_stride, int64_t head_stride,
+                           const float* S, const uint32_t* M_ord, const int32_t* rowptr,
+                           const int32_t* col, const int32_t* perm, int64_t num_nodes,
+                           int num_heads, int out_features, int heads_per_item, int group_begin,
+                           int group_count, int mean_mode, int concat, int const_attention,
+                           const float* bias, float dropout_p, const uint64_t* seed, float* out,
+                           int64_t out_ld, const float* resid, int64_t resid_ld, int elu,
+                           float* den, int64_t chunk, int hub_edges, const int32_t* hubs,
+                           const int32_t* hub_count, int64_t hub_bound, float* hub_part,
+                           gatx_stream_t stream);
 
 /* alpha [E2][NH] in edge_index' order from S, M and den (one thread per CSR slot, all heads of
  * an edge stored together), plus the argmax records (see gatx_edge_forward). */

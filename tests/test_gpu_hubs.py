@@ -1,0 +1,129 @@
+"""Hub splitting of the edge pass (gatx_graph_hub_plan + gatx_edge_forward_hubs): destination
+segments longer than GATX_HUB_EDGES are aggregated in pieces by parallel waves and combined in
+piece order. Checked against the oracle (the reference's dataflow) on graphs with hubs of a few
+to many pieces, every epilogue kind (concat, one-pass and multi-pass head mean, the reassociated
+first layer, dropout), and against the unsplit kernel."""
+import numpy as np
+import pytest
+import torch
+
+from golden_io import grad_seeds
+from oracle import gat_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+OUT_TOL = 1e-4
+GRAD_TOL = 1e-4
+
+
+def _hub_graph(n=3000, e=20000, hubs=(30000, 9000, 1001, 1000, 999), fin=16, seed=11):
+    """Uniform random edges plus hub destinations receiving the given in-degrees."""
+    rng = np.random.default_rng(seed)
+    src = [rng.integers(0, n, e)]
+    dst = [rng.integers(0, n, e)]
+    for i, d in enumerate(hubs):
+        src.append(rng.integers(0, n, d))
+        dst.append(np.full(d, 17 + 101 * i))
+    ei = np.stack([np.concatenate(src), np.concatenate(dst)]).astype(np.int64)
+    x = rng.standard_normal((n, fin)).astype(np.float32)
+    return x, ei
+
+
+def _run(device, x, ei, W, a, NH, F, concat, dropout=0.0, grads=True):
+    import gatx
+    layer = gatx.GATLayer(x.shape[1], F, NH, concat, dropout=dropout,
+                          add_self_loops=True).to(device)
+    with torch.no_grad():
+        layer.W.weight.copy_(torch.from_numpy(W))
+        layer.a.weight.copy_(torch.from_numpy(a))
+    if dropout > 0:
+        layer._dropout_seed = lambda *_: 77
+        layer.train()
+    xt = torch.from_numpy(x).to(device).requires_grad_(grads)
+    et = torch.from_numpy(ei).to(device)
+    gatx.clear_graph_cache()
+    out, (ei2, alpha) = layer(xt, et, return_attention_weights=True)
+    r = dict(out=out.detach().cpu().numpy(), alpha=alpha.detach().cpu().numpy(),
+             ei2=ei2.cpu().numpy())
+    if grads:
+        g_out, g_alpha = grad_seeds(tuple(out.shape), tuple(alpha.shape))
+        ((out * torch.from_numpy(g_out).to(device)).sum()
+         + (alpha * torch.from_numpy(g_alpha).to(device)).sum()).backward()
+        r["grad_x"] = xt.grad.cpu().numpy()
+        r["grad_W"] = layer.W.weight.grad.cpu().numpy()
+    return r
+
+
+CASES = {   # name: (fin, NH, F, concat, env)
+    "concat": (16, 4, 16, True, {}),
+    "concat_wide": (16, 2, 256, True, {}),
+    "mean_one_pass": (16, 6, 12, False, {}),
+    "mean_multi_pass": (16, 6, 12, False, {"GATX_MEAN_HEADS": "2"}),
+    "reassociated": (8, 4, 64, True, {}),
+    "dropout": (16, 4, 16, True, {}),
+}
+
+
+@pytest.mark.parametrize("T", ["1000", "333"])
+@pytest.mark.parametrize("name", list(CASES))
+def test_hub_split_vs_oracle(name, T, device, monkeypatch):
+    fin, NH, F, concat, env = CASES[name]
+    dropout = 0.5 if name == "dropout" else 0.0
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("GATX_HUB_EDGES", T)
+    monkeypatch.setenv("GATX_HUB_MIN_EDGES", "0")
+    from gatx import data as gd
+    x, ei = _hub_graph(fin=fin)
+    W = gd.xavier_uniform(6, NH * F, fin)
+    a = gd.xavier_uniform(7, NH, NH * 2 * F)
+    r = _run(device, x, ei, W, a, NH, F, concat, dropout)
+    keep = orc.dropout_keep(77, r["alpha"].shape[0], NH, dropout) if dropout > 0 else None
+    out, ei2, alpha, cache = orc.gat_layer_forward(x, ei, W, a, NH, F, concat, dropout_p=dropout,
+                                                   keep=keep)
+    np.testing.assert_array_equal(r["ei2"], ei2)
+    assert np.abs(r["out"] - out).max() <= OUT_TOL
+    assert np.abs(r["alpha"] - alpha).max() <= OUT_TOL
+    g_out, g_alpha = grad_seeds(out.shape, alpha.shape)
+    gr = orc.gat_layer_backward(cache, g_out, g_alpha)
+    for k in ("x", "W"):
+        err = np.abs(r[f"grad_{k}"] - gr[k]).max()
+        assert err <= GRAD_TOL * max(1.0, np.abs(gr[k]).max()), (k, err)
+    # the same layer without splitting: same result to fp32 summation-order noise
+    monkeypatch.setenv("GATX_HUB_EDGES", "0")
+    from gatx import functional
+    functional.reset_tuning()
+    r0 = _run(device, x, ei, W, a, NH, F, concat, dropout, grads=False)
+    assert np.abs(r["out"] - r0["out"]).max() <= 1e-5
+    assert np.abs(r["alpha"] - r0["alpha"]).max() <= 1e-5
+
+
+def test_hub_plan(device, monkeypatch):
+    """The plan lists every segment longer than T as ceil(deg / T) pieces in consecutive slots."""
+    from gatx import clear_graph_cache
+    from gatx.graph import graph_cache
+    x, ei = _hub_graph()
+    clear_graph_cache()
+    g = graph_cache.get(torch.from_numpy(ei).to(device), x.shape[0], True)
+    hubs, count, bound = g.hub_plan(1000)
+    torch.cuda.synchronize()
+    rowptr = g.rowptr.cpu().numpy()
+    deg = np.diff(rowptr)
+    want = {int(n): int(-(-d // 1000)) for n, d in enumerate(deg) if d > 1000}
+    c = int(count.item())
+    h = hubs[:c].cpu().numpy()
+    assert c == sum(want.values()) and c <= bound
+    got = {}
+    for node, p, pieces, first in h:
+        assert want[int(node)] == pieces
+        got.setdefault(int(node), set()).add((int(p), int(first)))
+    for node, pcs in got.items():
+        firsts = {f for _, f in pcs}
+        assert len(firsts) == 1 and {p for p, _ in pcs} == set(range(want[node]))
+    # slot ranges of different hubs are disjoint and cover [0, count)
+    starts = sorted((f, want[n]) for n, pcs in got.items() for f in {f for _, f in pcs})
+    pos = 0
+    for f, pieces in starts:
+        assert f == pos
+        pos += pieces
+    assert pos == c
