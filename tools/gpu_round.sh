@@ -9,7 +9,7 @@ OUT=$R/gpurun_out/$1
 mkdir -p "$OUT"
 exec 3>&1   # progress lines go to the call's stdout, never into a step's redirected output
 step() { echo "== $1" >&3; shift; "$@"; rc=$?; echo "rc=$rc" >&3; [ $rc -ne 0 ] && exit $rc; return 0; }
-step tests timeout -k 10 600 python -m pytest "$R/tests" -m gpu -x -q -p no:cacheprovider \
+step tests timeout -k 10 900 python -m pytest "$R/tests" -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread \
   --junitxml="$OUT/gpu_tests.xml" > "$OUT/gpu_tests.log" 2>&1
 tail -2 "$OUT/gpu_tests.log"
 step bench timeout -k 10 300 python "$R/bench.py" > "$OUT/bench.json" 2> "$OUT/bench.err"
