@@ -547,6 +547,55 @@ class GATLayerFunction(torch.autograd.Function):
         return g_x, g_W, g_a, g_b, g_r, None, None, None, None, None
 
 
+class SkipProjectionFunction(torch.autograd.Function):
+    """GATModel's Linear skip (`models/GATModel.py:107-110`, applied at `:136-145`) on the gatx
+    GEMMs instead of a vendor BLAS call: out = x W^T for a concat layer, and for a head-mean
+    layer the head mean of the projection as ONE product with the head-mean weight,
+    mean_h(x W_h^T) = x (mean_h W_h)^T (F output columns instead of NH*F plus a mean reduction).
+    Backward: g_x = g W_eff, g_W_eff = g^T x (deterministic split-K), g_W = g_W_eff broadcast
+    over the heads / NH for the mean."""
+
+    @staticmethod
+    def forward(ctx, x, W, num_heads, out_features, mean):
+        _require(x, "x")
+        _require(W, "skip weight")
+        x = x.contiguous()
+        N, F_in = x.shape
+        dev = x.device
+        W_eff = (W.detach().view(num_heads, out_features, F_in).mean(0) if mean
+                 else W.detach()).contiguous()
+        cols = W_eff.size(0)
+        out = torch.empty((N, cols), dtype=torch.float32, device=dev)
+        with _span("skip", (N, cols, F_in)):
+            call("gatx_gemm_f32", N, cols, F_in, ptr(x), F_in, 1, ptr(W_eff), 1, F_in, ptr(out),
+                 cols, cols, None, 0, 0, *gemm_workspace(N, cols, F_in, dev), stream())
+        ctx.save_for_backward(x, W_eff)
+        ctx.num_heads, ctx.mean = num_heads, mean
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, W_eff = ctx.saved_tensors
+        N, F_in = x.shape
+        cols = W_eff.size(0)
+        dev = x.device
+        s = stream()
+        g = g.contiguous()
+        g_x = g_W = None
+        if ctx.needs_input_grad[0]:
+            g_x = torch.empty((N, F_in), dtype=torch.float32, device=dev)
+            call("gatx_gemm_f32", N, F_in, cols, ptr(g), cols, 1, ptr(W_eff), F_in, 1, ptr(g_x),
+                 F_in, F_in, None, 0, 0, *gemm_workspace(N, F_in, cols, dev), s)
+        if ctx.needs_input_grad[1]:
+            gW = torch.empty((cols, F_in), dtype=torch.float32, device=dev)
+            wb = lib.gatx_gemm_splitk_workspace_bytes(cols, F_in, N)
+            ws = torch.empty(max(wb, 1), dtype=torch.uint8, device=dev)
+            call("gatx_gemm_f32_splitk", cols, F_in, N, ptr(g), 1, cols, ptr(x), F_in, 1,
+                 ptr(gW), F_in, 0, ptr(ws), wb, s)
+            g_W = gW.repeat(ctx.num_heads, 1).div_(ctx.num_heads) if ctx.mean else gW
+        return g_x, g_W, None, None, None
+
+
 def device_seed(seed, dev) -> torch.Tensor:
     """The dropout seed as the device scalar the kernels read: an int (tests, reproducible runs)
     is uploaded; a device int64 tensor (GATLayer draws one from torch's generator, so captured

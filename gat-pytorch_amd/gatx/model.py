@@ -52,12 +52,19 @@ class GATModel(nn.Module):
 
     def _resid(self, i, skip_count, layer_input):
         """Skip connection of layer i (`models/GATModel.py:135-145`) in the layer's output shape,
-        to be added inside the layer's fused epilogue."""
-        skip_output = self.skip_layer_list[skip_count](layer_input)
-        if self.heads_concat_per_layer[i]:
+        to be added inside the layer's fused epilogue. A Linear skip runs on the gatx GEMMs
+        (functional.SkipProjectionFunction; its head mean folded into the weight), except while
+        torch.compile traces (plain torch ops, which the compiler handles itself)."""
+        skip = self.skip_layer_list[skip_count]
+        nh, f = self.num_heads_per_layer[i + 1], self.head_output_features_per_layer[i + 1]
+        mean = not self.heads_concat_per_layer[i]
+        if isinstance(skip, nn.Linear) and not torch.compiler.is_compiling():
+            from .functional import SkipProjectionFunction
+            return SkipProjectionFunction.apply(layer_input, skip.weight, nh, f, mean)
+        skip_output = skip(layer_input)
+        if not mean:
             return skip_output
-        return skip_output.view(-1, self.num_heads_per_layer[i + 1],
-                                self.head_output_features_per_layer[i + 1]).mean(dim=1)
+        return skip_output.view(-1, nh, f).mean(dim=1)
 
     def _run(self, x, edge_index, with_attention):
         attention_weights_list = []

@@ -50,7 +50,7 @@ def test_compiled_train_step_equals_eager(device):
     the attention norm, backward — compiled with AOTAutograd (fwd + bwd graphs, no codegen: the
     same aten kernels as eager around the gatx ops) == eager."""
     from gatx import clear_graph_cache
-    model, cfg = _ppi_model(device, 2)
+    model, cfg = _ppi_model(device, 3)   # identity skip: every op is the same kernel in both
     model.train()
     x, ei = _batch(device, cfg)
     y = (torch.rand(x.size(0), 121, device=device, generator=torch.Generator(device=device)
