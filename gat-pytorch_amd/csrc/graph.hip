@@ -197,6 +197,10 @@ __global__ void __launch_bounds__(256) iota_kernel(int64_t n, int32_t* out) {
 //    ordered through per-(wave, digit) counts in LDS, rounds through running per-digit bases.
 constexpr int kRadixBits = 8, kRadix = 1 << kRadixBits;
 constexpr int kMaxSortItems = 16;
+// small sorts (keys < 2^12: graphs of up to 4095 nodes, PATTERN-size batches) take ONE pass of
+// 12-bit digits instead of two 8-bit passes: 4 launches fewer per graph build, on steps that are
+// launch-bound
+constexpr int kWideBits = 12;
 
 // keys per thread per block: up to 16, but at least ~256 blocks — a block walks its tile in
 // serial rounds, so small sorts (PATTERN: 50 k keys) need short tiles to fill the chip
@@ -206,30 +210,51 @@ inline int sort_items(int64_t n) {
   return it;
 }
 
+// (digit bits, keys per thread) of each pass for keys in [0, 2^bits)
+inline bool wide_pass(unsigned bits, int64_t n) { return bits > kRadixBits && bits <= kWideBits && n <= (1 << 20); }
+// the wide pass keeps ~48 blocks: its histogram (nblocks x 4096 counts) stays small to scan,
+// and each block walks few serial rounds
+inline int pass_items(unsigned bits, int64_t n) {
+  if (!wide_pass(bits, n)) return sort_items(n);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(kMaxSortItems, ceil_div(n, 256 * 48)));
+}
+
+template <int BITS>
 __global__ void __launch_bounds__(256) radix_hist_kernel(const int32_t* __restrict__ keys,
                                                          int64_t n, int shift, int items,
                                                          int64_t nblocks,
                                                          uint32_t* __restrict__ hist) {
-  __shared__ uint32_t h[kRadix];
-  h[threadIdx.x] = 0;
+  constexpr int R = 1 << BITS, PER = R / 256;
+  __shared__ uint32_t h[R];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) h[threadIdx.x + 256 * j] = 0;
   __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * 256 * items;
   for (int i = 0; i < items; ++i) {
     const int64_t idx = base + i * 256 + threadIdx.x;
-    if (idx < n) atomicAdd(&h[(keys[idx] >> shift) & (kRadix - 1)], 1u);
+    if (idx < n) atomicAdd(&h[(keys[idx] >> shift) & (R - 1)], 1u);
   }
   __syncthreads();
-  hist[(int64_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+#pragma unroll
+  for (int j = 0; j < PER; ++j)
+    hist[(int64_t)(threadIdx.x + 256 * j) * nblocks + blockIdx.x] = h[threadIdx.x + 256 * j];
 }
 
+template <int BITS>
 __global__ void __launch_bounds__(256) radix_scatter_kernel(
     const int32_t* __restrict__ keys, const int32_t* __restrict__ vals, int64_t n, int shift,
     int items, int64_t nblocks, const uint32_t* __restrict__ offs, int32_t* __restrict__ keys_out,
     int32_t* __restrict__ vals_out) {
-  __shared__ uint32_t base[kRadix];
-  __shared__ uint32_t cnt[4][kRadix];
+  constexpr int R = 1 << BITS, PER = R / 256;
+  __shared__ uint32_t base[R];
+  __shared__ uint32_t cnt[4][R];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  base[tid] = offs[(int64_t)tid * nblocks + blockIdx.x];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) base[tid + 256 * j] = offs[(int64_t)(tid + 256 * j) * nblocks + blockIdx.x];
+#pragma unroll
+  for (int w = 0; w < 4; ++w)
+#pragma unroll
+    for (int j = 0; j < PER; ++j) cnt[w][tid + 256 * j] = 0;
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const int64_t tile = (int64_t)blockIdx.x * 256 * items;
   for (int r = 0; r < items; ++r) {
@@ -237,18 +262,17 @@ __global__ void __launch_bounds__(256) radix_scatter_kernel(
     const bool valid = idx < n;
     const int32_t key = valid ? keys[idx] : 0;
     const int32_t val = valid ? (vals ? vals[idx] : (int32_t)idx) : 0;
-    const int d = (key >> shift) & (kRadix - 1);
-#pragma unroll
-    for (int w = 0; w < 4; ++w) cnt[w][tid] = 0;
-    __syncthreads();
+    const int d = (key >> shift) & (R - 1);
     uint64_t peers = __ballot(valid);
 #pragma unroll
-    for (int b = 0; b < kRadixBits; ++b) {
+    for (int b = 0; b < BITS; ++b) {
       const uint64_t bb = __ballot((d >> b) & 1);
       peers &= ((d >> b) & 1) ? bb : ~bb;
     }
     const int rank = __popcll(peers & lt);
-    if (valid && rank == 0) cnt[wave][d] = (uint32_t)__popcll(peers);
+    const bool lead = valid && rank == 0;   // one lane per (wave, digit present in it)
+    __syncthreads();   // the previous round's base / cnt updates are complete
+    if (lead) cnt[wave][d] = (uint32_t)__popcll(peers);
     __syncthreads();
     if (valid) {
       uint32_t pos = base[d] + rank;
@@ -257,8 +281,12 @@ __global__ void __launch_bounds__(256) radix_scatter_kernel(
       vals_out[pos] = val;
     }
     __syncthreads();
-    base[tid] += cnt[0][tid] + cnt[1][tid] + cnt[2][tid] + cnt[3][tid];
-    // the next round's cnt reset comes after a barrier this base update precedes
+    // only the digits of this round are touched: every wave's leader adds its count to the
+    // digit's base (commutative) and clears its own count, so no round walks all 2^BITS bins
+    if (lead) {
+      atomicAdd(&base[d], cnt[wave][d]);
+      cnt[wave][d] = 0;
+    }
   }
 }
 
@@ -302,15 +330,19 @@ size_t radix_scan_bytes(int64_t m) {
   return bytes;
 }
 
+inline int64_t hist_entries(int64_t n, unsigned bits) {
+  const int64_t nb = ceil_div(n > 0 ? n : 1, 256 * pass_items(bits, n));
+  return nb * (wide_pass(bits, n) ? (1 << kWideBits) : kRadix);
+}
+
 size_t sort_bytes(int64_t n, unsigned bits) {  // keys in [0, 2^bits)
-  (void)bits;
-  const int64_t nb = ceil_div(n > 0 ? n : 1, 256 * sort_items(n)), m = nb * kRadix;
+  const int64_t m = hist_entries(n, bits);
   return 2 * align256(sizeof(uint32_t) * m) + 2 * align256(sizeof(int32_t) * (n > 0 ? n : 1)) +
          align256(radix_scan_bytes(m)) + 256;
 }
 
-SortWs carve_sort(void* ws, int64_t n) {
-  const int64_t nb = ceil_div(n > 0 ? n : 1, 256 * sort_items(n)), m = nb * kRadix;
+SortWs carve_sort(void* ws, int64_t n, unsigned bits) {
+  const int64_t m = hist_entries(n, bits);
   char* p = (char*)ws;
   SortWs w;
   w.hist = (uint32_t*)p; p += align256(sizeof(uint32_t) * m);
@@ -329,10 +361,11 @@ int sort_pairs(const int32_t* keys_in, const int32_t* vals_in, int32_t* keys_out
                int32_t* vals_out, int64_t n, unsigned bits, void* ws, hipStream_t stream) {
   if (n <= 0) return 0;
   GATX_REQUIRE(n < (1ll << 31), "sort: too many keys");
-  const SortWs w = carve_sort(ws, n);
-  const int items = sort_items(n);
-  const int64_t nb = ceil_div(n, 256 * items), m = nb * kRadix;
-  const int passes = (int)ceil_div((int64_t)(bits > 0 ? bits : 1), kRadixBits);
+  const SortWs w = carve_sort(ws, n, bits);
+  const bool wide = wide_pass(bits, n);
+  const int items = pass_items(bits, n);
+  const int64_t nb = ceil_div(n, 256 * items), m = hist_entries(n, bits);
+  const int passes = wide ? 1 : (int)ceil_div((int64_t)(bits > 0 ? bits : 1), kRadixBits);
   const int32_t* ck = keys_in;
   const int32_t* cv = vals_in;
   for (int ps = 0; ps < passes; ++ps) {
@@ -340,14 +373,19 @@ int sort_pairs(const int32_t* keys_in, const int32_t* vals_in, int32_t* keys_out
     int32_t* ok = to_out ? keys_out : w.tk;
     int32_t* ov = to_out ? vals_out : w.tv;
     const int shift = ps * kRadixBits;
-    radix_hist_kernel<<<(unsigned)nb, 256, 0, stream>>>(ck, n, shift, items, nb, w.hist);
+    if (wide) radix_hist_kernel<kWideBits><<<(unsigned)nb, 256, 0, stream>>>(ck, n, 0, items, nb, w.hist);
+    else radix_hist_kernel<kRadixBits><<<(unsigned)nb, 256, 0, stream>>>(ck, n, shift, items, nb, w.hist);
     GATX_LAUNCH_CHECK("radix_hist");
     size_t b = w.scan_bytes;
     hipError_t r = rocprim::exclusive_scan(w.scan_tmp, b, w.hist, w.offs, 0u, (size_t)m,
                                            rocprim::plus<uint32_t>(), stream);
     if (r != hipSuccess) { set_error("radix scan: %s", hipGetErrorString(r)); return (int)r; }
-    radix_scatter_kernel<<<(unsigned)nb, 256, 0, stream>>>(ck, cv, n, shift, items, nb, w.offs,
-                                                           ok, ov);
+    if (wide)
+      radix_scatter_kernel<kWideBits><<<(unsigned)nb, 256, 0, stream>>>(ck, cv, n, 0, items, nb,
+                                                                        w.offs, ok, ov);
+    else
+      radix_scatter_kernel<kRadixBits><<<(unsigned)nb, 256, 0, stream>>>(ck, cv, n, shift, items,
+                                                                         nb, w.offs, ok, ov);
     GATX_LAUNCH_CHECK("radix_scatter");
     ck = ok;
     cv = ov;

@@ -18,6 +18,12 @@ from torch import nn
 
 from .layer import GATLayer
 
+# Linear skips of at least this many multiply-adds run on the gatx GEMM (x3: the PPI-scale
+# products, e.g. the notebook variant's 44900 x 1024 x 1024 skip, where hipBLASLt's fp32 path is
+# ~1.6x slower); smaller ones stay nn.Linear: at PATTERN's 952 x 96 x 48 a vendor launch takes
+# ~5 us against 6-14 us for the tiled / small-K gatx kernels (profiles/r02d_small)
+SKIP_GEMM_MIN_MACS = 1 << 26
+
 
 class GATModel(nn.Module):
     def __init__(self, num_classes: int, num_input_node_features: int, num_layers: int,
@@ -58,7 +64,8 @@ class GATModel(nn.Module):
         skip = self.skip_layer_list[skip_count]
         nh, f = self.num_heads_per_layer[i + 1], self.head_output_features_per_layer[i + 1]
         mean = not self.heads_concat_per_layer[i]
-        if isinstance(skip, nn.Linear) and not torch.compiler.is_compiling():
+        if (isinstance(skip, nn.Linear) and not torch.compiler.is_compiling()
+                and layer_input.size(0) * skip.weight.numel() >= SKIP_GEMM_MIN_MACS):
             from .functional import SkipProjectionFunction
             return SkipProjectionFunction.apply(layer_input, skip.weight, nh, f, mean)
         skip_output = skip(layer_input)
