@@ -683,11 +683,11 @@ __global__ void __launch_bounds__(256) node_scores_reg_kernel(const float* __res
 // models/gat_layer.py:109-110): alpha[e', h] = ex / (den[dst] + 1e-8), one thread per CSR slot,
 // all heads of an edge written together (one random 4*NH-byte store per edge instead of NH
 // scattered dwords). Also records the argmax (edge, head) entries for max()'s gradient.
-template <int NHC>
+template <int NHC, bool const_att>
 __global__ void __launch_bounds__(256) attention_alpha_kernel(
     const int32_t* __restrict__ col, const int32_t* __restrict__ rowidx,
     const int32_t* __restrict__ perm, int64_t E2, const float* __restrict__ S,
-    const uint32_t* __restrict__ M_ord, const float* __restrict__ den, int NH_rt, int const_att,
+    const uint32_t* __restrict__ M_ord, const float* __restrict__ den, int NH_rt,
     float* __restrict__ alpha, long long* __restrict__ argmax) {
   constexpr int VEC = (NHC % 4 == 0) ? 4 : ((NHC % 2 == 0) ? 2 : 1);
   const int NH = NHC > 0 ? NHC : NH_rt, S2 = 2 * NH;
@@ -697,23 +697,27 @@ __global__ void __launch_bounds__(256) attention_alpha_kernel(
     const int64_t s = col[e], d = rowidx[e];
     float* out = alpha + (int64_t)perm[e] * NH;
     if constexpr (NHC > 0) {
+      // constant attention (compile-time) has no score matrix — S is a placeholder — so it is
+      // never read
       float ss[NHC], sd[NHC], dn[NHC], a[NHC];
 #pragma unroll
       for (int h = 0; h < NHC; h += VEC) {
         if constexpr (VEC == 4) {
-          const float4 x = *(const float4*)(S + s * S2 + h);
-          const float4 y = *(const float4*)(S + d * S2 + NHC + h);
+          const float4 x = const_att ? float4{} : *(const float4*)(S + s * S2 + h);
+          const float4 y = const_att ? float4{} : *(const float4*)(S + d * S2 + NHC + h);
           const float4 z = *(const float4*)(den + d * NHC + h);
           ss[h] = x.x; ss[h + 1] = x.y; ss[h + 2] = x.z; ss[h + 3] = x.w;
           sd[h] = y.x; sd[h + 1] = y.y; sd[h + 2] = y.z; sd[h + 3] = y.w;
           dn[h] = z.x; dn[h + 1] = z.y; dn[h + 2] = z.z; dn[h + 3] = z.w;
         } else if constexpr (VEC == 2) {
-          const float2 x = *(const float2*)(S + s * S2 + h);
-          const float2 y = *(const float2*)(S + d * S2 + NHC + h);
+          const float2 x = const_att ? float2{} : *(const float2*)(S + s * S2 + h);
+          const float2 y = const_att ? float2{} : *(const float2*)(S + d * S2 + NHC + h);
           const float2 z = *(const float2*)(den + d * NHC + h);
           ss[h] = x.x; ss[h + 1] = x.y; sd[h] = y.x; sd[h + 1] = y.y; dn[h] = z.x; dn[h + 1] = z.y;
         } else {
-          ss[h] = S[s * S2 + h]; sd[h] = S[d * S2 + NHC + h]; dn[h] = den[d * NHC + h];
+          ss[h] = const_att ? 0.f : S[s * S2 + h];
+          sd[h] = const_att ? 0.f : S[d * S2 + NHC + h];
+          dn[h] = den[d * NHC + h];
         }
       }
       bool hit = false;
@@ -760,11 +764,11 @@ __global__ void __launch_bounds__(256) attention_alpha_kernel(
 // (coalesced) and writes alpha[p] (coalesced): the CSR-order kernel above scatters its writes
 // through perm (each 4*NH-byte row a separate partial granule). Tied argmax entries are
 // recorded by CSR slot as above, found by a scan of dst's segment (ties are rare).
-template <int NHC, typename I>
+template <int NHC, typename I, bool const_att>
 __global__ void __launch_bounds__(256) attention_alpha_ei_kernel(
     const I* __restrict__ ei, int64_t ld_, int64_t E2b, const long long* e2p,
     const float* __restrict__ S,
-    const uint32_t* __restrict__ M_ord, const float* __restrict__ den, int NH_rt, int const_att,
+    const uint32_t* __restrict__ M_ord, const float* __restrict__ den, int NH_rt,
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ perm,
     float* __restrict__ alpha, long long* __restrict__ argmax) {
   const int64_t E2 = e2p ? min(E2b, (int64_t)*e2p) : E2b;
@@ -789,7 +793,7 @@ __global__ void __launch_bounds__(256) attention_alpha_ei_kernel(
       for (int u = 0; u < UE; ++u)
 #pragma unroll
         for (int h = 0; h < NHC; ++h) {
-          a[u][h] = S[sv[u] * S2 + h] + S[dv[u] * S2 + NHC + h];
+          a[u][h] = const_att ? 0.f : S[sv[u] * S2 + h] + S[dv[u] * S2 + NHC + h];
           dn[u][h] = den[dv[u] * NHC + h];
         }
 #pragma unroll
@@ -826,7 +830,7 @@ __global__ void __launch_bounds__(256) attention_alpha_ei_kernel(
       float* out = alpha + p * NH;
       bool hit = false;
       for (int h = 0; h < NH; ++h) {
-        const float raw = S[s * S2 + h] + S[d * S2 + NH + h];
+        const float raw = const_att ? 0.f : S[s * S2 + h] + S[d * S2 + NH + h];
         hit |= (!const_att && raw == M);
         out[h] = (const_att ? 1.f : att_exp(raw, M)) / (den[d * NH + h] + kSoftmaxEps);
       }
@@ -942,8 +946,12 @@ extern "C" int gatx_attention_alpha(const int32_t* col, const int32_t* rowidx,
   hipStream_t st = (hipStream_t)s;
   const unsigned grid = grid_for(E2, 256, 8192);
 #define GATX_AL(C)                                                                             \
-  attention_alpha_kernel<C><<<grid, 256, 0, st>>>(col, rowidx, perm, E2, S, M_ord, den, NH,   \
-                                                  const_att, alpha, (long long*)argmax)
+  do {                                                                                         \
+    if (const_att) attention_alpha_kernel<C, true><<<grid, 256, 0, st>>>(                      \
+        col, rowidx, perm, E2, S, M_ord, den, NH, alpha, (long long*)argmax);                  \
+    else attention_alpha_kernel<C, false><<<grid, 256, 0, st>>>(                               \
+        col, rowidx, perm, E2, S, M_ord, den, NH, alpha, (long long*)argmax);                  \
+  } while (0)
   switch (NH) {
     case 1: GATX_AL(1); break; case 2: GATX_AL(2); break; case 4: GATX_AL(4); break;
     case 6: GATX_AL(6); break; case 8: GATX_AL(8); break; default: GATX_AL(0); break;
@@ -964,9 +972,14 @@ extern "C" int gatx_attention_alpha_ei(const void* edge_index, int is64, int64_t
   const unsigned grid = grid_for(ceil_div(E2, 4), 256, 8192);   // 4 edges per thread
   const long long* e2p = (const long long*)e2;
 #define GATX_AE(C, I)                                                                          \
-  attention_alpha_ei_kernel<C, I><<<grid, 256, 0, st>>>((const I*)edge_index, ld, E2, e2p, S,  \
-                                                        M_ord, den, NH, const_att, rowptr,     \
-                                                        perm, alpha, (long long*)argmax)
+  do {                                                                                         \
+    if (const_att) attention_alpha_ei_kernel<C, I, true><<<grid, 256, 0, st>>>(                \
+        (const I*)edge_index, ld, E2, e2p, S, M_ord, den, NH, rowptr, perm, alpha,             \
+        (long long*)argmax);                                                                   \
+    else attention_alpha_ei_kernel<C, I, false><<<grid, 256, 0, st>>>(                         \
+        (const I*)edge_index, ld, E2, e2p, S, M_ord, den, NH, rowptr, perm, alpha,             \
+        (long long*)argmax);                                                                   \
+  } while (0)
 #define GATX_AEI(I)                                                                            \
   switch (NH) {                                                                                \
     case 1: GATX_AE(1, I); break; case 2: GATX_AE(2, I); break; case 4: GATX_AE(4, I); break;  \

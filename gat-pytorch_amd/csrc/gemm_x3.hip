@@ -106,13 +106,6 @@ struct X3Tile {
       *(uint2*)(img + 2 * Img::BYTES + o) = make_uint2(l0, l1);
     }
   }
-  // MFMA 16x16x32 operand fragment whose k 0-15 come from plane P and k 16-31 from plane Q
-  // (rows rb..rb+15 of this 16-k tile): one product A_P B_P' + A_Q B_Q' per instruction.
-  static __device__ inline bf16x8 frag16(const char* P, const char* Q, int rb, int lane) {
-    static_assert(KC, "16x16x32 fragments read k-contiguous images");
-    const char* pl = (lane >> 5) ? Q : P;
-    return *(const bf16x8*)(pl + Img::off(rb + (lane & 15), 8 * ((lane >> 4) & 1)));
-  }
   // MFMA 32x32x16 operand fragment of rows rb..rb+31, k = k16..k16+15 from one plane.
   static __device__ inline bf16x8 frag(const char* plane, int rb, int k16, int lane) {
     if (KC) {
@@ -208,23 +201,20 @@ __device__ inline void x3_mainloop(const GemmArgs& g, const float* __restrict__ 
   store(smem, kb);
   __syncthreads();
   bf16x8 fa[MB][3], fb[NB][3];
-  for (int64_t kt = 0; kt < nk; ++kt) {
-    char* cur = smem + (kt & 1) * STAGE;
-    char* nxt = smem + ((kt & 1) ^ 1) * STAGE;
-    const bool more = kt + 1 < nk;
-    if (more && DBG < 3) load(kb + (kt + 1) * BK);
+  constexpr int PLA[6] = {2, 0, 1, 1, 0, 0};
+  constexpr int PLB[6] = {0, 2, 1, 0, 1, 0};
+  int64_t kt = 0;
+  auto frags = [&](const char* cur) {
 #pragma unroll
     for (int p = 0; p < 3; ++p) {
-      if (DBG == 4 && kt > 0) break;   // probe: fragments of the first K-tile reused
 #pragma unroll
       for (int x = 0; x < MB; ++x) fa[x][p] = TA::frag(cur + p * PA, wm * (MB * 32) + x * 32, 0, lane);
 #pragma unroll
       for (int x = 0; x < NB; ++x)
         fb[x][p] = TB::frag(cur + 3 * PA + p * PBy, wn * (NB * 32) + x * 32, 0, lane);
     }
-    // small terms first: (l,h) (h,l) (m,m) (m,h) (h,m) (h,h)
-    constexpr int PLA[6] = {2, 0, 1, 1, 0, 0};
-    constexpr int PLB[6] = {0, 2, 1, 0, 1, 0};
+  };
+  auto mfmas = [&]() {
 #pragma unroll
     for (int t = 0; t < 6; ++t)
 #pragma unroll
@@ -233,86 +223,58 @@ __device__ inline void x3_mainloop(const GemmArgs& g, const float* __restrict__ 
         for (int ni = 0; ni < NB; ++ni)
           acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[mi][PLA[t]], fb[ni][PLB[t]],
                                                                 acc[mi][ni], 0, 0, 0);
-    if (more && DBG < 2) store(nxt, kb + (kt + 1) * BK);
-    if (DBG != 4) __syncthreads();
-  }
-}
-
-typedef float floatx4 __attribute__((ext_vector_type(4)));
-
-// Probe (GATX_X3_DBG=6): the lock-step loop on v_mfma_f32_16x16x32_bf16, the six products as
-// three K=32 instructions over plane pairs: [h|m]x[h|m] = hh + mm, [h|m]x[m|h] = hm + mh,
-// [h|l]x[l|h] = hl + lh. Plain store epilogue (no bias / residual / ELU / splits).
-template <bool MASK>
-__device__ inline void x3_mainloop16(const GemmArgs& g, const float* __restrict__ A,
-                                     const float* __restrict__ B, int64_t m0, int64_t n0,
-                                     int64_t kb, int64_t K, int64_t nk, char* smem, int wm,
-                                     int wn, int lane, floatx4 (&acc)[8][4]) {
-  using C = X3Cfg<1>;
-  constexpr int NT = C::NT, BK = C::BK;
-  using TA = X3Tile<true, C::TBM, BK, NT, 0>;
-  using TB = X3Tile<true, C::TBN, BK, NT, 0>;
-  constexpr int PA = TA::Img::BYTES, PBy = TB::Img::BYTES;
-  constexpr int STAGE = 3 * (PA + PBy);
-  const int64_t M = g.M, N = g.N;
-  float4 va[TA::NV], vb[TB::NV];
-  const float* pa[TA::NV];
-  const float* pb[TB::NV];
-  int64_t sa = 0, sb = 0;
-  TA::setup(A, g.lda, m0, M, kb, pa, sa);
-  TB::setup(B, g.ldb, n0, N, kb, pb, sb);
-  auto load = [&](int64_t k0) {   // probe: K % 16 == 0 assumed
-    (void)k0;
+  };
+  auto load_full = [&]() {
 #pragma unroll
     for (int c = 0; c < TA::NV; ++c) { va[c] = *(const float4*)pa[c]; pa[c] += sa; }
 #pragma unroll
     for (int c = 0; c < TB::NV; ++c) { vb[c] = *(const float4*)pb[c]; pb[c] += sb; }
   };
-  auto store = [&](char* st, int64_t k0) {
-    TA::template store<false, false>(st, va, m0, M, k0, K);
-    TB::template store<false, false>(st + 3 * PA, vb, n0, N, k0, K);
+  auto store_full = [&](char* st) {
+    TA::template store<false, false>(st, va, m0, M, 0, K);
+    TB::template store<false, false>(st + 3 * PA, vb, n0, N, 0, K);
   };
-  load(kb);
-  store(smem, kb);
-  __syncthreads();
-  for (int64_t kt = 0; kt < nk; ++kt) {
-    const char* cur = smem + (kt & 1) * STAGE;
+  if constexpr (!MASK && DBG <= 1 && CFG == 1) {
+    // Steady state (full K-tiles, no branches): operands one K-tile further ahead. Tile kt + 1
+    // (loaded during iteration kt - 1) is split into the other stage right after this tile's
+    // fragment reads, then tile kt + 2's loads go out, then the MFMAs: the LDS stores drain under
+    // the MFMAs instead of just ahead of the barrier, and the global loads have a whole
+    // iteration to land. -5 to -6% against load-at-top / store-at-bottom on the PPI projection
+    // and 8192 x 4096 x 4096 shapes (tools/gpu_x3_ab.sh); forcing an interleave with
+    // sched_group_barrier was slower than the compiler's schedule. A partial last tile and the
+    // unaligned (MASK) path take the generic loop below, and so does CFG 0 (three workgroups per
+    // CU: the extra live operands spill under its 168-VGPR cap).
+    const int64_t nfull = (K - kb) / BK;
+    if (nfull >= 2) {
+      load_full();   // tile 1
+      for (; kt + 2 < nfull; ++kt) {
+        char* cur = smem + (kt & 1) * STAGE;
+        char* nxt = smem + ((kt & 1) ^ 1) * STAGE;
+        frags(cur);
+        store_full(nxt);
+        load_full();
+        mfmas();
+        __syncthreads();
+      }
+      char* cur = smem + (kt & 1) * STAGE;
+      char* nxt = smem + ((kt & 1) ^ 1) * STAGE;
+      frags(cur);
+      store_full(nxt);
+      mfmas();
+      __syncthreads();
+      ++kt;
+    }
+  }
+  for (; kt < nk; ++kt) {
+    char* cur = smem + (kt & 1) * STAGE;
     char* nxt = smem + ((kt & 1) ^ 1) * STAGE;
     const bool more = kt + 1 < nk;
-    if (more) load(kb + (kt + 1) * BK);
-    const char* ah = cur; const char* am = cur + PA; const char* al = cur + 2 * PA;
-    const char* bh = cur + 3 * PA; const char* bm = bh + PBy; const char* bl = bh + 2 * PBy;
-    bf16x8 fhm[8], fhl[8], gbhm[4], gbmh[4], gblh[4];
-#pragma unroll
-    for (int x = 0; x < 8; ++x) {
-      fhm[x] = TA::frag16(ah, am, wm * 128 + x * 16, lane);
-      fhl[x] = TA::frag16(ah, al, wm * 128 + x * 16, lane);
-    }
-#pragma unroll
-    for (int x = 0; x < 4; ++x) {
-      gbhm[x] = TB::frag16(bh, bm, wn * 64 + x * 16, lane);
-      gbmh[x] = TB::frag16(bm, bh, wn * 64 + x * 16, lane);
-      gblh[x] = TB::frag16(bl, bh, wn * 64 + x * 16, lane);
-    }
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni)
-        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fhl[mi], gblh[ni], acc[mi][ni], 0, 0, 0);
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni)
-        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fhm[mi], gbmh[ni], acc[mi][ni], 0, 0, 0);
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni)
-        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fhm[mi], gbhm[ni], acc[mi][ni], 0, 0, 0);
-    if (more) store(nxt, kb + (kt + 1) * BK);
-    __syncthreads();
+    if (more && DBG < 3) load(kb + (kt + 1) * BK);
+    if (DBG != 4 || kt == 0) frags(cur);   // probe 4: fragments of the first K-tile reused
+    mfmas();   // small terms first: (l,h) (h,l) (m,m) (m,h) (h,m) (h,h)
+    if (more && DBG < 2) store(nxt, kb + (kt + 1) * BK);
+    if (DBG != 4) __syncthreads();
   }
-  (void)MASK;
 }
 
 template <bool A_KC, bool B_KC, bool VEC, int TAG, int CFG, int DBG = 0>
@@ -348,27 +310,6 @@ __global__ void __launch_bounds__(X3Cfg<CFG>::NT, X3Cfg<CFG>::MINB) gemm_x3_kern
   const float* __restrict__ B = g.B + blockIdx.y * g.b_bs;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave / C::WGN, wn = wave % C::WGN;
-  if constexpr (DBG == 6) {
-    floatx4 a16[8][4];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) a16[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-    const int64_t nk16 = K > kb ? ceil_div(K - kb, C::BK) : 0;
-    if (nk16 > 0) x3_mainloop16<false>(g, A, B, m0, n0, kb, K, nk16, smem, wm, wn, lane, a16);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int64_t row = m0 + wm * 128 + i * 16 + (lane >> 4) * 4 + r;
-          const int64_t col = n0 + wn * 64 + j * 16 + (lane & 15);
-          if (row < g.M && col < g.N) g.C0[row * g.ldc0 + col] = a16[i][j][r];
-        }
-    return;
-  }
-
   floatx16 acc[C::MB][C::NB];
 #pragma unroll
   for (int i = 0; i < C::MB; ++i)
@@ -397,7 +338,7 @@ int launch_gemm_x3(const gk::GemmArgs& g, bool a_kc, bool b_kc, int batch, int t
   const int cfg = g.bm == 256 ? 1 : 0;
   // tuning probes only (wrong results): GATX_X3_DBG=1 conversion without the split arithmetic,
   // 2 no next-tile LDS stores, 3 no operand loads or stores, 4 MFMAs only (no LDS reads after the
-  // first K-tile, no barriers); 6 = the 16x16x32 MFMA shape (plain epilogue)
+  // first K-tile, no barriers)
   static const int dbg = [] {
     const char* e = getenv("GATX_X3_DBG");
     return e ? atoi(e) : 0;
@@ -407,8 +348,7 @@ int launch_gemm_x3(const gk::GemmArgs& g, bool a_kc, bool b_kc, int batch, int t
       if (dbg == 1) gemm_x3_kernel<true, true, true, 0, 1, 1><<<grid, 512, 0, stream>>>(g);
       else if (dbg == 2) gemm_x3_kernel<true, true, true, 0, 1, 2><<<grid, 512, 0, stream>>>(g);
       else if (dbg == 3) gemm_x3_kernel<true, true, true, 0, 1, 3><<<grid, 512, 0, stream>>>(g);
-      else if (dbg == 4) gemm_x3_kernel<true, true, true, 0, 1, 4><<<grid, 512, 0, stream>>>(g);
-      else gemm_x3_kernel<true, true, true, 0, 1, 6><<<grid, 512, 0, stream>>>(g);
+      else gemm_x3_kernel<true, true, true, 0, 1, 4><<<grid, 512, 0, stream>>>(g);
     } else {
       if (dbg == 1) gemm_x3_kernel<true, true, true, 0, 0, 1><<<grid, 256, 0, stream>>>(g);
       else gemm_x3_kernel<true, true, true, 0, 0, 2><<<grid, 256, 0, stream>>>(g);

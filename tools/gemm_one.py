@@ -29,3 +29,10 @@ for i in range(reps + 1):
 e.record(); torch.cuda.synchronize()
 t = s.elapsed_time(e) / reps
 print(f"mode {mode} {lay} {M}x{Nc}x{K}: {t*1e3:.1f} us {2.0*M*Nc*K/t/1e9:.1f} TF")
+if os.environ.get("GEMM_CHECK"):
+    torch.backends.cuda.matmul.allow_tf32 = False
+    Am = A if lay[0] == "n" else A.t()
+    Bm = B.t() if lay[1] == "t" else B
+    ref = (Am[:512].double() @ Bm.double())
+    err = ((C[:512].double() - ref).abs().max() / ref.abs().max()).item()
+    print(f"  check rows 0-511: max rel err {err:.2e}")
