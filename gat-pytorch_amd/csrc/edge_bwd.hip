@@ -53,7 +53,8 @@ __global__ void __launch_bounds__(256) prepare_go_kernel(const float* __restrict
                                                          int64_t N, int NH, int F, int Fp,
                                                          int concat, int elu,
                                                          float* __restrict__ go,
-                                                         float* __restrict__ g_pre) {
+                                                         float* __restrict__ g_pre,
+                                                         int64_t pre_ld) {
   const int OC = concat ? NH * F : F, GW = concat ? NH * Fp : Fp;
   const float scale = concat ? 1.f : 1.f / (float)NH;
   const int64_t total = N * GW;
@@ -69,7 +70,7 @@ __global__ void __launch_bounds__(256) prepare_go_kernel(const float* __restrict
         const float o = out[src];
         v = o > 0.f ? v : v * (o + 1.f);   // d elu(x) = elu(x) + 1 for x <= 0
       }
-      if (g_pre) g_pre[src] = v;
+      if (g_pre) g_pre[n * pre_ld + (concat ? h * F + f : f)] = v;
     }
     go[t] = v * scale;
   }
@@ -716,9 +717,12 @@ using namespace gatx;
     }                                                                                          \
   } while (0)
 
-extern "C" int gatx_prepare_go(const float* g_out, const float* out, int64_t N, int NH, int F,
-                               int concat, int elu, float* go, float* g_pre, gatx_stream_t s) {
+extern "C" int gatx_prepare_go_ex(const float* g_out, const float* out, int64_t N, int NH,
+                                  int F, int concat, int elu, float* go, float* g_pre,
+                                  int64_t pre_ld, gatx_stream_t s) {
   if (N == 0) return 0;
+  const int64_t OC = concat ? (int64_t)NH * F : F;
+  GATX_REQUIRE(pre_ld >= OC, "prepare_go: g_pre row stride below the output width");
   const int Fp = (int)round_up(F, 4);
   const int64_t GW = concat ? (int64_t)NH * Fp : Fp;
   GATX_REQUIRE(!elu || out, "prepare_go: elu needs the forward output");
@@ -726,7 +730,7 @@ extern "C" int gatx_prepare_go(const float* g_out, const float* out, int64_t N, 
                "prepare_go: g_pre may alias go only for concat layers with F % 4 == 0");
   const bool aligned = ((uintptr_t)g_out % 16 == 0) && ((uintptr_t)go % 16 == 0) &&
                        (!elu || (uintptr_t)out % 16 == 0) && ((uintptr_t)g_pre % 16 == 0);
-  if (F % 4 == 0 && aligned) {
+  if (F % 4 == 0 && aligned && pre_ld == OC) {
     const int64_t n4 = N * GW / 4;
     prepare_go_vec_kernel<<<grid_for(ceil_div(n4, 4), 256, 8192), 256, 0, (hipStream_t)s>>>(
         (const float4*)g_out, (const float4*)out, n4, elu, concat ? 1.f : 1.f / (float)NH,
@@ -735,9 +739,16 @@ extern "C" int gatx_prepare_go(const float* g_out, const float* out, int64_t N, 
     return 0;
   }
   prepare_go_kernel<<<grid_for(N * GW), 256, 0, (hipStream_t)s>>>(g_out, out, N, NH, F, Fp,
-                                                                  concat, elu, go, g_pre);
+                                                                  concat, elu, go, g_pre,
+                                                                  pre_ld);
   GATX_LAUNCH_CHECK("prepare_go");
   return 0;
+}
+
+extern "C" int gatx_prepare_go(const float* g_out, const float* out, int64_t N, int NH, int F,
+                               int concat, int elu, float* go, float* g_pre, gatx_stream_t s) {
+  return gatx_prepare_go_ex(g_out, out, N, NH, F, concat, elu, go, g_pre,
+                            concat ? (int64_t)NH * F : F, s);
 }
 
 extern "C" int gatx_edge_backward_dst_ex(const float* rows, int64_t row_stride,

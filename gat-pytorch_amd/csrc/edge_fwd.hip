@@ -550,14 +550,22 @@ __global__ void __launch_bounds__(256) waug_assemble_kernel(const float* __restr
                                                             const float* __restrict__ partial,
                                                             int n_cb, int NH, int F, int Fp,
                                                             int H2, int64_t F_in,
-                                                            float* __restrict__ W_aug) {
+                                                            float* __restrict__ W_aug,
+                                                            const float* __restrict__ W_skip,
+                                                            int skip_heads, int64_t skip_cols) {
   const int64_t Dp = (int64_t)NH * Fp;
-  const int64_t total = (Dp + H2) * F_in;
+  const int64_t nmain = (Dp + H2) * F_in, sk = skip_cols * F_in;
+  const int64_t total = nmain + sk;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = t / F_in, i = t - r * F_in;
     float v;
-    if (r < Dp) {
+    if (t >= nmain) {   // folded skip rows: mean over the skip's head blocks (a copy for 1)
+      const int64_t q = t - nmain;
+      v = W_skip[q];
+      for (int h = 1; h < skip_heads; ++h) v += W_skip[(int64_t)h * sk + q];
+      if (skip_heads > 1) v /= (float)skip_heads;
+    } else if (r < Dp) {
       const int h = (int)(r / Fp), f = (int)(r - (int64_t)h * Fp);
       v = (f < F) ? W[((int64_t)h * F + f) * F_in + i] : 0.f;
     } else {
@@ -566,6 +574,18 @@ __global__ void __launch_bounds__(256) waug_assemble_kernel(const float* __restr
       for (int cb = 0; cb < n_cb; ++cb) v += partial[((int64_t)cb * H2 + h2) * F_in + i];
     }
     W_aug[t] = v;
+  }
+}
+
+// Its gradient: g_W[(h * cols + c)][i] = g_eff[c][i] / heads for every head block.
+__global__ void __launch_bounds__(256) skip_grad_kernel(const float* __restrict__ g_eff,
+                                                        int heads, int64_t cols, int64_t F_in,
+                                                        float* __restrict__ g_W) {
+  const int64_t total = cols * F_in;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < heads * total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = t % total;
+    g_W[t] = heads > 1 ? g_eff[r] / (float)heads : g_eff[r];
   }
 }
 
@@ -875,9 +895,13 @@ int launch_edge_forward(unsigned grid, size_t lds, hipStream_t st, const EdgeFwd
 
 using namespace gatx;
 
-extern "C" int gatx_prepare_weights(const float* W, const float* a, int NH, int F, int64_t F_in,
-                                    float* W_aug, gatx_stream_t s) {
+extern "C" int gatx_prepare_weights_skip(const float* W, const float* a, int NH, int F,
+                                         int64_t F_in, const float* W_skip, int skip_heads,
+                                         int64_t skip_cols, float* W_aug, gatx_stream_t s) {
   hipStream_t st = (hipStream_t)s;
+  if (!W_skip) skip_cols = 0;
+  GATX_REQUIRE(skip_cols >= 0 && (skip_cols == 0 || skip_heads >= 1),
+               "prepare_weights: bad skip sizes");
   GATX_REQUIRE(NH >= 1 && F >= 1 && F_in >= 1, "prepare_weights: bad sizes");
   const int Fp = (int)round_up(F, 4);
   const int H2 = a ? 2 * NH : 0;
@@ -888,15 +912,36 @@ extern "C" int gatx_prepare_weights(const float* W, const float* a, int NH, int 
   if (H2) {
     // split-K partials are staged in the tail of the caller's buffer, which holds
     // gatx_prepare_weights_floats() floats: (Dp + 2NH) * F_in for W_aug + n_cb * 2NH * F_in.
-    partial = W_aug + ((int64_t)NH * Fp + H2) * F_in;
+    partial = W_aug + ((int64_t)NH * Fp + H2 + skip_cols) * F_in;
     dim3 g((unsigned)ceil_div(F_in, 64), (unsigned)n_cb);
     weff_partial_kernel<<<g, 256, 0, st>>>(W, a, NH, F, F_in, partial);
     GATX_LAUNCH_CHECK("weff_partial");
   }
-  waug_assemble_kernel<<<grid_for(((int64_t)NH * Fp + H2) * F_in), 256, 0, st>>>(
-      W, partial, n_cb, NH, F, Fp, H2, F_in, W_aug);
+  waug_assemble_kernel<<<grid_for(((int64_t)NH * Fp + H2 + skip_cols) * F_in), 256, 0, st>>>(
+      W, partial, n_cb, NH, F, Fp, H2, F_in, W_aug, W_skip, skip_heads, skip_cols);
   GATX_LAUNCH_CHECK("waug_assemble");
   return 0;
+}
+
+extern "C" int gatx_prepare_weights(const float* W, const float* a, int NH, int F, int64_t F_in,
+                                    float* W_aug, gatx_stream_t s) {
+  return gatx_prepare_weights_skip(W, a, NH, F, F_in, nullptr, 1, 0, W_aug, s);
+}
+
+extern "C" int gatx_skip_weight_grad(const float* g_eff, int heads, int64_t cols, int64_t F_in,
+                                     float* g_W, gatx_stream_t s) {
+  GATX_REQUIRE(heads >= 1 && cols >= 0 && F_in >= 0, "skip_weight_grad: bad sizes");
+  if (cols == 0 || F_in == 0) return 0;
+  skip_grad_kernel<<<grid_for(heads * cols * F_in), 256, 0, (hipStream_t)s>>>(g_eff, heads, cols,
+                                                                              F_in, g_W);
+  GATX_LAUNCH_CHECK("skip_grad");
+  return 0;
+}
+
+extern "C" int64_t gatx_prepare_weights_skip_floats(int NH, int F, int64_t F_in, int has_a,
+                                                   int64_t skip_cols) {
+  const int64_t Fp = round_up(F, 4), H2 = has_a ? 2 * NH : 0;
+  return (NH * Fp + H2 + skip_cols + ceil_div((int64_t)NH * F, kWeffRows) * H2) * F_in;
 }
 
 extern "C" int64_t gatx_prepare_weights_floats(int NH, int F, int64_t F_in, int has_a) {

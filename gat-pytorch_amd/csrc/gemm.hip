@@ -368,12 +368,15 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
                      float* C1, int64_t ldc1, int64_t c1_bs, int accumulate, const float* bias,
                      int64_t bias_bs, const float* resid, int64_t resid_ld, int64_t resid_bs,
                      int elu, void* workspace, size_t workspace_bytes, int tag,
-                     hipStream_t stream) {
+                     hipStream_t stream, int64_t n_split2 = -1, float* C2 = nullptr,
+                     int64_t ldc2 = 0) {
   GATX_REQUIRE(M >= 0 && N >= 0 && K >= 0 && batch >= 1, "gemm: negative size");
   if (M == 0 || N == 0) return 0;
   GATX_REQUIRE(sak == 1 || sam == 1, "gemm: A needs a unit stride");
   GATX_REQUIRE(sbn == 1 || sbk == 1, "gemm: B needs a unit stride");
   GATX_REQUIRE(n_split >= N || C1 != nullptr, "gemm: split output needs C1");
+  GATX_REQUIRE(n_split2 < 0 || (n_split2 >= n_split && (n_split2 >= N || C2 != nullptr)),
+               "gemm: third output range needs n_split2 >= n_split and C2");
   GATX_REQUIRE(K > 0 || accumulate, "gemm: K == 0 needs accumulate (output would be zero)");
   if (K == 0) return 0;
   GemmArgs g;
@@ -384,6 +387,8 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
   g.B = B; g.ldb = b_kc ? sbn : sbk; g.b_bs = b_bs;
   g.C0 = C0; g.ldc0 = ldc0; g.c0_bs = c0_bs; g.n_split = n_split;
   g.C1 = C1; g.ldc1 = ldc1; g.c1_bs = c1_bs;
+  g.n_split2 = n_split2 < 0 ? INT64_MAX : n_split2;
+  g.C2 = C2; g.ldc2 = ldc2;
   g.accumulate = accumulate;
   g.bias = bias; g.bias_bs = bias_bs;
   g.resid = resid; g.resid_ld = resid_ld; g.resid_bs = resid_bs;
@@ -471,6 +476,18 @@ extern "C" int gatx_projection_gemm(int64_t M, int64_t N, int64_t K, const float
   return gemm_impl(M, N, K, 1, A, sam, sak, 0, B, sbk, sbn, 0, C0, ldc0, 0, n_split, C1, ldc1, 0,
                    0, nullptr, 0, nullptr, 0, 0, 0, workspace, workspace_bytes, 0,
                    (hipStream_t)s);
+}
+
+extern "C" int gatx_projection_gemm3(int64_t M, int64_t N, int64_t K, const float* A,
+                                     int64_t sam, int64_t sak, const float* B, int64_t sbk,
+                                     int64_t sbn, float* C0, int64_t ldc0, int64_t n_split,
+                                     float* C1, int64_t ldc1, int64_t n_split2, float* C2,
+                                     int64_t ldc2, void* workspace, size_t workspace_bytes,
+                                     gatx_stream_t s) {
+  GATX_REQUIRE(n_split2 >= 0, "projection_gemm3: n_split2 must be >= 0");
+  return gemm_impl(M, N, K, 1, A, sam, sak, 0, B, sbk, sbn, 0, C0, ldc0, 0, n_split, C1, ldc1, 0,
+                   0, nullptr, 0, nullptr, 0, 0, 0, workspace, workspace_bytes, 0,
+                   (hipStream_t)s, n_split2, C2, ldc2);
 }
 
 extern "C" int gatx_gemm_f32_batched(int64_t batch, int64_t M, int64_t N, int64_t K,

@@ -104,6 +104,9 @@ struct GemmArgs {
   float* C0; int64_t ldc0, c0_bs;
   int64_t n_split;
   float* C1; int64_t ldc1, c1_bs;
+  // third output range (the folded skip projection): columns >= n_split2 go to C2 raw
+  int64_t n_split2;
+  float* C2; int64_t ldc2;
   int accumulate, a_vec, b_vec;
   int64_t tiles_m, tiles_n;
   // epilogue on C0 columns: C = elu?(acc (+C) + bias[col] + resid[row][col])
@@ -116,13 +119,15 @@ struct GemmArgs {
   int64_t dp_blocks, tail_rem; int tail_s, bm, bn; float* tail_partial;
 };
 
-// C = elu?(v (+C) + bias + resid) for one output element (columns >= n_split go to C1 raw)
+// C = elu?(v (+C) + bias + resid) for one output element (columns >= n_split go to C1 raw,
+// columns >= n_split2 to C2 raw)
 __device__ inline void store_out(const GemmArgs& g, int64_t b, int64_t row, int64_t col, float v) {
   float* Cb;
   int64_t ldc, c;
   const bool first = col < g.n_split;
   if (first) { Cb = g.C0 + b * g.c0_bs; ldc = g.ldc0; c = col; }
-  else { Cb = g.C1 + b * g.c1_bs; ldc = g.ldc1; c = col - g.n_split; }
+  else if (col < g.n_split2) { Cb = g.C1 + b * g.c1_bs; ldc = g.ldc1; c = col - g.n_split; }
+  else { Cb = g.C2; ldc = g.ldc2; c = col - g.n_split2; }
   float* p = Cb + row * ldc + c;
   if (g.accumulate) v += *p;
   if (first) {
@@ -151,7 +156,8 @@ __device__ inline void store_block(const GemmArgs& g, int64_t b, int64_t row0, i
   float* base;
   int64_t ldc;
   if (first) { base = g.C0 + b * g.c0_bs + col; ldc = g.ldc0; }
-  else { base = g.C1 + b * g.c1_bs + (col - g.n_split); ldc = g.ldc1; }
+  else if (col < g.n_split2) { base = g.C1 + b * g.c1_bs + (col - g.n_split); ldc = g.ldc1; }
+  else { base = g.C2 + (col - g.n_split2); ldc = g.ldc2; }
   const bool has_bias = first && g.bias != nullptr;
   const float* rp = (first && g.resid) ? g.resid + b * g.resid_bs + col : nullptr;
   const bool elu = first && g.elu;

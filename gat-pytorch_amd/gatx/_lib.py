@@ -56,6 +56,12 @@ SIGNATURES = {
     "gatx_pad_rows": (c_i, [P, c_i64, c_i64, c_i64, P, c_i64, P]),
     "gatx_projection_gemm": (c_i, [c_i64, c_i64, c_i64, P, c_i64, c_i64, P, c_i64, c_i64, P,
                                    c_i64, c_i64, P, c_i64, P, c_sz, P]),
+    "gatx_projection_gemm3": (c_i, [c_i64, c_i64, c_i64, P, c_i64, c_i64, P, c_i64, c_i64, P,
+                                    c_i64, c_i64, P, c_i64, c_i64, P, c_i64, P, c_sz, P]),
+    "gatx_prepare_weights_skip": (c_i, [P, P, c_i, c_i, c_i64, P, c_i, c_i64, P, P]),
+    "gatx_prepare_weights_skip_floats": (c_i64, [c_i, c_i, c_i64, c_i, c_i64]),
+    "gatx_prepare_go_ex": (c_i, [P, P, c_i64, c_i, c_i, c_i, c_i, P, P, c_i64, P]),
+    "gatx_skip_weight_grad": (c_i, [P, c_i, c_i64, c_i64, P, P]),
     "gatx_set_debug": (None, [c_i]),
     "gatx_set_gemm_mode": (None, [c_i]),
     "gatx_get_gemm_mode": (c_i, []),

@@ -87,6 +87,9 @@ class LayerShape:
         self.K_aug = self.Dp + self.H2
         self.ldg = _round4(self.K_aug)
         self.out_cols = self.NH * self.F if self.concat else self.F
+        # GATModel's Linear skip folded into the projection (skip_weight=): its out_cols rows
+        # follow W_aug's K_aug rows (0: no folded skip)
+        self.skip_cols = 0
         # derived weights (W_aug, padded W) may be cached: decided by gat_layer() before
         # autograd.Function.forward, inside which grad mode is always off (see _cacheable)
         self.cache_weights = True
@@ -163,11 +166,13 @@ def padded_weight(W, ld: int, use_cache: bool = True):
     return Wp
 
 
-def augmented_weight(W, a, sh: "LayerShape"):
-    """W_aug = [W padded per head; A_src W; A_dst W] (gatx_prepare_weights). Rebuilt every
-    training forward; in no-grad use cached on the parameters' identity and version counters,
-    so inference reuses it across steps while load_state_dict / optimizer steps rebuild it (see
-    _cacheable for the `.data` caveat)."""
+def augmented_weight(W, a, sh: "LayerShape", skip_W=None):
+    """W_aug = [W padded per head; A_src W; A_dst W] (gatx_prepare_weights), followed, when
+    GATModel's Linear skip is folded in (skip_W), by its out_cols rows W_skip_eff
+    (gatx_skip_weight_rows: the head mean folded into the weight for a head-mean layer). Rebuilt
+    every training forward; in no-grad use cached on the parameters' identity and version
+    counters, so inference reuses it across steps while load_state_dict / optimizer steps rebuild
+    it (see _cacheable for the `.data` caveat)."""
     global _WAUG_CACHE
     from collections import OrderedDict
     if _WAUG_CACHE is None:
@@ -175,17 +180,22 @@ def augmented_weight(W, a, sh: "LayerShape"):
     use_cache = sh.cache_weights
     key = (W.data_ptr(), version(W), tuple(W.shape), W.device,
            a.data_ptr() if a is not None else 0, version(a) if a is not None else -1,
-           sh.NH, sh.F)
+           sh.NH, sh.F, sh.concat if skip_W is not None else None,
+           skip_W.data_ptr() if skip_W is not None else 0,
+           version(skip_W) if skip_W is not None else -1)
     hit = _WAUG_CACHE.get(key) if use_cache else None
     if hit is not None:
         _WAUG_CACHE.move_to_end(key)
         return hit[2]
-    waug_floats = lib.gatx_prepare_weights_floats(sh.NH, sh.F, sh.F_in, int(a is not None))
+    C = sh.out_cols if skip_W is not None else 0
+    waug_floats = lib.gatx_prepare_weights_skip_floats(sh.NH, sh.F, sh.F_in, int(a is not None), C)
     W_aug = torch.empty(waug_floats, dtype=torch.float32, device=W.device)
     with _span("prepare_weights", (sh.NH, sh.F, sh.F_in)):
-        call("gatx_prepare_weights", ptr(W), ptr(a), sh.NH, sh.F, sh.F_in, ptr(W_aug), stream())
+        call("gatx_prepare_weights_skip", ptr(W), ptr(a), sh.NH, sh.F, sh.F_in, ptr(skip_W),
+             1 if sh.concat else sh.NH, C, ptr(W_aug), stream())
     if use_cache:
-        _WAUG_CACHE[key] = (W, a, W_aug)   # holding W / a pins their storage (no pointer reuse)
+        # holding W / a / skip_W pins their storage (no pointer reuse)
+        _WAUG_CACHE[key] = (W, a, W_aug, skip_W)
         while len(_WAUG_CACHE) > 16:
             _WAUG_CACHE.popitem(last=False)
     return W_aug
@@ -282,9 +292,11 @@ def reassoc_heads_per_item(sh: LayerShape) -> int:
 
 
 def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: int,
-                  resid=None, elu=False):
+                  resid=None, elu=False, skip_W=None):
     """Returns out (= elu?(layer(x) + resid) when fused), alpha (edge_index' order) and the saved
-    state for the backward."""
+    state for the backward. skip_W: GATModel's Linear skip folded into the projection GEMM (its
+    rows appended to W_aug; the GEMM writes the skip output R as a third output range and the
+    edge pass / output projection epilogue adds it): resid = x W_skip_eff^T without a launch."""
     N = x.size(0)
     dev = x.device
     s = stream()
@@ -297,8 +309,12 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
     # argmax[0] (tie count) is reset by gatx_attention_max; M_ord is written by it
     argmax = torch.empty(ARGMAX_CAP + 2, dtype=torch.int64, device=dev)
     M_ord = torch.empty(1, dtype=torch.int32, device=dev)
+    C = sh.skip_cols
+    R = torch.empty((N, C), **f32) if C else None   # the folded skip's output
+    if R is not None:
+        resid = R
     resid_p = ptr(resid) if resid is not None else None
-    W_aug = augmented_weight(W, a, sh)
+    W_aug = augmented_weight(W, a, sh, skip_W)
     saved = dict(W_aug=W_aug, M_ord=M_ord, den=den, argmax=argmax, Wh=None)
     if use_reassociation(sh):
         Fin_p = _round4(sh.F_in)
@@ -308,11 +324,15 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
         else:
             x_rows = x
         S = torch.empty((N, max(sh.H2, 1)), **f32)
+        if not sh.const or C:
+            # S = x [A_src W; A_dst W]^T, and the folded skip's R = x W_skip_eff^T from the rows
+            # after them as the second output range of the same launch
+            with _span("gemm_scores", (N, sh.H2 + C, sh.F_in)):
+                call("gatx_gemm_f32", N, sh.H2 + C, sh.F_in, ptr(x), sh.F_in, 1,
+                     ptr(W_aug) + 4 * sh.Dp * sh.F_in, 1, sh.F_in, ptr(S), max(sh.H2, 1), sh.H2,
+                     ptr(R) if C else None, max(C, 1), 0,
+                     *gemm_workspace(N, sh.H2 + C, sh.F_in, dev), s)
         if not sh.const:
-            with _span("gemm_scores", (N, sh.H2, sh.F_in)):
-                call("gatx_gemm_f32", N, sh.H2, sh.F_in, ptr(x), sh.F_in, 1,
-                     ptr(W_aug) + 4 * sh.Dp * sh.F_in, 1, sh.F_in, ptr(S), sh.H2, sh.H2, None,
-                     0, 0, *gemm_workspace(N, sh.H2, sh.F_in, dev), s)
             with _span("attention_max", (E2, sh.NH)):
                 call("gatx_attention_max", ptr(graph.col), ptr(graph.rowidx), E2, graph.e2_ptr,
                      ptr(S), sh.NH, ptr(M_ord), ptr(argmax), ptr(_max_ws(dev)), s)
@@ -337,7 +357,12 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
         return out, alpha, saved
     Wh = torch.empty((N, sh.Dp), **f32)
     S = torch.empty((N, max(sh.H2, 1)), **f32)
-    if fold_scores_into_gemm(sh):
+    if C:   # one launch: [Wh | S | R] = x [W_aug; W_skip_eff]^T into three outputs
+        with _span("gemm", (N, sh.K_aug + C, sh.F_in, sh.NH, sh.F)):
+            call("gatx_projection_gemm3", N, sh.K_aug + C, sh.F_in, ptr(x), sh.F_in, 1,
+                 ptr(W_aug), 1, sh.F_in, ptr(Wh), sh.Dp, sh.Dp, ptr(S), max(sh.H2, 1), sh.K_aug,
+                 ptr(R), C, *gemm_workspace(N, sh.K_aug + C, sh.F_in, dev), s)
+    elif fold_scores_into_gemm(sh):
         with _span("gemm", (N, sh.K_aug, sh.F_in, sh.NH, sh.F)):
             call("gatx_projection_gemm", N, sh.K_aug, sh.F_in, ptr(x), sh.F_in, 1, ptr(W_aug), 1,
                  sh.F_in, ptr(Wh), sh.Dp, sh.Dp, ptr(S), max(sh.H2, 1),
@@ -380,10 +405,12 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
 
 def layer_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShape, p: float,
                    seed: int, saved, need_x: bool, need_W: bool, need_a: bool, need_bias: bool,
-                   out=None, elu=False, need_resid=False, resid_is_x=False):
+                   out=None, elu=False, need_resid=False, resid_is_x=False, need_skip=False):
     """Gradients of layer_forward; returns (g_x, g_W, g_a, g_bias, g_resid). With resid_is_x
     (GATModel's identity skip) the skip gradient is folded into g_x by the g_x GEMM's
-    accumulate epilogue and g_resid is None."""
+    accumulate epilogue and g_resid is None. With a folded Linear skip (sh.skip_cols) its
+    gradient rides in G_aug's last columns: g_x includes it, and with need_skip the gradient of
+    W_skip_eff is left in saved["g_skip_eff"]."""
     N = x.size(0)
     dev = x.device
     s = stream()
@@ -393,7 +420,7 @@ def layer_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShape, 
     graph.ensure_transpose()
     if saved.get("reassoc") and not need_x and not sh.const and sh.NH <= 8:
         return _reassoc_backward(g_out, g_alpha, x, W, a, bias, graph, sh, p, seed, saved,
-                                 need_W, need_a, need_bias, out, elu, need_resid)
+                                 need_W, need_a, need_bias, out, elu, need_resid, need_skip)
     if saved["Wh"] is None:   # reassociated forward never built Wh: project now
         Wh = torch.empty((N, sh.Dp), **f32)
         call("gatx_gemm_f32", N, sh.Dp, sh.F_in, ptr(x), sh.F_in, 1, ptr(saved["W_aug"]), 1,
@@ -401,14 +428,21 @@ def layer_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShape, 
              s)
         saved["Wh"] = Wh
     go = torch.empty((N, sh.Dp if sh.concat else sh.Fp), **f32)
-    g_pre = None
-    if need_resid or (need_bias and elu):
+    C = sh.skip_cols
+    # folded skip: its gradient g_pre occupies G_aug's columns K_aug.. (written by prepare_go),
+    # so the g_x and weight-gradient GEMMs below cover the skip in the same launches
+    ldg = _round4(sh.K_aug + C) if C else sh.ldg
+    G_aug = torch.empty((N, ldg), **f32)
+    g_pre, pre_ld, pre_p = None, sh.out_cols, None
+    if C:
+        pre_ld, pre_p = ldg, ptr(G_aug) + 4 * sh.K_aug
+    elif need_resid or (need_bias and elu):
         # concat with F % 4 == 0: go already is the gradient before the skip-add (same layout,
         # scale 1), and go is dead once the source pass has run, so it doubles as g_pre
         g_pre = go if (sh.concat and sh.F % 4 == 0) else torch.empty((N, sh.out_cols), **f32)
-    call("gatx_prepare_go", ptr(g_out), ptr(out) if elu else None, N, sh.NH, sh.F,
-         int(sh.concat), int(elu), ptr(go), ptr(g_pre), s)
-    G_aug = torch.empty((N, sh.ldg), **f32)
+        pre_p = ptr(g_pre)
+    call("gatx_prepare_go_ex", ptr(g_out), ptr(out) if elu else None, N, sh.NH, sh.F,
+         int(sh.concat), int(elu), ptr(go), pre_p, pre_ld, s)
     g_raw = g_corr = None
     if not sh.const:
         g_raw = torch.empty((sh.NH, max(E2, 1)), **f32)
@@ -417,42 +451,45 @@ def layer_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShape, 
              ptr(saved["den"]), ptr(graph.rowptr), ptr(graph.col), ptr(graph.perm), N, E2,
              sh.NH, sh.F, int(sh.concat), float(p), ptr(seed), ptr(go),
              ptr(g_alpha.contiguous()) if g_alpha is not None else None, ptr(g_raw), ptr(gsd),
-             ptr(G_aug), sh.ldg, s)
+             ptr(G_aug), ldg, s)
     call("gatx_edge_backward_src", ptr(saved["S"]), ptr(saved["M_ord"]), ptr(saved["den"]),
          ptr(graph.srowptr), ptr(graph.scol), ptr(graph.seid), ptr(graph.perm), N, E2, sh.NH,
          sh.F, int(sh.concat), int(sh.const), float(p), ptr(seed), ptr(go), ptr(g_raw), None,
-         ptr(G_aug), sh.ldg, s)
+         ptr(G_aug), ldg, s)
     if not sh.const:   # max()'s share, added into both logit-gradient columns of G_aug
         mws = torch.empty(lib.gatx_max_backward_workspace_bytes(), dtype=torch.uint8, device=dev)
         call("gatx_max_backward", ptr(saved["argmax"]), ptr(gsd), ptr(saved["S"]),
              ptr(saved["M_ord"]), ptr(graph.col), ptr(graph.rowidx), N, E2, graph.e2_ptr, sh.NH,
-             None, ptr(G_aug), sh.ldg, sh.Dp, ptr(mws), s)
+             None, ptr(G_aug), ldg, sh.Dp, ptr(mws), s)
     g_x = g_W = g_a = g_bias = None
     W_aug = saved["W_aug"]
+    KC = sh.K_aug + C   # GEMM depth / rows over [g_Wh | g_s | g_skip]
     if need_bias and bias is not None:   # before g_pre may become g_x's accumulator
         g_bias = torch.empty_like(bias)
-        src = g_pre if elu else g_out
-        call("gatx_colsum", ptr(src), N, sh.out_cols, sh.out_cols, ptr(g_bias), s)
+        src_p, src_ld = (pre_p, pre_ld) if elu else (ptr(g_out), sh.out_cols)
+        call("gatx_colsum", src_p, N, sh.out_cols, src_ld, ptr(g_bias), s)
     fold = resid_is_x and need_x and g_pre is not None
     if need_x:
         g_x = g_pre if fold else torch.empty((N, sh.F_in), **f32)
         # W_aug^T (F_in x K_aug, 4 MB at PPI): both GEMM operands k-contiguous (the n-contiguous
         # B staging of W_aug as stored ran this product ~25% slower)
-        W_augT = torch.empty((sh.F_in, sh.ldg), **f32)
-        call("gatx_transpose_f32", sh.K_aug, sh.F_in, ptr(W_aug), sh.F_in, ptr(W_augT), sh.ldg, s)
-        call("gatx_gemm_f32", N, sh.F_in, sh.K_aug, ptr(G_aug), sh.ldg, 1, ptr(W_augT), 1,
-             sh.ldg, ptr(g_x), sh.F_in, sh.F_in, None, 0, int(fold),
-             *gemm_workspace(N, sh.F_in, sh.K_aug, dev), s)
-    if need_W or need_a:
-        gW_aug = torch.empty((sh.K_aug, sh.F_in), **f32)
-        ws_bytes = lib.gatx_gemm_splitk_workspace_bytes(sh.K_aug, sh.F_in, N)
+        W_augT = torch.empty((sh.F_in, ldg), **f32)
+        call("gatx_transpose_f32", KC, sh.F_in, ptr(W_aug), sh.F_in, ptr(W_augT), ldg, s)
+        call("gatx_gemm_f32", N, sh.F_in, KC, ptr(G_aug), ldg, 1, ptr(W_augT), 1,
+             ldg, ptr(g_x), sh.F_in, sh.F_in, None, 0, int(fold),
+             *gemm_workspace(N, sh.F_in, KC, dev), s)
+    if need_W or need_a or need_skip:
+        gW_aug = torch.empty((KC, sh.F_in), **f32)
+        ws_bytes = lib.gatx_gemm_splitk_workspace_bytes(KC, sh.F_in, N)
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-        call("gatx_gemm_f32_splitk", sh.K_aug, sh.F_in, N, ptr(G_aug), 1, sh.ldg, ptr(x),
+        call("gatx_gemm_f32_splitk", KC, sh.F_in, N, ptr(G_aug), 1, ldg, ptr(x),
              sh.F_in, 1, ptr(gW_aug), sh.F_in, 0, ptr(ws), ws_bytes, s)
         g_W = torch.empty_like(W)
         g_a = torch.empty_like(a) if a is not None else None
         call("gatx_weight_grads", ptr(gW_aug), ptr(W), ptr(a), sh.NH, sh.F, sh.F_in, ptr(g_W),
              ptr(g_a), s)
+        if need_skip:
+            saved["g_skip_eff"] = gW_aug[sh.K_aug:]
     g_resid = None
     if need_resid and not fold:
         g_resid = g_pre
@@ -460,7 +497,7 @@ def layer_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShape, 
 
 
 def _reassoc_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShape, p, seed,
-                      saved, need_W, need_a, need_bias, out, elu, need_resid):
+                      saved, need_W, need_a, need_bias, out, elu, need_resid, need_skip=False):
     """Backward of the reassociated first layer when its input needs no gradient (the model
     input): never forms Wh or its (N, NH*F) gradient.
       g_Z[n,h] = go[n,h] . W_h                      batched GEMM (g_Z[n,h] . x_src == g_alpha)
@@ -478,73 +515,97 @@ def _reassoc_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShap
     Fin_p = _round4(F_in)
     Z, x_rows = saved["Z"], saved["x_rows"]
     go = torch.empty((N, sh.Dp), **f32)
-    g_pre = torch.empty((N, sh.out_cols), **f32) if (need_resid or (need_bias and elu)) else None
-    call("gatx_prepare_go", ptr(g_out), ptr(out) if elu else None, N, NH, F, 1, int(elu),
-         ptr(go), ptr(g_pre), s)
+    C = sh.skip_cols
+    # [g_s_src | g_s_dst | g_skip]: a folded skip's gradient in G_s's last columns, so the score
+    # rows' split-K GEMM also yields the skip weight's gradient
+    lds = _round4(2 * NH + C) if C else 2 * NH
+    G_s = torch.empty((N, lds), **f32)
+    g_pre, pre_ld, pre_p = None, sh.out_cols, None
+    if C:
+        pre_ld, pre_p = lds, ptr(G_s) + 4 * 2 * NH
+    elif need_resid or (need_bias and elu):
+        g_pre = torch.empty((N, sh.out_cols), **f32)
+        pre_p = ptr(g_pre)
+    call("gatx_prepare_go_ex", ptr(g_out), ptr(out) if elu else None, N, NH, F, 1, int(elu),
+         ptr(go), pre_p, pre_ld, s)
     Wp = padded_weight(W, Fin_p, sh.cache_weights)    # [NH*F][Fin_p], zero tail
     g_Z = torch.empty((N, NH * Fin_p), **f32)
     call("gatx_gemm_f32_batched", NH, N, Fin_p, F, ptr(go), sh.Dp, 1, Fp, ptr(Wp), Fin_p, 1,
          F * Fin_p, ptr(g_Z), NH * Fin_p, Fin_p, 0, None, 0, None, 0, 0, 0, s)
-    G_s = torch.empty((N, 2 * NH), **f32)            # [g_s_src | g_s_dst]
     g_raw = torch.empty((NH, max(E2, 1)), **f32)
     gsd = torch.empty((N, NH), **f32)
     call("gatx_edge_backward_dst_ex", ptr(x_rows), Fin_p, 0, ptr(saved["S"]), ptr(saved["M_ord"]),
          ptr(saved["den"]), ptr(graph.rowptr), ptr(graph.col), ptr(graph.perm), N, E2, NH, Fin_p,
          ptr(g_Z), NH * Fin_p, Fin_p, float(p), ptr(seed),
          ptr(g_alpha.contiguous()) if g_alpha is not None else None, ptr(g_raw), ptr(gsd),
-         ptr(G_s), 2 * NH, 0, s)
+         ptr(G_s), lds, 0, s)
     call("gatx_edge_backward_src_scores", ptr(graph.srowptr), ptr(graph.seid), N, E2, NH,
-         ptr(g_raw), None, ptr(G_s), 2 * NH, 0, s)
+         ptr(g_raw), None, ptr(G_s), lds, 0, s)
     mws = torch.empty(lib.gatx_max_backward_workspace_bytes(), dtype=torch.uint8, device=dev)
     call("gatx_max_backward", ptr(saved["argmax"]), ptr(gsd), ptr(saved["S"]),
          ptr(saved["M_ord"]), ptr(graph.col), ptr(graph.rowidx), N, E2, graph.e2_ptr, NH, None,
-         ptr(G_s), 2 * NH, 0, ptr(mws), s)
+         ptr(G_s), lds, 0, ptr(mws), s)
     g_W = g_a = g_bias = None
-    if need_W or need_a:
-        gW_aug = torch.empty((sh.K_aug, F_in), **f32)
+    if need_W or need_a or need_skip:
+        gW_aug = torch.empty((sh.K_aug + C, F_in), **f32)
         # main rows, head h at rows h*Fp.. : go_h^T (F x N) . Z_h (N x F_in)
         wb = lib.gatx_gemm_splitk_batched_workspace_bytes(NH, F, F_in, N)
         ws = torch.empty(max(wb, 1), dtype=torch.uint8, device=dev)
         call("gatx_gemm_f32_splitk_batched", NH, F, F_in, N, ptr(go), 1, sh.Dp, Fp, ptr(Z),
              NH * Fin_p, 1, Fin_p, ptr(gW_aug), F_in, Fp * F_in, 0, ptr(ws), wb, s)
-        # score rows: G_s^T (2NH x N) . x (N x F_in)
-        wb2 = lib.gatx_gemm_splitk_workspace_bytes(2 * NH, F_in, N)
+        # score rows (+ folded skip rows): G_s^T (2NH + C x N) . x (N x F_in)
+        wb2 = lib.gatx_gemm_splitk_workspace_bytes(2 * NH + C, F_in, N)
         ws2 = torch.empty(max(wb2, 1), dtype=torch.uint8, device=dev)
-        call("gatx_gemm_f32_splitk", 2 * NH, F_in, N, ptr(G_s), 1, 2 * NH, ptr(x), F_in, 1,
+        call("gatx_gemm_f32_splitk", 2 * NH + C, F_in, N, ptr(G_s), 1, lds, ptr(x), F_in, 1,
              ptr(gW_aug) + 4 * sh.Dp * F_in, F_in, 0, ptr(ws2), wb2, s)
         g_W = torch.empty_like(W)
         g_a = torch.empty_like(a)
         call("gatx_weight_grads", ptr(gW_aug), ptr(W), ptr(a), NH, F, F_in, ptr(g_W), ptr(g_a), s)
+        if need_skip:
+            saved["g_skip_eff"] = gW_aug[sh.K_aug:]
     if need_bias and bias is not None:
         g_bias = torch.empty_like(bias)
-        src = g_pre if elu else g_out
-        call("gatx_colsum", ptr(src), N, sh.out_cols, sh.out_cols, ptr(g_bias), s)
+        src_p, src_ld = (pre_p, pre_ld) if elu else (ptr(g_out), sh.out_cols)
+        call("gatx_colsum", src_p, N, sh.out_cols, src_ld, ptr(g_bias), s)
     return (None, (g_W if need_W else None), (g_a if need_a else None), g_bias,
             g_pre if need_resid else None)
 
 
 class GATLayerFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, W, a, bias, resid, graph, sh, p, seed, elu):
-        out, alpha, saved = layer_forward(x, W, a, bias, graph, sh, p, seed, resid, elu)
+    def forward(ctx, x, W, a, bias, resid, skip_W, graph, sh, p, seed, elu):
+        out, alpha, saved = layer_forward(x, W, a, bias, graph, sh, p, seed, resid, elu, skip_W)
         ctx.graph, ctx.sh, ctx.p, ctx.seed, ctx.saved, ctx.elu = graph, sh, p, seed, saved, elu
         ctx.has_resid = resid is not None
         ctx.resid_is_x = resid is not None and resid is x
-        ctx.save_for_backward(x, W, a, bias, out if elu else None)
+        ctx.has_skip = skip_W is not None
+        ctx.save_for_backward(x, W, a, bias, out if elu else None, skip_W)
         return out, alpha
 
     @staticmethod
     def backward(ctx, g_out, g_alpha):
-        x, W, a, bias, out = ctx.saved_tensors
+        x, W, a, bias, out, skip_W = ctx.saved_tensors
         if g_out is None:
             g_out = torch.zeros((x.size(0), ctx.sh.out_cols), dtype=torch.float32,
                                 device=x.device)
-        nx, nW, na, nb, nr = ctx.needs_input_grad[:5]
+        nx, nW, na, nb, nr, ns = ctx.needs_input_grad[:6]
+        sh = ctx.sh
         g_x, g_W, g_a, g_b, g_r = layer_backward(
-            g_out, g_alpha, x, W, a, bias, ctx.graph, ctx.sh, ctx.p, ctx.seed, ctx.saved, nx, nW,
+            g_out, g_alpha, x, W, a, bias, ctx.graph, sh, ctx.p, ctx.seed, ctx.saved, nx, nW,
             na, nb, out=out, elu=ctx.elu, need_resid=bool(ctx.has_resid and nr),
-            resid_is_x=ctx.resid_is_x)
-        return g_x, g_W, g_a, g_b, g_r, None, None, None, None, None
+            resid_is_x=ctx.resid_is_x, need_skip=bool(ctx.has_skip and ns))
+        g_s = None
+        if ctx.has_skip and ns:
+            # gradient of W_skip_eff: W_skip's own for concat / one head; a head-mean layer's
+            # W_skip gets it in every head block, / NH
+            eff = ctx.saved.pop("g_skip_eff")
+            if sh.concat or sh.NH == 1:
+                g_s = eff
+            else:
+                g_s = torch.empty_like(skip_W)
+                call("gatx_skip_weight_grad", ptr(eff), sh.NH, sh.skip_cols, sh.F_in, ptr(g_s),
+                     stream())
+        return g_x, g_W, g_a, g_b, g_r, g_s, None, None, None, None, None
 
 
 class SkipProjectionFunction(torch.autograd.Function):
@@ -609,17 +670,18 @@ def device_seed(seed, dev) -> torch.Tensor:
 
 def gat_layer(x, edge_index, W, a, bias, num_heads, out_features, concat, add_self_loops,
               const_attention=False, dropout_p=0.0, seed=0, graph: Graph | None = None,
-              resid=None, elu=False):
+              resid=None, elu=False, skip_weight=None):
     """Functional form of GATLayer.forward: returns (out, edge_index', alpha), the last two at
     their exact size (reads |edge_index'| from the device: one sync per new graph)."""
     out, graph, alpha = gat_layer_lazy(x, edge_index, W, a, bias, num_heads, out_features, concat,
                                        add_self_loops, const_attention, dropout_p, seed, graph,
-                                       resid, elu)
+                                       resid, elu, skip_weight)
     return out, graph.edge_index, alpha[:graph.num_edges]
 
 
 def prepare_layer(x, edge_index, W, a, bias, num_heads, out_features, concat, add_self_loops,
-                  const_attention=False, graph: Graph | None = None, resid=None):
+                  const_attention=False, graph: Graph | None = None, resid=None,
+                  skip_weight=None):
     """Argument checks of GATLayer.forward (the reference's own errors) and the layer's Graph:
     returns (x, W, a, resid, LayerShape, Graph) with contiguous tensors."""
     from .graph import graph_cache
@@ -635,7 +697,15 @@ def prepare_layer(x, edge_index, W, a, bias, num_heads, out_features, concat, ad
     W = W.contiguous()
     a = a.contiguous() if a is not None else None
     sh = LayerShape(num_heads, out_features, x.size(1), concat, const_attention)
-    sh.cache_weights = _cacheable(W, a)
+    sh.cache_weights = _cacheable(W, a, skip_weight)
+    if skip_weight is not None:
+        _require(skip_weight, "skip_weight")
+        if resid is not None:
+            raise RuntimeError("gatx: resid and skip_weight are exclusive")
+        if tuple(skip_weight.shape) != (num_heads * out_features, x.size(1)):
+            raise RuntimeError(f"skip weight shape {tuple(skip_weight.shape)} does not match "
+                               f"({num_heads * out_features}, {x.size(1)})")
+        sh.skip_cols = sh.out_cols
     if W.shape != (num_heads * out_features, x.size(1)):
         raise RuntimeError(f"W.weight shape {tuple(W.shape)} does not match "
                            f"({num_heads * out_features}, {x.size(1)})")
@@ -659,17 +729,22 @@ def prepare_layer(x, edge_index, W, a, bias, num_heads, out_features, concat, ad
 
 def gat_layer_lazy(x, edge_index, W, a, bias, num_heads, out_features, concat, add_self_loops,
                    const_attention=False, dropout_p=0.0, seed=0, graph: Graph | None = None,
-                   resid=None, elu=False):
+                   resid=None, elu=False, skip_weight=None):
     """gat_layer without any host sync: returns (out, graph, alpha_bound) where alpha_bound is
     (graph.edge_bound, NH) and its first graph.num_edges rows are alpha in edge_index' order.
     resid / elu fuse GATModel's skip-add and ELU into the layer's epilogue:
-    out = elu?(layer(x) + resid)."""
+    out = elu?(layer(x) + resid). skip_weight (GATModel's Linear skip, (NH*F, F_in)) folds the
+    skip projection itself into the layer: resid = x W_skip^T (concat) or its head mean, computed
+    by the layer's own projection GEMM."""
     x, W, a, resid, sh, graph = prepare_layer(x, edge_index, W, a, bias, num_heads, out_features,
                                               concat, add_self_loops, const_attention, graph,
-                                              resid)
+                                              resid, skip_weight)
+    if skip_weight is not None:
+        skip_weight = skip_weight.contiguous()
     p = float(dropout_p)
     seed_t = device_seed(seed, x.device) if p > 0 else None
-    out, alpha = GATLayerFunction.apply(x, W, a, bias, resid, graph, sh, p, seed_t, bool(elu))
+    out, alpha = GATLayerFunction.apply(x, W, a, bias, resid, skip_weight, graph, sh, p, seed_t,
+                                        bool(elu))
     return out, graph, alpha
 
 

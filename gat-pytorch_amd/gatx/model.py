@@ -25,6 +25,12 @@ from .layer import GATLayer
 SKIP_GEMM_MIN_MACS = 1 << 26
 
 
+def _skip_fold_enabled() -> bool:
+    """GATX_SKIP_FOLD=0 turns the folded skip projection off (A/B tests and measurements)."""
+    from .functional import _env_int
+    return _env_int("GATX_SKIP_FOLD", 1) != 0
+
+
 class GATModel(nn.Module):
     def __init__(self, num_classes: int, num_input_node_features: int, num_layers: int,
                  num_heads_per_layer: List[int], heads_concat_per_layer: List[bool],
@@ -80,13 +86,21 @@ class GATModel(nn.Module):
         for i in range(L):
             layer_input = x
             x = F.dropout(x, p=self.dropout, training=self.training)
-            resid = None
+            resid = skip_w = None
             if self.add_skip_connection[i]:
-                resid = self._resid(i, skip_count, layer_input)
+                skip = self.skip_layer_list[skip_count]
+                if (isinstance(skip, nn.Linear) and (self.dropout == 0 or not self.training)
+                        and not torch.compiler.is_compiling() and _skip_fold_enabled()):
+                    # the skip reads the layer's own input (no input dropout in effect): its
+                    # projection is folded into the layer's projection GEMM (one launch)
+                    skip_w = skip.weight
+                else:
+                    resid = self._resid(i, skip_count, layer_input)
                 skip_count += 1
             # layer -> (+ skip) -> ELU except after the last layer, fused in the layer epilogue
+            extra = {"skip_weight": skip_w} if skip_w is not None else {}
             out = self.gat_layer_list[i](x, edge_index, return_attention_weights=with_attention,
-                                         resid=resid, elu=(i != L - 1))
+                                         resid=resid, elu=(i != L - 1), **extra)
             if with_attention:
                 x, (edge_index, att) = out
                 attention_weights_list.append(att)

@@ -90,6 +90,17 @@ int gatx_prepare_weights(const float* W, const float* a, int NH, int F, int64_t 
                          float* W_aug, gatx_stream_t stream);
 /* Floats the W_aug buffer must hold: (Dp + 2NH) * F_in plus split-K scratch behind it. */
 int64_t gatx_prepare_weights_floats(int NH, int F, int64_t F_in, int has_a);
+/* gatx_prepare_weights with GATModel's Linear skip folded in (models/GATModel.py:107-110,
+ * applied at :136-145 to the same layer input as W): skip_cols rows W_skip_eff follow the
+ * Dp + 2NH rows, W_skip_eff[c][i] = mean_h W_skip[h*skip_cols + c][i] over skip_heads row blocks
+ * (skip_heads = NH for a head-mean layer: mean_h(x W_h^T) == x (mean_h W_h)^T, :143-145; 1 for
+ * concat: a copy, :140-141), written by the same launch. Buffer:
+ * gatx_prepare_weights_skip_floats(). W_skip == NULL: gatx_prepare_weights. */
+int gatx_prepare_weights_skip(const float* W, const float* a, int NH, int F, int64_t F_in,
+                              const float* W_skip, int skip_heads, int64_t skip_cols,
+                              float* W_aug, gatx_stream_t stream);
+int64_t gatx_prepare_weights_skip_floats(int NH, int F, int64_t F_in, int has_a,
+                                         int64_t skip_cols);
 
 /* fp32 GEMM on MFMA (v_mfma_f32_32x32x2_f32): C = A * B (+ C if accumulate).
  * A(m,k) = A[m*sam + k*sak], B(k,n) = B[k*sbk + n*sbn]; one of sam/sak and one of sbk/sbn must
@@ -140,6 +151,19 @@ int gatx_projection_gemm(int64_t M, int64_t N, int64_t K, const float* A, int64_
                          int64_t sak, const float* B, int64_t sbk, int64_t sbn, float* C0,
                          int64_t ldc0, int64_t n_split, float* C1, int64_t ldc1,
                          void* workspace, size_t workspace_bytes, gatx_stream_t stream);
+/* The projection with GATModel's Linear skip folded in (models/GATModel.py:107-110 applied at
+ * :136-145; the skip reads the same layer input as W, gat_layer.py:64): B = [W_aug; W_skip_eff],
+ * columns n < n_split -> C0 (Wh), n_split <= n < n_split2 -> C1 (S), n >= n_split2 -> C2[m*ldc2 +
+ * n - n_split2] (the skip output, added by the edge pass epilogue). One launch instead of the
+ * projection plus a separate skip GEMM. */
+int gatx_projection_gemm3(int64_t M, int64_t N, int64_t K, const float* A, int64_t sam,
+                          int64_t sak, const float* B, int64_t sbk, int64_t sbn, float* C0,
+                          int64_t ldc0, int64_t n_split, float* C1, int64_t ldc1,
+                          int64_t n_split2, float* C2, int64_t ldc2, void* workspace,
+                          size_t workspace_bytes, gatx_stream_t stream);
+/* Its gradient: g_W_skip[h*cols + c][i] = g_eff[c][i] / heads for every head block h. */
+int gatx_skip_weight_grad(const float* g_eff, int heads, int64_t cols, int64_t F_in, float* g_W,
+                          gatx_stream_t stream);
 
 /* The same for `batch` independent products (batch b offsets A, B, C by b*a_bs, b*b_bs,
  * b*c_bs floats) with a fused epilogue C = elu?(A*B (+C) + bias[b*bias_bs + n] +
@@ -269,6 +293,11 @@ int gatx_pad_rows(const float* src, int64_t rows, int64_t cols, int64_t ld_src, 
  * per head. g_pre (nullable) receives the unpadded elu-gated gradient (the residual's gradient). */
 int gatx_prepare_go(const float* g_out, const float* out, int64_t num_nodes, int NH, int F,
                     int concat, int elu, float* go, float* g_pre, gatx_stream_t stream);
+/* The same with g_pre rows pre_ld floats apart (>= the output width): the folded skip's
+ * gradient written straight into its columns of G_aug (gatx_prepare_weights_skip). */
+int gatx_prepare_go_ex(const float* g_out, const float* out, int64_t num_nodes, int NH, int F,
+                       int concat, int elu, float* go, float* g_pre, int64_t pre_ld,
+                       gatx_stream_t stream);
 
 /* Destination pass, one wave per (node n, head h):
  *   g_alpha~[e,h] = <go[n,h,:], Wh[src,h,:]>; g_alpha = g_alpha~ * keep/(1-p) + g_alpha_ret

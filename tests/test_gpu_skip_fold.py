@@ -1,0 +1,126 @@
+"""GATModel's Linear skip folded into the layer's projection GEMM (GATLayer(..., skip_weight=W_s):
+W_s's rows appended to W_aug, the skip output written as the GEMM's third output range and added
+by the edge-pass / output-projection epilogue) against the fp64 oracle: the layer plus
+`x W_s^T` (concat) or its head mean (`models/GATModel.py:136-145`), ELU, and the gradients of x,
+W, a and W_s. Covers both first-layer dataflows (reassociated: the skip rides on the score GEMM;
+direct: gatx_projection_gemm3), head mean, const attention and an input without gradient.
+Model level: a PATTERN-shaped GATModel (every layer a Linear skip) with the fold matches the
+oracle's model forward/backward and the unfolded path (GATX_SKIP_FOLD=0)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import gat_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+OUT_TOL = 1e-4
+GRAD_TOL = 1e-4
+
+
+def _skip_ref(x, Ws, NH, F, concat):
+    so = x @ Ws.T
+    return so if concat else so.reshape(-1, NH, F).mean(axis=1)
+
+
+@pytest.mark.parametrize("fin,NH,F,concat,const,elu,need_x", [
+    (3, 4, 12, True, False, True, False),     # PATTERN L0: reassociated, input without grad
+    (48, 4, 24, True, False, True, True),     # PATTERN L1: reassociated, general backward
+    (96, 4, 12, True, False, True, True),     # PATTERN L2: direct projection (gemm3)
+    (48, 1, 1, False, False, False, True),    # PATTERN L3: one-head mean, no ELU
+    (32, 4, 16, False, False, True, True),    # head mean over 4 heads
+    (64, 6, 37, False, False, False, True),   # head mean, F % 4 != 0
+    (96, 4, 12, True, True, True, True),      # const attention, direct
+    (5, 4, 12, True, True, False, False),     # const attention, reassociated
+])
+def test_folded_skip_layer_vs_oracle(fin, NH, F, concat, const, elu, need_x, device):
+    import gatx
+    from gatx import data as gd
+    b = gd.uniform_graph_batch(3, 150, 1800, fin, feature_seed=31 + fin)
+    W = gd.xavier_uniform(32 + NH, NH * F, fin)
+    a = gd.xavier_uniform(33 + NH, NH, NH * 2 * F)
+    Ws = gd.xavier_uniform(34 + F, NH * F, fin)
+    layer = gatx.GATLayer(fin, F, NH, concat, add_self_loops=True,
+                          const_attention=const).to(device)
+    with torch.no_grad():
+        layer.W.weight.copy_(torch.from_numpy(W))
+        if not const:
+            layer.a.weight.copy_(torch.from_numpy(a))
+    x = torch.from_numpy(b.x).to(device).requires_grad_(need_x)
+    ws = torch.from_numpy(Ws).to(device).requires_grad_(True)
+    ei = torch.from_numpy(b.edge_index).to(device)
+    out = layer(x, ei, skip_weight=ws, elu=elu)
+    g = gd.normal(35, out.numel()).reshape(tuple(out.shape))
+    (out * torch.from_numpy(g).to(device)).sum().backward()
+    torch.cuda.synchronize()
+
+    xd = b.x.astype(np.float64)
+    o, _, _, cache = orc.gat_layer_forward(xd, b.edge_index, W, a, NH, F, concat,
+                                           const_attention=const, dtype=np.float64)
+    pre = o + _skip_ref(xd, Ws.astype(np.float64), NH, F, concat)
+    post = orc.elu(pre) if elu else pre
+    assert np.abs(out.detach().cpu().numpy() - post).max() <= OUT_TOL
+    g_pre = g * np.where(pre > 0, 1.0, np.exp(np.minimum(pre, 0))) if elu else g.astype(np.float64)
+    gr = orc.gat_layer_backward(cache, g_pre)
+    g_so = g_pre if concat else np.repeat(g_pre[:, None, :] / NH, NH, axis=1).reshape(len(xd), -1)
+    refs = [("W", layer.W.weight.grad, gr["W"]), ("skip", ws.grad, g_so.T @ xd)]
+    if not const:
+        refs.append(("a", layer.a.weight.grad, gr["a"]))
+    if need_x:
+        refs.append(("x", x.grad, gr["x"] + g_so @ Ws.astype(np.float64)))
+    else:
+        assert x.grad is None
+    for k, t, ref in refs:
+        err = np.abs(t.cpu().numpy() - ref).max()
+        assert err <= GRAD_TOL * max(1.0, np.abs(ref).max()), (k, err)
+
+
+def _pattern_model(device, seed):
+    import gatx
+    from gatx.config import data_config
+    torch.manual_seed(seed)
+    return gatx.GATModel(**data_config["PATTERN"]).to(device)
+
+
+def test_folded_skip_pattern_model(device, monkeypatch):
+    """PATTERN 4-layer model (Linear skips on every layer, 3 -> 48 -> 96 -> 48 -> 1): folded
+    forward and gradients vs the fp64 oracle, and vs the unfolded path within fp32 noise."""
+    from gatx import data as gd
+    from gatx.config import data_config
+    cfg = data_config["PATTERN"]
+    b = gd.uniform_graph_batch(4, 120, 1400, cfg["num_input_node_features"], feature_seed=41)
+    ei = torch.from_numpy(b.edge_index).to(device)
+    results = {}
+    for fold in ("1", "0"):
+        monkeypatch.setenv("GATX_SKIP_FOLD", fold)
+        from gatx import functional
+        functional.reset_tuning()
+        model = _pattern_model(device, 5)
+        x = torch.from_numpy(b.x).to(device)
+        out = model(x, ei)
+        g = torch.from_numpy(gd.normal(42, out.numel()).reshape(tuple(out.shape))).to(device)
+        (out * g).sum().backward()
+        torch.cuda.synchronize()
+        results[fold] = (out.detach().cpu().numpy(),
+                         {n: p.grad.detach().cpu().numpy() for n, p in model.named_parameters()},
+                         model, g.cpu().numpy())
+    out1, gr1, model, g = results["1"]
+    out0, gr0, _, _ = results["0"]
+    for n in gr1:
+        assert np.abs(gr1[n] - gr0[n]).max() <= 1e-4 * max(1.0, np.abs(gr0[n]).max()), n
+    assert np.abs(out1 - out0).max() <= 1e-4
+    L = cfg["num_layers"]
+    layers = [(model.gat_layer_list[i].W.weight.detach().cpu().numpy(),
+               model.gat_layer_list[i].a.weight.detach().cpu().numpy()) for i in range(L)]
+    skips = [s.weight.detach().cpu().numpy() for s in model.skip_layer_list]
+    ref_out, ref = orc.gat_model_forward_backward(
+        b.x, b.edge_index, layers, skips, cfg["num_heads_per_layer"],
+        cfg["head_output_features_per_layer"][1:], cfg["heads_concat_per_layer"],
+        cfg["add_skip_connection"], g)
+    scale = max(1.0, np.abs(ref_out).max())
+    assert np.abs(out1 - ref_out).max() <= OUT_TOL * scale
+    for i in range(L):
+        for k, name in (("W", f"gat_layer_list.{i}.W.weight"), ("a", f"gat_layer_list.{i}.a.weight"),
+                        ("skip", f"skip_layer_list.{i}.weight")):
+            r = ref[k][i]
+            assert np.abs(gr1[name] - r).max() <= GRAD_TOL * max(1.0, np.abs(r).max()), name
