@@ -54,9 +54,14 @@ __global__ void __launch_bounds__(256) prepare_go_kernel(const float* __restrict
                                                          int concat, int elu,
                                                          float* __restrict__ go,
                                                          float* __restrict__ g_pre,
-                                                         int64_t pre_ld) {
+                                                         int64_t pre_ld, float out_p,
+                                                         const uint64_t* __restrict__ out_seed) {
   const int OC = concat ? NH * F : F, GW = concat ? NH * Fp : Fp;
   const float scale = concat ? 1.f : 1.f / (float)NH;
+  // the next layer's input dropout fused into this layer's epilogue: out holds the dropped
+  // output, g_out its gradient — take the mask's gradient, and ELU's from out * (1 - p)
+  const uint64_t osd = out_p > 0.f ? *out_seed : 0ull;
+  const float oscale = out_p > 0.f ? 1.f / (1.f - out_p) : 1.f;
   const int64_t total = N * GW;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
@@ -66,8 +71,9 @@ __global__ void __launch_bounds__(256) prepare_go_kernel(const float* __restrict
     if (f < F) {
       const int64_t src = n * OC + (concat ? h * F + f : f);
       v = g_out[src];
+      if (out_p > 0.f) v = dropout_keep(osd, src, out_p) ? v * oscale : 0.f;
       if (elu) {
-        const float o = out[src];
+        const float o = out_p > 0.f ? out[src] * (1.f - out_p) : out[src];
         v = o > 0.f ? v : v * (o + 1.f);   // d elu(x) = elu(x) + 1 for x <= 0
       }
       if (g_pre) g_pre[n * pre_ld + (concat ? h * F + f : f)] = v;
@@ -719,7 +725,10 @@ using namespace gatx;
 
 extern "C" int gatx_prepare_go_ex(const float* g_out, const float* out, int64_t N, int NH,
                                   int F, int concat, int elu, float* go, float* g_pre,
-                                  int64_t pre_ld, gatx_stream_t s) {
+                                  int64_t pre_ld, float out_p, const uint64_t* out_seed,
+                                  gatx_stream_t s) {
+  GATX_REQUIRE(out_p >= 0.f && out_p < 1.f && (out_p == 0.f || out_seed),
+               "prepare_go: output dropout needs p in [0, 1) and its device seed");
   if (N == 0) return 0;
   const int64_t OC = concat ? (int64_t)NH * F : F;
   GATX_REQUIRE(pre_ld >= OC, "prepare_go: g_pre row stride below the output width");
@@ -730,7 +739,7 @@ extern "C" int gatx_prepare_go_ex(const float* g_out, const float* out, int64_t 
                "prepare_go: g_pre may alias go only for concat layers with F % 4 == 0");
   const bool aligned = ((uintptr_t)g_out % 16 == 0) && ((uintptr_t)go % 16 == 0) &&
                        (!elu || (uintptr_t)out % 16 == 0) && ((uintptr_t)g_pre % 16 == 0);
-  if (F % 4 == 0 && aligned && pre_ld == OC) {
+  if (F % 4 == 0 && aligned && pre_ld == OC && out_p == 0.f) {
     const int64_t n4 = N * GW / 4;
     prepare_go_vec_kernel<<<grid_for(ceil_div(n4, 4), 256, 8192), 256, 0, (hipStream_t)s>>>(
         (const float4*)g_out, (const float4*)out, n4, elu, concat ? 1.f : 1.f / (float)NH,
@@ -740,7 +749,7 @@ extern "C" int gatx_prepare_go_ex(const float* g_out, const float* out, int64_t 
   }
   prepare_go_kernel<<<grid_for(N * GW), 256, 0, (hipStream_t)s>>>(g_out, out, N, NH, F, Fp,
                                                                   concat, elu, go, g_pre,
-                                                                  pre_ld);
+                                                                  pre_ld, out_p, out_seed);
   GATX_LAUNCH_CHECK("prepare_go");
   return 0;
 }
@@ -748,7 +757,7 @@ extern "C" int gatx_prepare_go_ex(const float* g_out, const float* out, int64_t 
 extern "C" int gatx_prepare_go(const float* g_out, const float* out, int64_t N, int NH, int F,
                                int concat, int elu, float* go, float* g_pre, gatx_stream_t s) {
   return gatx_prepare_go_ex(g_out, out, N, NH, F, concat, elu, go, g_pre,
-                            concat ? (int64_t)NH * F : F, s);
+                            concat ? (int64_t)NH * F : F, 0.f, nullptr, s);
 }
 
 extern "C" int gatx_edge_backward_dst_ex(const float* rows, int64_t row_stride,

@@ -135,6 +135,11 @@ struct EdgeFwdArgs {
   const float* resid;      // fused epilogue: out = elu?(agg + bias + resid)
   int64_t resid_ld;
   int elu;
+  // the next layer's input dropout fused after the ELU (models/GATModel.py:130 applied to this
+  // output): out = keep(out_seed, n * out_cols + col) ? v / (1 - out_p) : 0
+  float out_p;
+  const uint64_t* out_seed;
+  int64_t out_cols;
   float* den;
   int lds_row;
   int64_t chunk;           // destination nodes per (chunk, head-group) sweep
@@ -168,9 +173,15 @@ __device__ inline int64_t xcd_contiguous(int64_t b, int64_t nb) {
   return (xcd < r) ? xcd * (q + 1) + j : r * (q + 1) + (xcd - r) * q + j;
 }
 
+__device__ inline float out_dropout(float v, const EdgeFwdArgs& g, int64_t n, int64_t col) {
+  return dropout_keep(*g.out_seed, n * g.out_cols + col, g.out_p) ? v * (1.f / (1.f - g.out_p))
+                                                                   : 0.f;
+}
+
 __device__ inline float epilogue(float v, const EdgeFwdArgs& g, int64_t n, int64_t col) {
   if (g.resid) v += g.resid[n * g.resid_ld + col];
   if (g.elu) v = elu_act(v);
+  if (g.out_p > 0.f) v = out_dropout(v, g, n, col);
   return v;
 }
 
@@ -213,6 +224,12 @@ __device__ inline void finish_item(const EdgeFwdArgs& g, int64_t n, int h0, int 
             r.y = elu_act(r.y);
             r.z = elu_act(r.z);
             r.w = elu_act(r.w);
+          }
+          if (g.out_p > 0.f) {
+            r.x = out_dropout(r.x, g, n, cb);
+            r.y = out_dropout(r.y, g, n, cb + 1);
+            r.z = out_dropout(r.z, g, n, cb + 2);
+            r.w = out_dropout(r.w, g, n, cb + 3);
           }
           const f4v ov = {r.x, r.y, r.z, r.w};
           __builtin_nontemporal_store(ov, (f4v*)(orow + cb));
@@ -1090,15 +1107,21 @@ extern "C" size_t gatx_edge_forward_hub_part_bytes(int64_t hub_bound, int NH, in
   return (size_t)hub_bound * (group_count > 0 ? group_count : NH / HS) * W * sizeof(float);
 }
 
-extern "C" int gatx_edge_forward_hubs(
+extern "C" int gatx_edge_forward_drop(
     const float* rows, int64_t row_stride, int64_t head_stride, const float* S,
     const uint32_t* M_ord, const int32_t* rowptr, const int32_t* col, const int32_t* perm,
     int64_t N, int NH, int F, int heads_per_item, int group_begin, int group_count,
     int mean_mode, int concat, int const_att, const float* bias,
     float p, const uint64_t* seed, float* out, int64_t out_ld, const float* resid, int64_t resid_ld,
     int elu, float* den, int64_t chunk, int hub_edges, const int32_t* hubs,
-    const int32_t* hub_count, int64_t hub_bound, float* hub_part, gatx_stream_t s) {
+    const int32_t* hub_count, int64_t hub_bound, float* hub_part, float out_p,
+    const uint64_t* out_seed, gatx_stream_t s) {
   hipStream_t st = (hipStream_t)s;
+  GATX_REQUIRE(out_p >= 0.f && out_p < 1.f, "edge_forward: output dropout must be in [0, 1)");
+  GATX_REQUIRE(out_p == 0.f || out_seed != nullptr,
+               "edge_forward: output dropout needs its device seed");
+  GATX_REQUIRE(out_p == 0.f || mean_mode == 0 || mean_mode == 3,
+               "edge_forward: output dropout belongs to the last head-mean pass");
   GATX_REQUIRE(NH >= 1 && F >= 1, "edge_forward: bad sizes");
   GATX_REQUIRE(concat || bias == nullptr || NH == 1,
                "edge_forward: bias with head-mean needs num_heads == 1");
@@ -1130,6 +1153,7 @@ extern "C" int gatx_edge_forward_hubs(
   g.N = N; g.NH = NH; g.F = F; g.Fp = Fp; g.HS = HS; g.concat = concat; g.const_att = const_att;
   g.bias = bias; g.p_drop = p; g.seed = seed; g.out = out; g.out_ld = out_ld;
   g.resid = resid; g.resid_ld = resid_ld; g.elu = elu;
+  g.out_p = out_p; g.out_seed = out_seed; g.out_cols = concat ? (int64_t)NH * F : F;
   g.den = den;
   g.vec_out = concat && (F & 3) == 0 && out_ld % 4 == 0 && ((uintptr_t)out % 16) == 0 &&
               (!resid || (resid_ld % 4 == 0 && ((uintptr_t)resid % 16) == 0)) &&
@@ -1181,4 +1205,46 @@ extern "C" int gatx_edge_forward(const float* Wh, const float* S, const uint32_t
                                  concat ? (int64_t)NH * F : F, nullptr, 0, 0, den, 0, s));
   return gatx_attention_alpha(col, rowidx, perm, E2, S, M_ord, den, NH, const_att,
                               alpha, argmax, s);
+}
+
+extern "C" int gatx_edge_forward_hubs(
+    const float* rows, int64_t row_stride, int64_t head_stride, const float* S,
+    const uint32_t* M_ord, const int32_t* rowptr, const int32_t* col, const int32_t* perm,
+    int64_t N, int NH, int F, int heads_per_item, int group_begin, int group_count,
+    int mean_mode, int concat, int const_att, const float* bias,
+    float p, const uint64_t* seed, float* out, int64_t out_ld, const float* resid, int64_t resid_ld,
+    int elu, float* den, int64_t chunk, int hub_edges, const int32_t* hubs,
+    const int32_t* hub_count, int64_t hub_bound, float* hub_part, gatx_stream_t s) {
+  return gatx_edge_forward_drop(rows, row_stride, head_stride, S, M_ord, rowptr, col, perm, N, NH,
+                                F, heads_per_item, group_begin, group_count, mean_mode, concat,
+                                const_att, bias, p, seed, out, out_ld, resid, resid_ld, elu, den,
+                                chunk, hub_edges, hubs, hub_count, hub_bound, hub_part, 0.f,
+                                nullptr, s);
+}
+
+namespace gatx {
+namespace {
+// GATModel's input dropout (models/GATModel.py:130) as a counter-based mask on the element
+// index, the same hash as the attention dropout and the fused epilogue's: y = keep ? x / (1 - p)
+// : 0. Its own backward (the gradient takes the same mask and scale).
+__global__ void __launch_bounds__(256) dropout_kernel(const float* __restrict__ x, int64_t n,
+                                                      float p, const uint64_t* __restrict__ seed,
+                                                      float* __restrict__ y) {
+  const uint64_t sd = *seed;
+  const float scale = 1.f / (1.f - p);
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n;
+       t += (int64_t)gridDim.x * blockDim.x)
+    y[t] = dropout_keep(sd, t, p) ? x[t] * scale : 0.f;
+}
+}  // namespace
+}  // namespace gatx
+
+extern "C" int gatx_dropout(const float* x, int64_t n, float p, const uint64_t* seed, float* y,
+                            gatx_stream_t s) {
+  GATX_REQUIRE(n >= 0 && p >= 0.f && p < 1.f, "dropout: bad arguments");
+  GATX_REQUIRE(seed != nullptr, "dropout: needs the device seed");
+  if (n == 0) return 0;
+  dropout_kernel<<<grid_for(n), 256, 0, (hipStream_t)s>>>(x, n, p, seed, y);
+  GATX_LAUNCH_CHECK("dropout");
+  return 0;
 }

@@ -50,6 +50,9 @@ SIGNATURES = {
     "gatx_edge_forward_hubs": (c_i, [P, c_i64, c_i64, P, P, P, P, P, c_i64, c_i, c_i, c_i, c_i,
                                      c_i, c_i, c_i, c_i, P, c_f, P, P, c_i64, P, c_i64, c_i, P,
                                      c_i64, c_i, P, P, c_i64, P, P]),
+    "gatx_edge_forward_drop": (c_i, [P, c_i64, c_i64, P, P, P, P, P, c_i64, c_i, c_i, c_i, c_i,
+                                     c_i, c_i, c_i, c_i, P, c_f, P, P, c_i64, P, c_i64, c_i, P,
+                                     c_i64, c_i, P, P, c_i64, P, c_f, P, P]),
     "gatx_edge_forward_hub_part_bytes": (c_sz, [c_i64, c_i, c_i, c_i, c_i]),
     "gatx_graph_hub_bound": (c_i64, [c_i64, c_i]),
     "gatx_graph_hub_plan": (c_i, [P, c_i64, c_i, P, c_i64, P, P]),
@@ -60,7 +63,8 @@ SIGNATURES = {
                                     c_i64, c_i64, P, c_i64, c_i64, P, c_i64, P, c_sz, P]),
     "gatx_prepare_weights_skip": (c_i, [P, P, c_i, c_i, c_i64, P, c_i, c_i64, P, P]),
     "gatx_prepare_weights_skip_floats": (c_i64, [c_i, c_i, c_i64, c_i, c_i64]),
-    "gatx_prepare_go_ex": (c_i, [P, P, c_i64, c_i, c_i, c_i, c_i, P, P, c_i64, P]),
+    "gatx_prepare_go_ex": (c_i, [P, P, c_i64, c_i, c_i, c_i, c_i, P, P, c_i64, c_f, P, P]),
+    "gatx_dropout": (c_i, [P, c_i64, c_f, P, P, P]),
     "gatx_skip_weight_grad": (c_i, [P, c_i, c_i64, c_i64, P, P]),
     "gatx_set_debug": (None, [c_i]),
     "gatx_set_gemm_mode": (None, [c_i]),

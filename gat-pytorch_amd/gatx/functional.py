@@ -291,12 +291,22 @@ def reassoc_heads_per_item(sh: LayerShape) -> int:
     return max(fits) if fits else 0
 
 
+def fuses_output_dropout(num_heads, out_features, in_features, concat, const_attention=False):
+    """Whether a layer of this shape can apply the NEXT layer's input dropout in its own epilogue
+    (gatx_edge_forward_drop): every layer whose output comes from the edge pass, i.e. all but
+    the reassociated first-layer dataflow (its output comes from the batched GEMM's epilogue)."""
+    return not use_reassociation(LayerShape(num_heads, out_features, in_features, concat,
+                                            const_attention))
+
+
 def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: int,
-                  resid=None, elu=False, skip_W=None):
+                  resid=None, elu=False, skip_W=None, out_p=0.0, out_seed=None):
     """Returns out (= elu?(layer(x) + resid) when fused), alpha (edge_index' order) and the saved
     state for the backward. skip_W: GATModel's Linear skip folded into the projection GEMM (its
     rows appended to W_aug; the GEMM writes the skip output R as a third output range and the
-    edge pass / output projection epilogue adds it): resid = x W_skip_eff^T without a launch."""
+    edge pass / output projection epilogue adds it): resid = x W_skip_eff^T without a launch.
+    out_p / out_seed: the next layer's input dropout applied by this layer's edge-pass epilogue
+    (fuses_output_dropout must hold); the returned out is then the dropped output."""
     N = x.size(0)
     dev = x.device
     s = stream()
@@ -315,8 +325,12 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
         resid = R
     resid_p = ptr(resid) if resid is not None else None
     W_aug = augmented_weight(W, a, sh, skip_W)
-    saved = dict(W_aug=W_aug, M_ord=M_ord, den=den, argmax=argmax, Wh=None)
+    saved = dict(W_aug=W_aug, M_ord=M_ord, den=den, argmax=argmax, Wh=None, out_p=float(out_p),
+                 out_seed=out_seed)
+    drop_args = (float(out_p), ptr(out_seed) if out_p > 0 else None)
     if use_reassociation(sh):
+        if out_p > 0:
+            raise RuntimeError("gatx: output dropout is not fused into a reassociated layer")
         Fin_p = _round4(sh.F_in)
         if Fin_p != sh.F_in:
             x_rows = torch.empty((N, Fin_p), **f32)
@@ -383,20 +397,22 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
         ng = sh.NH // hs
         if sh.concat or ng == 1:
             hub = hub_args(graph, sh, hs, ng, dev)
-            call("gatx_edge_forward_hubs", ptr(Wh), sh.Dp, sh.Fp, ptr(S), ptr(M_ord),
+            call("gatx_edge_forward_drop", ptr(Wh), sh.Dp, sh.Fp, ptr(S), ptr(M_ord),
                  ptr(graph.rowptr), ptr(graph.col), ptr(graph.perm), N, sh.NH, sh.F, hs,
                  0, 0, 0, int(sh.concat), int(sh.const), ptr(bias), float(p), ptr(seed),
-                 ptr(out), sh.out_cols, resid_p, sh.out_cols, int(elu), ptr(den), chunk, *hub, s)
+                 ptr(out), sh.out_cols, resid_p, sh.out_cols, int(elu), ptr(den), chunk, *hub,
+                 *drop_args, s)
         else:   # head mean over groups: one launch per group, accumulated in stream order
             hub = hub_args(graph, sh, hs, 1, dev)
             for gi in range(ng):
                 last = gi == ng - 1
                 mode = 1 if gi == 0 else (3 if last else 2)
-                call("gatx_edge_forward_hubs", ptr(Wh), sh.Dp, sh.Fp, ptr(S), ptr(M_ord),
+                call("gatx_edge_forward_drop", ptr(Wh), sh.Dp, sh.Fp, ptr(S), ptr(M_ord),
                      ptr(graph.rowptr), ptr(graph.col), ptr(graph.perm), N, sh.NH, sh.F, hs,
                      gi, 1, mode, 0, int(sh.const), ptr(bias) if last else None, float(p),
                      ptr(seed), ptr(out), sh.out_cols, resid_p if last else None, sh.out_cols,
-                     int(elu) if last else 0, ptr(den), chunk, *hub, s)
+                     int(elu) if last else 0, ptr(den), chunk, *hub,
+                     *(drop_args if last else (0.0, None)), s)
     with _span("attention_alpha", (E2, sh.NH)):
         _attention_alpha(graph, S, M_ord, den, sh, alpha, argmax, s)
     saved.update(Wh=Wh, S=S, reassoc=False)
@@ -441,8 +457,10 @@ def layer_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShape, 
         # scale 1), and go is dead once the source pass has run, so it doubles as g_pre
         g_pre = go if (sh.concat and sh.F % 4 == 0) else torch.empty((N, sh.out_cols), **f32)
         pre_p = ptr(g_pre)
+    out_p = saved.get("out_p", 0.0)
     call("gatx_prepare_go_ex", ptr(g_out), ptr(out) if elu else None, N, sh.NH, sh.F,
-         int(sh.concat), int(elu), ptr(go), pre_p, pre_ld, s)
+         int(sh.concat), int(elu), ptr(go), pre_p, pre_ld, out_p,
+         ptr(saved["out_seed"]) if out_p > 0 else None, s)
     g_raw = g_corr = None
     if not sh.const:
         g_raw = torch.empty((sh.NH, max(E2, 1)), **f32)
@@ -527,7 +545,7 @@ def _reassoc_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShap
         g_pre = torch.empty((N, sh.out_cols), **f32)
         pre_p = ptr(g_pre)
     call("gatx_prepare_go_ex", ptr(g_out), ptr(out) if elu else None, N, NH, F, 1, int(elu),
-         ptr(go), pre_p, pre_ld, s)
+         ptr(go), pre_p, pre_ld, 0.0, None, s)
     Wp = padded_weight(W, Fin_p, sh.cache_weights)    # [NH*F][Fin_p], zero tail
     g_Z = torch.empty((N, NH * Fin_p), **f32)
     call("gatx_gemm_f32_batched", NH, N, Fin_p, F, ptr(go), sh.Dp, 1, Fp, ptr(Wp), Fin_p, 1,
@@ -573,8 +591,9 @@ def _reassoc_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShap
 
 class GATLayerFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, W, a, bias, resid, skip_W, graph, sh, p, seed, elu):
-        out, alpha, saved = layer_forward(x, W, a, bias, graph, sh, p, seed, resid, elu, skip_W)
+    def forward(ctx, x, W, a, bias, resid, skip_W, graph, sh, p, seed, elu, out_p, out_seed):
+        out, alpha, saved = layer_forward(x, W, a, bias, graph, sh, p, seed, resid, elu, skip_W,
+                                          out_p, out_seed)
         ctx.graph, ctx.sh, ctx.p, ctx.seed, ctx.saved, ctx.elu = graph, sh, p, seed, saved, elu
         ctx.has_resid = resid is not None
         ctx.resid_is_x = resid is not None and resid is x
@@ -605,7 +624,7 @@ class GATLayerFunction(torch.autograd.Function):
                 g_s = torch.empty_like(skip_W)
                 call("gatx_skip_weight_grad", ptr(eff), sh.NH, sh.skip_cols, sh.F_in, ptr(g_s),
                      stream())
-        return g_x, g_W, g_a, g_b, g_r, g_s, None, None, None, None, None
+        return g_x, g_W, g_a, g_b, g_r, g_s, None, None, None, None, None, None, None
 
 
 class SkipProjectionFunction(torch.autograd.Function):
@@ -655,6 +674,35 @@ class SkipProjectionFunction(torch.autograd.Function):
                  ptr(gW), F_in, 0, ptr(ws), wb, s)
             g_W = gW.repeat(ctx.num_heads, 1).div_(ctx.num_heads) if ctx.mean else gW
         return g_x, g_W, None, None, None
+
+
+class InputDropoutFunction(torch.autograd.Function):
+    """GATModel's input dropout (`models/GATModel.py:130`, F.dropout) on gatx_dropout: the
+    counter-based keep mask of the element index under a device seed (torch's generator draws
+    the seed, so it follows torch.cuda.manual_seed and is graph-capturable); the backward is the
+    same mask on the gradient. Used where the dropout cannot ride on the producing layer's
+    epilogue (the model input, or after a reassociated layer)."""
+
+    @staticmethod
+    def forward(ctx, x, p, seed):
+        _require(x, "x")
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        call("gatx_dropout", ptr(x), x.numel(), float(p), ptr(seed), ptr(y), stream())
+        ctx.p, ctx.seed = float(p), seed
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        gx = torch.empty_like(g)
+        call("gatx_dropout", ptr(g), g.numel(), ctx.p, ptr(ctx.seed), ptr(gx), stream())
+        return gx, None, None
+
+
+def input_dropout(x, p: float, seed):
+    """y = dropout(x) with gatx's mask (see InputDropoutFunction); seed: int or device int64."""
+    return InputDropoutFunction.apply(x, float(p), device_seed(seed, x.device))
 
 
 def device_seed(seed, dev) -> torch.Tensor:
@@ -729,13 +777,15 @@ def prepare_layer(x, edge_index, W, a, bias, num_heads, out_features, concat, ad
 
 def gat_layer_lazy(x, edge_index, W, a, bias, num_heads, out_features, concat, add_self_loops,
                    const_attention=False, dropout_p=0.0, seed=0, graph: Graph | None = None,
-                   resid=None, elu=False, skip_weight=None):
+                   resid=None, elu=False, skip_weight=None, out_dropout=None):
     """gat_layer without any host sync: returns (out, graph, alpha_bound) where alpha_bound is
     (graph.edge_bound, NH) and its first graph.num_edges rows are alpha in edge_index' order.
     resid / elu fuse GATModel's skip-add and ELU into the layer's epilogue:
     out = elu?(layer(x) + resid). skip_weight (GATModel's Linear skip, (NH*F, F_in)) folds the
     skip projection itself into the layer: resid = x W_skip^T (concat) or its head mean, computed
-    by the layer's own projection GEMM."""
+    by the layer's own projection GEMM. out_dropout = (p, device int64 seed): the next layer's
+    input dropout (GATModel.py:130) applied by this layer's epilogue (see fuses_output_dropout);
+    out is then the dropped output, with the mask of gatx_dropout under that seed."""
     x, W, a, resid, sh, graph = prepare_layer(x, edge_index, W, a, bias, num_heads, out_features,
                                               concat, add_self_loops, const_attention, graph,
                                               resid, skip_weight)
@@ -743,8 +793,15 @@ def gat_layer_lazy(x, edge_index, W, a, bias, num_heads, out_features, concat, a
         skip_weight = skip_weight.contiguous()
     p = float(dropout_p)
     seed_t = device_seed(seed, x.device) if p > 0 else None
+    out_p, out_seed = 0.0, None
+    if out_dropout is not None and float(out_dropout[0]) > 0:
+        out_p = float(out_dropout[0])
+        out_seed = device_seed(out_dropout[1], x.device)
+        if not fuses_output_dropout(num_heads, out_features, x.size(1), concat, const_attention):
+            raise RuntimeError("gatx: out_dropout needs a layer whose output comes from the edge "
+                               "pass (fuses_output_dropout)")
     out, alpha = GATLayerFunction.apply(x, W, a, bias, resid, skip_weight, graph, sh, p, seed_t,
-                                        bool(elu))
+                                        bool(elu), out_p, out_seed)
     return out, graph, alpha
 
 

@@ -78,19 +78,21 @@ class GATLayer(nn.Module):
         self.__dict__["_attention"] = value
 
     def forward(self, x, edge_index, return_attention_weights=False, *, graph=None, resid=None,
-                elu=False, skip_weight=None):
+                elu=False, skip_weight=None, out_dropout=None):
         """Reference signature (`models/gat_layer.py:42`); keyword-only extras: `graph` (a
         prebuilt gatx.Graph), `resid` / `elu` (GATModel's skip-add + ELU fused into the
         epilogue: returns elu?(out + resid)), `skip_weight` (GATModel's Linear skip weight,
-        folded into this layer's projection GEMM: resid = x W_skip^T, or its head mean). Without
+        folded into this layer's projection GEMM: resid = x W_skip^T, or its head mean),
+        `out_dropout` ((p, device seed): the next layer's input dropout applied by this layer's
+        epilogue, gatx.functional.fuses_output_dropout). Without
         return_attention_weights nothing waits for the device (|edge_index'| is only known
         there)."""
         p = float(self.dropout) if (self.dropout > 0 and self.training) else 0.0
         if torch.compiler.is_compiling():
             # traced by torch.compile: the registered op (gatx/ops.py), opaque to the compiler
-            if graph is not None or skip_weight is not None:
-                raise RuntimeError("gatx: graph= / skip_weight= are not supported under "
-                                   "torch.compile")
+            if graph is not None or skip_weight is not None or out_dropout is not None:
+                raise RuntimeError("gatx: graph= / skip_weight= / out_dropout= are not supported "
+                                   "under torch.compile")
             seed_t = self._dropout_seed(x.device) if p > 0 else None
             out, ei2, alpha, _ = torch.ops.gatx.layer_fwd(
                 x, edge_index, self.W.weight, None if self.const_attention else self.a.weight,
@@ -104,7 +106,7 @@ class GATLayer(nn.Module):
             x, edge_index, self.W.weight, None if self.const_attention else self.a.weight,
             self.bias_param if self.bias else None, self.num_heads, self.out_features,
             self.concat, self.add_self_loops, self.const_attention, p, seed, graph=graph,
-            resid=resid, elu=elu, skip_weight=skip_weight)
+            resid=resid, elu=elu, skip_weight=skip_weight, out_dropout=out_dropout)
         self.normalised_attention_coeffs = (g, alpha)
         if return_attention_weights:
             return out, (g.edge_index, self.normalised_attention_coeffs)

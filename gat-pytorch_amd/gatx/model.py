@@ -25,6 +25,13 @@ from .layer import GATLayer
 SKIP_GEMM_MIN_MACS = 1 << 26
 
 
+def _dropout_fuse_enabled() -> bool:
+    """GATX_DROPOUT_FUSE=0 applies every input dropout with the standalone gatx kernel instead
+    of the producing layer's epilogue (A/B tests)."""
+    from .functional import _env_int
+    return _env_int("GATX_DROPOUT_FUSE", 1) != 0
+
+
 def _skip_fold_enabled() -> bool:
     """GATX_SKIP_FOLD=0 turns the folded skip projection off (A/B tests and measurements)."""
     from .functional import _env_int
@@ -79,13 +86,37 @@ class GATModel(nn.Module):
             return skip_output
         return skip_output.view(-1, nh, f).mean(dim=1)
 
+    def _fuse_next_dropout(self, i) -> bool:
+        """Layer i applies layer i+1's input dropout in its epilogue: layer i+1 has no skip (the
+        skip reads the undropped input) and layer i's output comes from the edge pass."""
+        from .functional import fuses_output_dropout
+        if i + 1 >= len(self.gat_layer_list) or self.add_skip_connection[i + 1]:
+            return False
+        lay = self.gat_layer_list[i]
+        return _dropout_fuse_enabled() and fuses_output_dropout(
+            lay.num_heads, lay.out_features, lay.in_features, lay.concat, lay.const_attention)
+
     def _run(self, x, edge_index, with_attention):
         attention_weights_list = []
         skip_count = 0
         L = len(self.gat_layer_list)
+        # input dropout (models/GATModel.py:130) on gatx's counter-based mask: one device seed per
+        # layer input drawn up front (the same draws whichever way each dropout is applied),
+        # applied by the producing layer's epilogue where it can be, else by gatx_dropout
+        gx_drop = (self.training and self.dropout > 0 and x.is_cuda
+                   and not torch.compiler.is_compiling())
+        seeds = ([torch.randint(0, 2 ** 62, (1,), dtype=torch.int64, device=x.device)
+                  for _ in range(L)] if gx_drop else None)
+        pre_dropped = False
         for i in range(L):
             layer_input = x
-            x = F.dropout(x, p=self.dropout, training=self.training)
+            if gx_drop:
+                if not pre_dropped:
+                    from .functional import input_dropout
+                    x = input_dropout(x, self.dropout, seeds[i])
+            else:
+                x = F.dropout(x, p=self.dropout, training=self.training)
+            fuse_next = gx_drop and self._fuse_next_dropout(i)
             resid = skip_w = None
             if self.add_skip_connection[i]:
                 skip = self.skip_layer_list[skip_count]
@@ -99,6 +130,9 @@ class GATModel(nn.Module):
                 skip_count += 1
             # layer -> (+ skip) -> ELU except after the last layer, fused in the layer epilogue
             extra = {"skip_weight": skip_w} if skip_w is not None else {}
+            if fuse_next:
+                extra["out_dropout"] = (self.dropout, seeds[i + 1])
+            pre_dropped = fuse_next
             out = self.gat_layer_list[i](x, edge_index, return_attention_weights=with_attention,
                                          resid=resid, elu=(i != L - 1), **extra)
             if with_attention:
@@ -109,7 +143,9 @@ class GATModel(nn.Module):
         return x, edge_index, attention_weights_list
 
     def forward(self, x, edge_index):
-        """`models/GATModel.py:120-151`: dropout -> layer -> skip -> ELU, per layer."""
+        """`models/GATModel.py:120-151`: dropout -> layer -> skip -> ELU, per layer. In training
+        with dropout the masks are gatx's counter-based ones (torch's RNG stream cannot be
+        matched bit for bit); the next layer's dropout rides on the layer's epilogue."""
         return self._run(x, edge_index, False)[0]
 
     def forward_and_return_attention(self, x, edge_index, return_attention_weights=True):

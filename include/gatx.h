@@ -253,6 +253,24 @@ int gatx_edge_forward_hubs(const float* rows, int64_t row_stride, int64_t head_s
                            float* den, int64_t chunk, int hub_edges, const int32_t* hubs,
                            const int32_t* hub_count, int64_t hub_bound, float* hub_part,
                            gatx_stream_t stream);
+/* gatx_edge_forward_hubs with the NEXT layer's input dropout (models/GATModel.py:130, applied
+ * to this layer's output) fused after the ELU: out = keep(out_seed, n*OC + c) ? v/(1-out_p) : 0
+ * (OC = output width; the mask of gatx_dropout). For the last head-mean pass only. */
+int gatx_edge_forward_drop(const float* rows, int64_t row_stride, int64_t head_stride,
+                           const float* S, const uint32_t* M_ord, const int32_t* rowptr,
+                           const int32_t* col, const int32_t* perm, int64_t num_nodes,
+                           int num_heads, int out_features, int heads_per_item, int group_begin,
+                           int group_count, int mean_mode, int concat, int const_attention,
+                           const float* bias, float dropout_p, const uint64_t* seed, float* out,
+                           int64_t out_ld, const float* resid, int64_t resid_ld, int elu,
+                           float* den, int64_t chunk, int hub_edges, const int32_t* hubs,
+                           const int32_t* hub_count, int64_t hub_bound, float* hub_part,
+                           float out_p, const uint64_t* out_seed, gatx_stream_t stream);
+/* GATModel's input dropout (models/GATModel.py:130, F.dropout) as a counter-based mask on the
+ * element index (the attention dropout's splitmix64 hash): y[i] = keep(seed, i) ? x[i]/(1-p) : 0.
+ * The gradient is the same call on g_y. In place (y == x) is allowed. */
+int gatx_dropout(const float* x, int64_t n, float p, const uint64_t* seed, float* y,
+                 gatx_stream_t stream);
 
 /* alpha [E2][NH] in edge_index' order from S, M and den (one thread per CSR slot, all heads of
  * an edge stored together), plus the argmax records (see gatx_edge_forward). */
@@ -294,10 +312,12 @@ int gatx_pad_rows(const float* src, int64_t rows, int64_t cols, int64_t ld_src, 
 int gatx_prepare_go(const float* g_out, const float* out, int64_t num_nodes, int NH, int F,
                     int concat, int elu, float* go, float* g_pre, gatx_stream_t stream);
 /* The same with g_pre rows pre_ld floats apart (>= the output width): the folded skip's
- * gradient written straight into its columns of G_aug (gatx_prepare_weights_skip). */
+ * gradient written straight into its columns of G_aug (gatx_prepare_weights_skip); out_p /
+ * out_seed: the layer's output carries the next layer's fused input dropout
+ * (gatx_edge_forward_drop): g_out goes through the mask, ELU's derivative from out * (1-p). */
 int gatx_prepare_go_ex(const float* g_out, const float* out, int64_t num_nodes, int NH, int F,
                        int concat, int elu, float* go, float* g_pre, int64_t pre_ld,
-                       gatx_stream_t stream);
+                       float out_p, const uint64_t* out_seed, gatx_stream_t stream);
 
 /* Destination pass, one wave per (node n, head h):
  *   g_alpha~[e,h] = <go[n,h,:], Wh[src,h,:]>; g_alpha = g_alpha~ * keep/(1-p) + g_alpha_ret
