@@ -419,6 +419,10 @@ def main():
     ap.add_argument("--rmat-edges", type=int, default=160_000_000)
     ap.add_argument("--cached-graph", action="store_true",
                     help="reuse the CSR across steps (excludes graph preprocessing)")
+    ap.add_argument("--wiring", choices=["gatx", "reference"], default="gatx",
+                    help="gatx: skip / ELU / dropout fused into the layers; reference: the "
+                         "reference GATModel.forward op for op around gatx GATLayers (the "
+                         "INTEGRATION.md drop-in)")
     ap.add_argument("--hipgraph", choices=["auto", "on", "off"], default="auto",
                     help="replay each step as one captured hipGraph (gatx.capture). auto: forward "
                          "steps, and PATTERN training on one GPU")
@@ -462,6 +466,7 @@ def main():
     cfg = dict(data_config[ds])
     torch.manual_seed(0)
     model = GATModel(**cfg).to(dev)
+    model.fuse_wiring = args.wiring == "gatx"
     model.train(args.mode == "train")
     b = gd.dataset_batch(ds, args.graphs, graph_seed=42 + 1000 * rank, feature_seed=1 + rank)
     x = torch.from_numpy(b.x).to(dev)
@@ -592,7 +597,10 @@ def main():
                    "parallelism": ("replicas" if planetoid and world > 1
                                    else f"graph-batch dp{world}"),
                    "launch": "hipGraph replay (last steps//10 eager, HIP-event instrumented)"
-                             if use_graph else "eager"},
+                             if use_graph else "eager",
+                   "wiring": ("gatx (skip / ELU / dropout fused into the layers)"
+                              if args.wiring == "gatx" else
+                              "reference GATModel.forward around gatx GATLayers (drop-in)")},
         "unique_GBps": round(uniq / step_s / 1e9, 1),
         "roofline_time_frac": round(t_roof / step_s, 4),
         "roofline_time_basis": "sum over the forward's kernels of max(unique bytes / 8 TB/s, "

@@ -68,6 +68,11 @@ class GATModel(nn.Module):
                                    else nn.Linear(fin, skip_out, bias=False))
         self.gat_layer_list = nn.ModuleList(gat_layers)
         self.skip_layer_list = nn.ModuleList(skip_layers)
+        # True: skip / ELU / dropout fused into the layers (gatx's wiring). False: the
+        # reference's own forward (`models/GATModel.py:120-151`) op for op around gatx GATLayers —
+        # exactly what the INTEGRATION.md §1 drop-in (swap the import) runs; bench.py
+        # --wiring reference times it
+        self.fuse_wiring = True
 
     def _resid(self, i, skip_count, layer_input):
         """Skip connection of layer i (`models/GATModel.py:135-145`) in the layer's output shape,
@@ -96,7 +101,37 @@ class GATModel(nn.Module):
         return _dropout_fuse_enabled() and fuses_output_dropout(
             lay.num_heads, lay.out_features, lay.in_features, lay.concat, lay.const_attention)
 
+    def _run_reference_wiring(self, x, edge_index, with_attention):
+        """`models/GATModel.py:153-187` with the gatx layer: dropout, layer, skip module (+ head
+        mean), add, ELU as separate torch ops."""
+        attention_weights_list = []
+        skip_count = 0
+        L = len(self.gat_layer_list)
+        for i in range(L):
+            layer_input = x
+            x = F.dropout(x, p=self.dropout, training=self.training)
+            out = self.gat_layer_list[i](x, edge_index, return_attention_weights=with_attention)
+            if with_attention:
+                x, (edge_index, att) = out
+                attention_weights_list.append(att)
+            else:
+                x = out
+            if self.add_skip_connection[i]:
+                skip_output = self.skip_layer_list[skip_count](layer_input)
+                skip_count += 1
+                if self.heads_concat_per_layer[i]:
+                    x = x + skip_output
+                else:
+                    skip_output = skip_output.view(-1, self.num_heads_per_layer[i + 1],
+                                                   self.head_output_features_per_layer[i + 1])
+                    x = x + skip_output.mean(dim=1)
+            if i != L - 1:
+                x = F.elu(x)
+        return x, edge_index, attention_weights_list
+
     def _run(self, x, edge_index, with_attention):
+        if not self.fuse_wiring:
+            return self._run_reference_wiring(x, edge_index, with_attention)
         attention_weights_list = []
         skip_count = 0
         L = len(self.gat_layer_list)

@@ -124,3 +124,31 @@ def test_folded_skip_pattern_model(device, monkeypatch):
                         ("skip", f"skip_layer_list.{i}.weight")):
             r = ref[k][i]
             assert np.abs(gr1[name] - r).max() <= GRAD_TOL * max(1.0, np.abs(r).max()), name
+
+
+@pytest.mark.parametrize("ds", ["PPI", "PATTERN"])
+def test_reference_wiring_equals_fused(ds, device):
+    """gatx.GATModel with fuse_wiring=False runs the reference's GATModel.forward op for op
+    around gatx layers (the INTEGRATION.md drop-in; bench.py --wiring reference): same output
+    and gradients as the fused wiring within fp32 noise."""
+    import gatx
+    from gatx import data as gd
+    from gatx.config import data_config
+    cfg = dict(data_config[ds])
+    b = gd.dataset_batch(ds, 2, graph_seed=7, feature_seed=8)
+    x = torch.from_numpy(b.x).to(device)
+    ei = torch.from_numpy(b.edge_index).to(device)
+    res = []
+    for fuse in (True, False):
+        torch.manual_seed(11)
+        model = gatx.GATModel(**cfg).to(device)
+        model.fuse_wiring = fuse
+        out = model(x, ei)
+        g = torch.from_numpy(gd.normal(9, out.numel()).reshape(tuple(out.shape))).to(device)
+        (out * g).sum().backward()
+        res.append((out.detach().cpu().numpy(),
+                    {n: p.grad.cpu().numpy() for n, p in model.named_parameters()}))
+    (o1, g1), (o0, g0) = res
+    assert np.abs(o1 - o0).max() <= 1e-4 * max(1.0, np.abs(o0).max())
+    for n in g0:
+        assert np.abs(g1[n] - g0[n]).max() <= 1e-4 * max(1.0, np.abs(g0[n]).max()), n
