@@ -177,15 +177,27 @@ class GATModel(nn.Module):
                 x = out
         return x, edge_index, attention_weights_list
 
-    def forward(self, x, edge_index):
-        """`models/GATModel.py:120-151`: dropout -> layer -> skip -> ELU, per layer. In training
-        with dropout the masks are gatx's counter-based ones (torch's RNG stream cannot be
-        matched bit for bit); the next layer's dropout rides on the layer's epilogue."""
-        return self._run(x, edge_index, False)[0]
+    @staticmethod
+    def _unpack(x, edge_index):
+        # the reference takes a PyG-style batch (`data.x`, `data.edge_index`); tensors also work
+        if edge_index is None:
+            if not (hasattr(x, "x") and hasattr(x, "edge_index")):
+                raise TypeError("GATModel: pass (x, edge_index) or an object with .x and "
+                                ".edge_index")
+            return x.x, x.edge_index
+        return x, edge_index
 
-    def forward_and_return_attention(self, x, edge_index, return_attention_weights=True):
-        """`models/GATModel.py:153-187`: as forward, also returning edge_index' and the alphas."""
-        return self._run(x, edge_index, True)
+    def forward(self, x, edge_index=None):
+        """`models/GATModel.py:120-151` (`forward(data)`, or `forward(x, edge_index)`): dropout
+        -> layer -> skip -> ELU, per layer. In training with dropout the masks are gatx's
+        counter-based ones (torch's RNG stream cannot be matched bit for bit); the next layer's
+        dropout rides on the layer's epilogue."""
+        return self._run(*self._unpack(x, edge_index), False)[0]
+
+    def forward_and_return_attention(self, x, edge_index=None, return_attention_weights=True):
+        """`models/GATModel.py:153-187` (`(data)` or `(x, edge_index)`): as forward, also
+        returning edge_index' and the alphas."""
+        return self._run(*self._unpack(x, edge_index), True)
 
     @staticmethod
     def calc_attention_norm(edge_index, attention_list):

@@ -152,3 +152,24 @@ def test_reference_wiring_equals_fused(ds, device):
     assert np.abs(o1 - o0).max() <= 1e-4 * max(1.0, np.abs(o0).max())
     for n in g0:
         assert np.abs(g1[n] - g0[n]).max() <= 1e-4 * max(1.0, np.abs(g0[n]).max()), n
+
+
+def test_model_accepts_reference_data_object(device):
+    """forward(data) / forward_and_return_attention(data) as the reference calls them
+    (`models/GATModel.py:120-121, 153-154`: data.x, data.edge_index)."""
+    from types import SimpleNamespace
+    import gatx
+    from gatx import data as gd
+    from gatx.config import data_config
+    b = gd.dataset_batch("PATTERN", 2, graph_seed=3, feature_seed=4)
+    x = torch.from_numpy(b.x).to(device)
+    ei = torch.from_numpy(b.edge_index).to(device)
+    torch.manual_seed(2)
+    model = gatx.GATModel(**data_config["PATTERN"]).to(device).eval()
+    data = SimpleNamespace(x=x, edge_index=ei)
+    with torch.no_grad():
+        a = model(x, ei)
+        b2 = model(data)
+        o, ei2, atts = model.forward_and_return_attention(data)
+    assert torch.equal(a, b2) and torch.equal(a, o)
+    assert len(atts) == data_config["PATTERN"]["num_layers"] and ei2.shape[0] == 2
