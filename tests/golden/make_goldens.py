@@ -346,8 +346,24 @@ def model_case(name, x, ei, gen, layers, skips, dataset, wgen=None):
     print(f"{name}: N={x.shape[0]} out={tuple(xt.shape)}")
 
 
+def ppi_full_cases():
+    """The three PPI layer shapes on one full-size PPI graph (2245 nodes, 61318 edges: SURVEY.md
+    §8c golden 3 at the dataset's size, `run_config.py:18-33`); large arrays as row samples plus
+    whole-array checksums."""
+    for lname, (fin, F, NH, cc) in {"l0": (50, 256, 4, True), "l1": (1024, 256, 4, True),
+                                     "l2": (1024, 121, 6, False)}.items():
+        g = dict(G=1, n=2245, e=61318, in_features=fin, feature_seed=13)
+        xx, ee = gen_batch(g)
+        run_layer_case(f"ppi_full_{lname}", xx, ee, fin, F, NH, cc,
+                       gdata.xavier_uniform(22, NH * F, fin),
+                       gdata.xavier_uniform(23, NH, NH * 2 * F), gen=g, wgen=[22, 23])
+
+
 if __name__ == "__main__":
-    if "--extra-only" in sys.argv:
+    if "--ppi-full-only" in sys.argv:
+        torch.set_num_threads(8)
+        ppi_full_cases()
+    elif "--extra-only" in sys.argv:
         torch.set_num_threads(8)
         extra_cases()
     else:
