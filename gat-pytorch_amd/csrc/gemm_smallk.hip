@@ -21,6 +21,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int SK_WAVES = 8, SK_KMAX = 64, SK_NMAX = 256;
 constexpr int SK_KSLOTS = SK_KMAX / 8;
+constexpr int SK_PLANE = SK_KSLOTS * SK_NMAX * 16;   // bytes per bf16 plane of B
 
 __device__ inline uint32_t sk_cvt_pk(float a, float b) {
   typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
@@ -48,18 +49,14 @@ __device__ inline void sk_split8(const float (&v)[8], uint4& h, uint4& m, uint4&
 
 // A row-major (k-contiguous, lda), B as rows of k (ldb: B(k, n) = B[n * ldb + k]). VEC: A rows
 // 16-byte aligned (lda % 4 == 0, aligned base), so full 8-k groups load as two float4.
-// NM: output columns per workgroup (blockIdx.z picks the column slice): 256 = one workgroup
-// per CU (96 KB of planes), 128 = two (48 KB).
-template <bool VEC, int NM>
-__global__ void __launch_bounds__(64 * SK_WAVES, NM == 256 ? 1 : 2) gemm_smallk_kernel(GemmArgs g) {
-  constexpr int SK_PLANE = SK_KSLOTS * NM * 16;   // bytes per bf16 plane of B
+template <bool VEC>
+__global__ void __launch_bounds__(64 * SK_WAVES, 1) gemm_smallk_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) char wl[3 * SK_PLANE];
-  __shared__ float bias_l[NM];
+  __shared__ float bias_l[SK_NMAX];
   const int b = blockIdx.y;
-  const int n_base = blockIdx.z * NM;
   const float* __restrict__ A = g.A + b * g.a_bs;
-  const float* __restrict__ B = g.B + b * g.b_bs + (int64_t)n_base * g.ldb;
-  const int K = (int)g.K, N = min((int)g.N - n_base, NM);
+  const float* __restrict__ B = g.B + b * g.b_bs;
+  const int K = (int)g.K, N = (int)g.N;
   const int64_t M = g.M;
   const int ncb = (N + 31) / 32;
 
@@ -75,13 +72,13 @@ __global__ void __launch_bounds__(64 * SK_WAVES, NM == 256 ? 1 : 2) gemm_smallk_
     }
     uint4 h, m, l;
     sk_split8(v, h, m, l);
-    const int o = (kc * NM + n) * 16;
+    const int o = (kc * SK_NMAX + n) * 16;
     *(uint4*)(wl + o) = h;
     *(uint4*)(wl + SK_PLANE + o) = m;
     *(uint4*)(wl + 2 * SK_PLANE + o) = l;
   }
-  for (int t = threadIdx.x; t < NM; t += 64 * SK_WAVES)
-    bias_l[t] = (g.bias && t < N) ? g.bias[b * g.bias_bs + n_base + t] : 0.f;
+  for (int t = threadIdx.x; t < SK_NMAX; t += 64 * SK_WAVES)
+    bias_l[t] = (g.bias && t < N) ? g.bias[b * g.bias_bs + t] : 0.f;
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5;
@@ -139,7 +136,7 @@ __global__ void __launch_bounds__(64 * SK_WAVES, NM == 256 ? 1 : 2) gemm_smallk_
 #pragma unroll
           for (int p = 0; p < 3; ++p)
             fb[i][p] = *(const bf16x8*)(wl + p * SK_PLANE +
-                                        ((2 * s + half) * NM + (cb + i) * 32 + (lane & 31)) * 16);
+                                        ((2 * s + half) * SK_NMAX + (cb + i) * 32 + (lane & 31)) * 16);
         // small terms first: (l,h) (h,l) (m,m) (m,h) (h,m) (h,h), as gemm_x3_kernel
         constexpr int PLA[6] = {2, 0, 1, 1, 0, 0};
         constexpr int PLB[6] = {0, 2, 1, 0, 1, 0};
@@ -158,7 +155,7 @@ __global__ void __launch_bounds__(64 * SK_WAVES, NM == 256 ? 1 : 2) gemm_smallk_
         const int col = (cb + i) * 32 + (lane & 31);
         if (col >= N) continue;
         const float bv = bias_l[col];
-        float* base = g.C0 + b * g.c0_bs + n_base + col;
+        float* base = g.C0 + b * g.c0_bs + col;
         const int64_t row0 = rb * 32 + 4 * half;
         const bool full = row0 + 27 < M;
 #pragma unroll
@@ -186,23 +183,13 @@ int launch_gemm_smallk(const gk::GemmArgs& g, int batch, hipStream_t stream) {
   GATX_REQUIRE(g.K <= SK_KMAX && g.N <= SK_NMAX && batch < 65536, "gemm_smallk: shape");
   // one 96-KB workgroup per CU: ~256 workgroups over the batch entries, each sweeping its
   // entry's 32-row blocks
-  static const int nm = [] {   // A/B: GATX_SMALLK_NM=128 (two column slices per entry)
-    const char* e = getenv("GATX_SMALLK_NM");
-    return e && atoi(e) == 128 ? 128 : 256;
-  }();
   const int64_t nrb = ceil_div(g.M, 32);
-  const unsigned nz = (unsigned)ceil_div(g.N, nm);
-  const int64_t per = std::max<int64_t>(1, (nm == 256 ? 256 : 512) / (batch * (int64_t)nz));
+  const int64_t per = std::max<int64_t>(1, 256 / batch);
   const unsigned gx = (unsigned)std::min<int64_t>(per, ceil_div(nrb, SK_WAVES));
-  dim3 grid(gx, (unsigned)batch, nz);
+  dim3 grid(gx, (unsigned)batch);
   const bool vec = ((uintptr_t)g.A % 16 == 0) && g.lda % 4 == 0 && g.a_bs % 4 == 0;
-  if (nm == 128) {
-    if (vec) gemm_smallk_kernel<true, 128><<<grid, 64 * SK_WAVES, 0, stream>>>(g);
-    else gemm_smallk_kernel<false, 128><<<grid, 64 * SK_WAVES, 0, stream>>>(g);
-  } else {
-    if (vec) gemm_smallk_kernel<true, 256><<<grid, 64 * SK_WAVES, 0, stream>>>(g);
-    else gemm_smallk_kernel<false, 256><<<grid, 64 * SK_WAVES, 0, stream>>>(g);
-  }
+  if (vec) gemm_smallk_kernel<true><<<grid, 64 * SK_WAVES, 0, stream>>>(g);
+  else gemm_smallk_kernel<false><<<grid, 64 * SK_WAVES, 0, stream>>>(g);
   GATX_LAUNCH_CHECK("gemm_smallk");
   return 0;
 }
