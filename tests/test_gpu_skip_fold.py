@@ -173,3 +173,31 @@ def test_model_accepts_reference_data_object(device):
         o, ei2, atts = model.forward_and_return_attention(data)
     assert torch.equal(a, b2) and torch.equal(a, o)
     assert len(atts) == data_config["PATTERN"]["num_layers"] and ei2.shape[0] == 2
+
+
+@pytest.mark.parametrize("mode", [1, 0])   # x3 (default) and f32-MFMA arithmetic
+@pytest.mark.parametrize("M,N,K,s1,s2", [(96, 300, 64, 128, 200), (44900, 1036 + 48, 256, 1024, 1036),
+                                          (3001, 450, 96, 48, 56)])
+def test_projection_gemm3_three_outputs(mode, M, N, K, s1, s2, device):
+    """gatx_projection_gemm3's three output ranges (the folded skip's C2) in both arithmetics,
+    including shapes whose last partial wave is split along K (workspace, fix-up kernel)."""
+    from gatx._lib import call, lib, ptr, stream
+    from gatx.functional import gemm_workspace
+    g = torch.Generator(device=device).manual_seed(M + N)
+    A = torch.randn(M, K, device=device, generator=g)
+    W = torch.randn(N, K, device=device, generator=g)   # B(k, n) = W[n, k], as W_aug
+    C0 = torch.full((M, s1), float("nan"), device=device)
+    C1 = torch.full((M, s2 - s1), float("nan"), device=device)
+    C2 = torch.full((M, N - s2), float("nan"), device=device)
+    lib.gatx_set_gemm_mode(mode)
+    try:
+        ws = gemm_workspace(M, N, K, device)
+        call("gatx_projection_gemm3", M, N, K, ptr(A), K, 1, ptr(W), 1, K, ptr(C0), s1, s1,
+             ptr(C1), s2 - s1, s2, ptr(C2), N - s2, *ws, stream())
+        torch.cuda.synchronize()
+    finally:
+        lib.gatx_set_gemm_mode(1)
+    ref = A.double() @ W.double().t()
+    got = torch.cat([C0, C1, C2], 1).double()
+    assert torch.isfinite(got).all()
+    assert (got - ref).abs().max().item() < 1e-4 * max(1.0, K ** 0.5)
