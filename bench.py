@@ -1,7 +1,8 @@
 """Benchmark: GAT-layer edges/s + achieved HBM GB/s, PPI 3-layer forward (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--graphs G] [--mode fwd|train]
-                    [--workload ppi|pattern|rmat]
+                    [--workload ppi|pattern|rmat|cora|citeseer|pubmed]
+                    [--wiring gatx|reference]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
 Workload: per rank a synthetic PPI-shaped batch of G graphs (2245 nodes and 61318
