@@ -290,6 +290,96 @@ __global__ void __launch_bounds__(256) radix_scatter_kernel(
   }
 }
 
+// The same pass with the block's tile staged in LDS: every key is first placed at its stable
+// position within the tile's digit-sorted order (the round ranking above, against the tile's own
+// per-digit exclusive prefix), then the tile is written out in that order, so consecutive
+// threads store consecutive positions of one digit's run (runs of ~tile/2^BITS keys) instead of
+// one scattered 4-byte store per key.
+template <int BITS>
+__global__ void __launch_bounds__(256) radix_scatter_lds_kernel(
+    const int32_t* __restrict__ keys, const int32_t* __restrict__ vals, int64_t n, int shift,
+    int items, int64_t nblocks, const uint32_t* __restrict__ offs,
+    const uint32_t* __restrict__ hist, int32_t* __restrict__ keys_out,
+    int32_t* __restrict__ vals_out) {
+  constexpr int R = 1 << BITS, PER = R / 256;
+  __shared__ uint32_t gbase[R];    // the digit's first global position for this block
+  __shared__ uint32_t lstart[R];   // the digit's first position within the tile
+  __shared__ uint32_t lrun[R];     // running position within the tile
+  __shared__ uint32_t cnt[4][R];
+  __shared__ int32_t tk[kMaxSortItems * 256];
+  __shared__ int32_t tv[kMaxSortItems * 256];
+  __shared__ uint32_t wsum[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // this block's digit counts -> exclusive prefix over the digits (PER consecutive per thread)
+  uint32_t c[PER], tot = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int d = tid * PER + j;
+    c[j] = hist[(int64_t)d * nblocks + blockIdx.x];
+    tot += c[j];
+    gbase[d] = offs[(int64_t)d * nblocks + blockIdx.x];
+  }
+  uint32_t x = tot;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wave] = x;
+#pragma unroll
+  for (int w = 0; w < 4; ++w)
+#pragma unroll
+    for (int j = 0; j < PER; ++j) cnt[w][tid + 256 * j] = 0;
+  __syncthreads();
+  uint32_t run = x - tot;
+  for (int w = 0; w < wave; ++w) run += wsum[w];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    lstart[tid * PER + j] = run;
+    lrun[tid * PER + j] = run;
+    run += c[j];
+  }
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const int64_t tile = (int64_t)blockIdx.x * 256 * items;
+  for (int r = 0; r < items; ++r) {
+    const int64_t idx = tile + r * 256 + tid;
+    const bool valid = idx < n;
+    const int32_t key = valid ? keys[idx] : 0;
+    const int32_t val = valid ? (vals ? vals[idx] : (int32_t)idx) : 0;
+    const int d = (key >> shift) & (R - 1);
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < BITS; ++b) {
+      const uint64_t bb = __ballot((d >> b) & 1);
+      peers &= ((d >> b) & 1) ? bb : ~bb;
+    }
+    const int rank = __popcll(peers & lt);
+    const bool lead = valid && rank == 0;
+    __syncthreads();   // lstart/lrun ready (first round) / previous round's updates complete
+    if (lead) cnt[wave][d] = (uint32_t)__popcll(peers);
+    __syncthreads();
+    if (valid) {
+      uint32_t pos = lrun[d] + rank;
+      for (int w = 0; w < wave; ++w) pos += cnt[w][d];
+      tk[pos] = key;
+      tv[pos] = val;
+    }
+    __syncthreads();
+    if (lead) {
+      atomicAdd(&lrun[d], cnt[wave][d]);
+      cnt[wave][d] = 0;
+    }
+  }
+  __syncthreads();
+  const int64_t count = min((int64_t)items * 256, n - tile);
+  for (int j = tid; j < count; j += 256) {
+    const int32_t key = tk[j];
+    const int d = (key >> shift) & (R - 1);
+    const uint32_t gpos = gbase[d] + ((uint32_t)j - lstart[d]);
+    keys_out[gpos] = key;
+    vals_out[gpos] = tv[j];
+  }
+}
+
 inline unsigned grid_for(int64_t n, int block = 256, int64_t cap = 16384) {
   int64_t g = ceil_div(n > 0 ? n : 1, block);
   return (unsigned)(g < cap ? g : cap);
@@ -380,7 +470,17 @@ int sort_pairs(const int32_t* keys_in, const int32_t* vals_in, int32_t* keys_out
     hipError_t r = rocprim::exclusive_scan(w.scan_tmp, b, w.hist, w.offs, 0u, (size_t)m,
                                            rocprim::plus<uint32_t>(), stream);
     if (r != hipSuccess) { set_error("radix scan: %s", hipGetErrorString(r)); return (int)r; }
-    if (wide)
+    static const bool lds_tiles = [] {   // A/B: GATX_RADIX_LDS=0 keeps the direct scatter
+      const char* e = getenv("GATX_RADIX_LDS");
+      return !(e && strcmp(e, "0") == 0);
+    }();
+    if (lds_tiles && wide)
+      radix_scatter_lds_kernel<kWideBits><<<(unsigned)nb, 256, 0, stream>>>(
+          ck, cv, n, 0, items, nb, w.offs, w.hist, ok, ov);
+    else if (lds_tiles)
+      radix_scatter_lds_kernel<kRadixBits><<<(unsigned)nb, 256, 0, stream>>>(
+          ck, cv, n, shift, items, nb, w.offs, w.hist, ok, ov);
+    else if (wide)
       radix_scatter_kernel<kWideBits><<<(unsigned)nb, 256, 0, stream>>>(ck, cv, n, 0, items, nb,
                                                                         w.offs, ok, ov);
     else
