@@ -1,0 +1,60 @@
+"""Host-side decisions of the GATModel wiring fused into the layers (CPU, no kernel calls): which
+layers fold their Linear skip into the projection GEMM, which apply the next layer's input
+dropout in their epilogue, and the skip-fold / dropout-fuse switches. Reference wiring:
+`models/GATModel.py:64-116` (skip construction) and `:128-149` (dropout, skip-add, ELU)."""
+import pytest
+
+from gatx.config import data_config
+
+
+def _model(name, **over):
+    import gatx
+    cfg = dict(data_config[name])
+    cfg.update(over)
+    return gatx.GATModel(**cfg)
+
+
+def test_skip_modules_follow_the_reference():
+    from torch import nn
+    pat = _model("PATTERN")   # 3 -> 48 -> 96 -> 48 -> 1: every skip a Linear
+    assert all(isinstance(s, nn.Linear) for s in pat.skip_layer_list)
+    assert [tuple(s.weight.shape) for s in pat.skip_layer_list] == [(48, 3), (96, 48), (48, 96),
+                                                                      (1, 48)]
+    ppi = _model("PPI")       # layer 1's skip is 1024 -> 1024: Identity
+    assert len(ppi.skip_layer_list) == 1 and isinstance(ppi.skip_layer_list[0], nn.Identity)
+
+
+@pytest.mark.parametrize("name,expected", [
+    ("Cora", [True, False]),       # layer 0 (1433 -> 8x8) feeds layer 1's dropout
+    ("Pubmed", [True, False]),
+    ("Citeseer", [True, False]),
+    ("PPI", [False, True, False]),    # layer 1 has a skip (reads the undropped input), so layer
+                                      # 0 does not drop for it; layer 1 feeds layer 2's dropout
+    ("PATTERN", [False, False, False, False]),   # every layer has a skip
+])
+def test_next_layer_dropout_fusion_decisions(name, expected):
+    m = _model(name)
+    assert [m._fuse_next_dropout(i) for i in range(m.num_layers)] == expected
+
+
+def test_dropout_fuse_switch(monkeypatch):
+    from gatx import functional
+    monkeypatch.setenv("GATX_DROPOUT_FUSE", "0")
+    functional.reset_tuning()
+    m = _model("Cora")
+    assert not any(m._fuse_next_dropout(i) for i in range(m.num_layers))
+
+
+def test_output_dropout_needs_an_edge_pass_epilogue():
+    from gatx.functional import fuses_output_dropout, use_reassociation, LayerShape
+    # PPI layer 0 (50 -> 4 x 256) is reassociated: no fused output dropout
+    assert use_reassociation(LayerShape(4, 256, 50, True, False))
+    assert not fuses_output_dropout(4, 256, 50, True)
+    # head-mean layers and wide inputs take the direct edge pass
+    assert fuses_output_dropout(6, 121, 1024, False)
+    assert fuses_output_dropout(8, 8, 1433, True)
+
+
+def test_reference_wiring_flag_defaults_to_fused():
+    m = _model("PPI")
+    assert m.fuse_wiring is True
