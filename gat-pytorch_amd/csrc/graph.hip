@@ -240,11 +240,12 @@ __global__ void __launch_bounds__(256) radix_hist_kernel(const int32_t* __restri
     hist[(int64_t)(threadIdx.x + 256 * j) * nblocks + blockIdx.x] = h[threadIdx.x + 256 * j];
 }
 
-template <int BITS>
+template <int BITS, bool V2 = false>
 __global__ void __launch_bounds__(256) radix_scatter_kernel(
     const int32_t* __restrict__ keys, const int32_t* __restrict__ vals, int64_t n, int shift,
     int items, int64_t nblocks, const uint32_t* __restrict__ offs, int32_t* __restrict__ keys_out,
-    int32_t* __restrict__ vals_out) {
+    int32_t* __restrict__ vals_out, const int32_t* __restrict__ vals2 = nullptr,
+    int32_t* __restrict__ vals2_out = nullptr) {
   constexpr int R = 1 << BITS, PER = R / 256;
   __shared__ uint32_t base[R];
   __shared__ uint32_t cnt[4][R];
@@ -262,6 +263,7 @@ __global__ void __launch_bounds__(256) radix_scatter_kernel(
     const bool valid = idx < n;
     const int32_t key = valid ? keys[idx] : 0;
     const int32_t val = valid ? (vals ? vals[idx] : (int32_t)idx) : 0;
+    const int32_t val2 = (V2 && valid) ? vals2[idx] : 0;
     const int d = (key >> shift) & (R - 1);
     uint64_t peers = __ballot(valid);
 #pragma unroll
@@ -279,6 +281,7 @@ __global__ void __launch_bounds__(256) radix_scatter_kernel(
       for (int w = 0; w < wave; ++w) pos += cnt[w][d];
       keys_out[pos] = key;
       vals_out[pos] = val;
+      if (V2) vals2_out[pos] = val2;
     }
     __syncthreads();
     // only the digits of this round are touched: every wave's leader adds its count to the
@@ -295,12 +298,13 @@ __global__ void __launch_bounds__(256) radix_scatter_kernel(
 // per-digit exclusive prefix), then the tile is written out in that order, so consecutive
 // threads store consecutive positions of one digit's run (runs of ~tile/2^BITS keys) instead of
 // one scattered 4-byte store per key.
-template <int BITS>
+template <int BITS, bool V2 = false>
 __global__ void __launch_bounds__(256) radix_scatter_lds_kernel(
     const int32_t* __restrict__ keys, const int32_t* __restrict__ vals, int64_t n, int shift,
     int items, int64_t nblocks, const uint32_t* __restrict__ offs,
     const uint32_t* __restrict__ hist, int32_t* __restrict__ keys_out,
-    int32_t* __restrict__ vals_out) {
+    int32_t* __restrict__ vals_out, const int32_t* __restrict__ vals2 = nullptr,
+    int32_t* __restrict__ vals2_out = nullptr) {
   constexpr int R = 1 << BITS, PER = R / 256;
   __shared__ uint32_t gbase[R];    // the digit's first global position for this block
   __shared__ uint32_t lstart[R];   // the digit's first position within the tile
@@ -308,6 +312,7 @@ __global__ void __launch_bounds__(256) radix_scatter_lds_kernel(
   __shared__ uint32_t cnt[4][R];
   __shared__ int32_t tk[kMaxSortItems * 256];
   __shared__ int32_t tv[kMaxSortItems * 256];
+  __shared__ int32_t tv2[V2 ? kMaxSortItems * 256 : 1];   // a second carried value (V2)
   __shared__ uint32_t wsum[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // this block's digit counts -> exclusive prefix over the digits (PER consecutive per thread)
@@ -345,6 +350,7 @@ __global__ void __launch_bounds__(256) radix_scatter_lds_kernel(
     const bool valid = idx < n;
     const int32_t key = valid ? keys[idx] : 0;
     const int32_t val = valid ? (vals ? vals[idx] : (int32_t)idx) : 0;
+    const int32_t val2 = (V2 && valid) ? vals2[idx] : 0;
     const int d = (key >> shift) & (R - 1);
     uint64_t peers = __ballot(valid);
 #pragma unroll
@@ -362,6 +368,7 @@ __global__ void __launch_bounds__(256) radix_scatter_lds_kernel(
       for (int w = 0; w < wave; ++w) pos += cnt[w][d];
       tk[pos] = key;
       tv[pos] = val;
+      if (V2) tv2[pos] = val2;
     }
     __syncthreads();
     if (lead) {
@@ -377,6 +384,7 @@ __global__ void __launch_bounds__(256) radix_scatter_lds_kernel(
     const uint32_t gpos = gbase[d] + ((uint32_t)j - lstart[d]);
     keys_out[gpos] = key;
     vals_out[gpos] = tv[j];
+    if (V2) vals2_out[gpos] = tv2[j];
   }
 }
 
@@ -408,6 +416,7 @@ struct SortWs {
   uint32_t* offs;
   int32_t* tk;
   int32_t* tv;
+  int32_t* tv2;
   void* scan_tmp;
   size_t scan_bytes;
 };
@@ -425,13 +434,13 @@ inline int64_t hist_entries(int64_t n, unsigned bits) {
   return nb * (wide_pass(bits, n) ? (1 << kWideBits) : kRadix);
 }
 
-size_t sort_bytes(int64_t n, unsigned bits) {  // keys in [0, 2^bits)
+size_t sort_bytes(int64_t n, unsigned bits, bool v2 = false) {  // keys in [0, 2^bits)
   const int64_t m = hist_entries(n, bits);
-  return 2 * align256(sizeof(uint32_t) * m) + 2 * align256(sizeof(int32_t) * (n > 0 ? n : 1)) +
+  return 2 * align256(sizeof(uint32_t) * m) + (v2 ? 3 : 2) * align256(sizeof(int32_t) * (n > 0 ? n : 1)) +
          align256(radix_scan_bytes(m)) + 256;
 }
 
-SortWs carve_sort(void* ws, int64_t n, unsigned bits) {
+SortWs carve_sort(void* ws, int64_t n, unsigned bits, bool v2 = false) {
   const int64_t m = hist_entries(n, bits);
   char* p = (char*)ws;
   SortWs w;
@@ -439,6 +448,8 @@ SortWs carve_sort(void* ws, int64_t n, unsigned bits) {
   w.offs = (uint32_t*)p; p += align256(sizeof(uint32_t) * m);
   w.tk = (int32_t*)p; p += align256(sizeof(int32_t) * (n > 0 ? n : 1));
   w.tv = (int32_t*)p; p += align256(sizeof(int32_t) * (n > 0 ? n : 1));
+  w.tv2 = nullptr;
+  if (v2) { w.tv2 = (int32_t*)p; p += align256(sizeof(int32_t) * (n > 0 ? n : 1)); }
   w.scan_tmp = p;
   w.scan_bytes = radix_scan_bytes(m);
   return w;
@@ -447,21 +458,27 @@ SortWs carve_sort(void* ws, int64_t n, unsigned bits) {
 // keys_in -> (keys_out, vals_out) sorted stably by key; vals_in NULL = the identity (input
 // positions). Passes alternate between the output and the workspace pair so the last one lands
 // in the output.
+// vals2_in / vals2_out (nullable): a second value carried along (the graph build's source ids,
+// so the CSR's col needs no gather through perm afterwards).
 int sort_pairs(const int32_t* keys_in, const int32_t* vals_in, int32_t* keys_out,
-               int32_t* vals_out, int64_t n, unsigned bits, void* ws, hipStream_t stream) {
+               int32_t* vals_out, int64_t n, unsigned bits, void* ws, hipStream_t stream,
+               const int32_t* vals2_in = nullptr, int32_t* vals2_out = nullptr) {
   if (n <= 0) return 0;
   GATX_REQUIRE(n < (1ll << 31), "sort: too many keys");
-  const SortWs w = carve_sort(ws, n, bits);
+  const bool v2 = vals2_in != nullptr;
+  const SortWs w = carve_sort(ws, n, bits, v2);
   const bool wide = wide_pass(bits, n);
   const int items = pass_items(bits, n);
   const int64_t nb = ceil_div(n, 256 * items), m = hist_entries(n, bits);
   const int passes = wide ? 1 : (int)ceil_div((int64_t)(bits > 0 ? bits : 1), kRadixBits);
   const int32_t* ck = keys_in;
   const int32_t* cv = vals_in;
+  const int32_t* cv2 = vals2_in;
   for (int ps = 0; ps < passes; ++ps) {
     const bool to_out = ((passes - 1 - ps) % 2) == 0;
     int32_t* ok = to_out ? keys_out : w.tk;
     int32_t* ov = to_out ? vals_out : w.tv;
+    int32_t* ov2 = v2 ? (to_out ? vals2_out : w.tv2) : nullptr;
     const int shift = ps * kRadixBits;
     if (wide) radix_hist_kernel<kWideBits><<<(unsigned)nb, 256, 0, stream>>>(ck, n, 0, items, nb, w.hist);
     else radix_hist_kernel<kRadixBits><<<(unsigned)nb, 256, 0, stream>>>(ck, n, shift, items, nb, w.hist);
@@ -474,7 +491,16 @@ int sort_pairs(const int32_t* keys_in, const int32_t* vals_in, int32_t* keys_out
       const char* e = getenv("GATX_RADIX_LDS");
       return !(e && strcmp(e, "0") == 0);
     }();
-    if (lds_tiles && wide)
+    if (v2 && wide)   // (the wide LDS tile has no room for a second value)
+      radix_scatter_kernel<kWideBits, true><<<(unsigned)nb, 256, 0, stream>>>(
+          ck, cv, n, 0, items, nb, w.offs, ok, ov, cv2, ov2);
+    else if (v2 && lds_tiles)
+      radix_scatter_lds_kernel<kRadixBits, true><<<(unsigned)nb, 256, 0, stream>>>(
+          ck, cv, n, shift, items, nb, w.offs, w.hist, ok, ov, cv2, ov2);
+    else if (v2)
+      radix_scatter_kernel<kRadixBits, true><<<(unsigned)nb, 256, 0, stream>>>(
+          ck, cv, n, shift, items, nb, w.offs, ok, ov, cv2, ov2);
+    else if (lds_tiles && wide)
       radix_scatter_lds_kernel<kWideBits><<<(unsigned)nb, 256, 0, stream>>>(
           ck, cv, n, 0, items, nb, w.offs, w.hist, ok, ov);
     else if (lds_tiles)
@@ -489,6 +515,7 @@ int sort_pairs(const int32_t* keys_in, const int32_t* vals_in, int32_t* keys_out
     GATX_LAUNCH_CHECK("radix_scatter");
     ck = ok;
     cv = ov;
+    cv2 = ov2;
   }
   return 0;
 }
@@ -523,9 +550,9 @@ int graph_build_impl(const void* ei, int64_t E, int64_t ld, int add_loops, int64
     GATX_LAUNCH_CHECK("compact");
   }
   if (E_bound > 0) {
-    GATX_CALL(sort_pairs(dst32, iota, rowidx, perm, E_bound, bits_for(N + 1), tmp, stream));
-    gather_kernel<<<grid_for(E_bound), 256, 0, stream>>>(src32, perm, E_bound, col);
-    GATX_LAUNCH_CHECK("gather col");
+    // src ids ride along as a second value: col comes out of the sort (no gather through perm)
+    GATX_CALL(sort_pairs(dst32, iota, rowidx, perm, E_bound, bits_for(N + 1), tmp, stream, src32,
+                         col));
   }
   rowptr_kernel<<<grid_for(E_bound + 1), 256, 0, stream>>>(rowidx, E_bound, N, rowptr);
   GATX_LAUNCH_CHECK("rowptr");
@@ -582,7 +609,7 @@ extern "C" int gatx_graph_meta(const void* edge_index, int is64, int64_t E, int6
 extern "C" size_t gatx_graph_build_workspace_bytes(int64_t E, int64_t E_bound, int64_t N) {
   size_t b = align256(sizeof(int32_t) * (E > 0 ? E : 1)) +
              3 * align256(sizeof(int32_t) * (E_bound > 0 ? E_bound : 1));
-  size_t t = std::max(scan_bytes(E), sort_bytes(E_bound, bits_for(N + 1)));
+  size_t t = std::max(scan_bytes(E), sort_bytes(E_bound, bits_for(N + 1), true));
   return b + align256(t) + 256;
 }
 
