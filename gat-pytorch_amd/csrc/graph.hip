@@ -170,13 +170,6 @@ __global__ void __launch_bounds__(256) rowptr_kernel(const int32_t* keys, int64_
   }
 }
 
-__global__ void __launch_bounds__(256) gather_kernel(const int32_t* src, const int32_t* idx,
-                                                      int64_t n, int32_t* out) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x)
-    out[i] = src[idx[i]];
-}
-
 __global__ void __launch_bounds__(256) iota_kernel(int64_t n, int32_t* out) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -632,8 +625,8 @@ extern "C" int gatx_graph_build(const void* edge_index, int is64, int64_t E, int
 }
 
 extern "C" size_t gatx_graph_transpose_workspace_bytes(int64_t E_bound, int64_t N) {
-  return 2 * align256(sizeof(int32_t) * (E_bound > 0 ? E_bound : 1)) +
-         align256(sort_bytes(E_bound, bits_for(N + 1))) + 256;
+  return 3 * align256(sizeof(int32_t) * (E_bound > 0 ? E_bound : 1)) +
+         align256(sort_bytes(E_bound, bits_for(N + 1), true)) + 256;
 }
 
 extern "C" int gatx_graph_transpose(const int32_t* col, const int32_t* rowidx, int64_t N,
@@ -644,21 +637,19 @@ extern "C" int gatx_graph_transpose(const int32_t* col, const int32_t* rowidx, i
   char* p = (char*)ws;
   int32_t* iota = (int32_t*)p;  p += align256(sizeof(int32_t) * (E_bound > 0 ? E_bound : 1));
   int32_t* keys = (int32_t*)p;  p += align256(sizeof(int32_t) * (E_bound > 0 ? E_bound : 1));
+  int32_t* skeys = (int32_t*)p; p += align256(sizeof(int32_t) * (E_bound > 0 ? E_bound : 1));
   size_t used = (size_t)(p - (char*)ws);
   GATX_REQUIRE(used <= ws_bytes, "graph_transpose: workspace too small");
-  int32_t* skeys = scol;   // sorted keys land in scol first, then scol is gathered over them
   if (E_bound > 0) {
     tkeys_kernel<<<grid_for(E_bound), 256, 0, stream>>>(col, (const long long*)e2, E_bound, N,
                                                         keys, iota);
     GATX_LAUNCH_CHECK("tkeys");
-    GATX_CALL(sort_pairs(keys, iota, skeys, seid, E_bound, bits_for(N + 1), (void*)p, stream));
+    // each slot's destination rides through the sort as a second value: scol comes out sorted
+    GATX_CALL(sort_pairs(keys, iota, skeys, seid, E_bound, bits_for(N + 1), (void*)p, stream,
+                         rowidx, scol));
   }
   rowptr_kernel<<<grid_for(E_bound + 1), 256, 0, stream>>>(skeys, E_bound, N, srowptr);
   GATX_LAUNCH_CHECK("srowptr");
-  if (E_bound > 0) {
-    gather_kernel<<<grid_for(E_bound), 256, 0, stream>>>(rowidx, seid, E_bound, scol);
-    GATX_LAUNCH_CHECK("gather scol");
-  }
   return 0;
 }
 
