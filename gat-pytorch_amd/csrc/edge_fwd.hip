@@ -825,13 +825,39 @@ __global__ void __launch_bounds__(256) attention_alpha_ei_kernel(
         sv[u] = (int64_t)ei[p];
         dv[u] = (int64_t)ei[ld + p];
       }
+      // score and denominator rows as float4 / float2 loads (rows of 2NH / NH floats: aligned
+      // whenever NH is a multiple of the vector width; torch's allocations are 256-B aligned)
       float a[UE][NHA], dn[UE][NHA];
 #pragma unroll
       for (int u = 0; u < UE; ++u)
 #pragma unroll
-        for (int h = 0; h < NHC; ++h) {
-          a[u][h] = const_att ? 0.f : S[sv[u] * S2 + h] + S[dv[u] * S2 + NHC + h];
-          dn[u][h] = den[dv[u] * NHC + h];
+        for (int h = 0; h < NHC; h += VEC) {
+          const float* ps = S + sv[u] * S2 + h;
+          const float* pd = S + dv[u] * S2 + NHC + h;
+          const float* pn = den + dv[u] * NHC + h;
+          if constexpr (VEC == 4) {
+            const float4 z = *(const float4*)pn;
+            dn[u][h] = z.x; dn[u][h + 1] = z.y; dn[u][h + 2] = z.z; dn[u][h + 3] = z.w;
+            if (!const_att) {
+              const float4 x = *(const float4*)ps, y = *(const float4*)pd;
+              a[u][h] = x.x + y.x; a[u][h + 1] = x.y + y.y;
+              a[u][h + 2] = x.z + y.z; a[u][h + 3] = x.w + y.w;
+            } else {
+              a[u][h] = a[u][h + 1] = a[u][h + 2] = a[u][h + 3] = 0.f;
+            }
+          } else if constexpr (VEC == 2) {
+            const float2 z = *(const float2*)pn;
+            dn[u][h] = z.x; dn[u][h + 1] = z.y;
+            if (!const_att) {
+              const float2 x = *(const float2*)ps, y = *(const float2*)pd;
+              a[u][h] = x.x + y.x; a[u][h + 1] = x.y + y.y;
+            } else {
+              a[u][h] = a[u][h + 1] = 0.f;
+            }
+          } else {
+            dn[u][h] = *pn;
+            a[u][h] = const_att ? 0.f : *ps + *pd;
+          }
         }
 #pragma unroll
       for (int u = 0; u < UE; ++u) {
@@ -1042,8 +1068,11 @@ extern "C" int gatx_attention_alpha_ei(const void* edge_index, int is64, int64_t
         (const I*)edge_index, ld, E2, e2p, S, M_ord, den, NH, rowptr, perm, alpha,             \
         (long long*)argmax);                                                                   \
   } while (0)
+  // the head-count variants load score / den rows and store alpha rows as vectors
+  const bool al = ((uintptr_t)S % 16) == 0 && ((uintptr_t)den % 16) == 0 &&
+                  ((uintptr_t)alpha % 16) == 0;
 #define GATX_AEI(I)                                                                            \
-  switch (NH) {                                                                                \
+  switch (al ? NH : 0) {                                                                       \
     case 1: GATX_AE(1, I); break; case 2: GATX_AE(2, I); break; case 4: GATX_AE(4, I); break;  \
     case 6: GATX_AE(6, I); break; case 8: GATX_AE(8, I); break; default: GATX_AE(0, I); break; \
   }
