@@ -5,6 +5,10 @@
                     [--wiring gatx|reference]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
+`bench.py --gpus N` with N > 1 started as a single process starts the N ranks itself (children
+under torch.distributed.run, before any GPU call here) and relays rank 0's line; under
+torch.distributed.run (WORLD_SIZE set) each process is one rank and WORLD_SIZE must equal N.
+
 Workload: per rank a synthetic PPI-shaped batch of G graphs (2245 nodes and 61318
 uniformly random directed edges per graph; x ~ N(0,1), 50 features), the reference PPI config
 (`run_config.py:18-33`: 3 layers, 4/4/6 heads, 256/256/121 features, concat/concat/mean, skip on
@@ -43,6 +47,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "gat-pytorch_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -79,10 +84,15 @@ def run_timed(step, steps, world, dev, instr_step=None):
     bracketed), so instrumenting every step would inflate the headline by 3-6%; this way the
     kernel timings are live, inside the timed region, at < 1% cost to it. With a captured
     hipGraph `step`, the instrumented steps run `instr_step` (the same step, eagerly): events
-    bracket individual launches, which a graph replay does not expose."""
+    bracket individual launches, which a graph replay does not expose.
+    The region is bracketed by two gatx_region_mark dispatches (the first carries `steps` in its
+    grid size) enqueued outside the clock, so a rocprofv3 counter pass can cut exactly these
+    steps' dispatches out of its trace (tools/pmc_summary.py)."""
+    from gatx import _lib
     from gatx.functional import KernelTimer, set_kernel_timer
     n_instr = max(1, steps // 10)
     timer = KernelTimer()
+    _lib.call("gatx_region_mark", steps, _lib.stream())
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -98,12 +108,14 @@ def run_timed(step, steps, world, dev, instr_step=None):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     set_kernel_timer(None)
+    _lib.call("gatx_region_mark", 1, _lib.stream())
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64,
                          device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     return elapsed, timer.summary(), n_instr
+
 
 def layer_dims(cfg):
     heads = [1] + cfg["num_heads_per_layer"]
@@ -167,33 +179,51 @@ def layer_dataflow(N, E2, F_in, NH, F, concat, resid):
     return out
 
 
+def edge_pricer(dims, flows):
+    """edge_bytes(i, info) for roofline_objects: the compulsory bytes of the i-th edge_forward
+    record of a step. Records come in layer order, one per layer (a head-mean layer's head-group
+    launches share one record), so the layer is i mod the layer count; the record's head count
+    must match that layer's."""
+    def price(i, info):
+        li = i % len(dims)
+        if info[2] != dims[li][1]:
+            raise KeyError(f"edge record {i} {info} does not match layer {li} {dims[li]}")
+        return [bb for k, bb, _ in flows[li] if k == "edge_forward"][0]
+    return price
+
+
 def graph_build_bytes(E, E2, N):
     """Compulsory bytes of the per-step graph preprocessing: read edge_index (int64), write
     edge_index' (int64) and the int32 CSR (col, rowidx, perm, rowptr)."""
     return 16 * E + 16 * E2 + 12 * E2 + 4 * (N + 1)
 
 
-def pmc_step_bytes(pm_path, step_ms):
-    """L2->fabric bytes per step measured by rocprofv3 (FETCH_SIZE x 2 + WRITE_SIZE, the
-    MI355X_MICROARCH.md gfx950 correction; Infinity-Cache hits are included, so this bounds HBM
-    traffic from above), summed over the kernels of the profiled steps (kernels launched at least
-    once per step; one-off setup kernels excluded)."""
+def load_pmc(pm_path):
+    """A committed tools/pmc_summary.py summary, or None (missing, or written before the
+    region-marked window existed: such a summary cannot tell step kernels from setup kernels)."""
     if not os.path.exists(pm_path):
         return None
     pm = json.load(open(pm_path))
-    steps = pm.get("steps", 4)
-    tot = 0.0
-    for v in pm["kernels"].values():
-        if v["launches"] >= steps:
-            tot += (v["hbm_read_bytes"] + v["hbm_write_bytes"]) * v["launches"]
-    per_step = tot / steps
+    return pm if "window" in pm else None
+
+
+def pmc_step_bytes(pm, step_ms, pm_path=""):
+    """Fabric bytes per step measured by rocprofv3 (FETCH_SIZE x 2 + WRITE_SIZE, the
+    MI355X_MICROARCH.md gfx950 correction; Infinity-Cache hits are included, so this bounds HBM
+    traffic from above): every dispatch between bench.py's two region marks, over the step count
+    the first mark carries (tools/pmc_summary.py)."""
+    if pm is None:
+        return None
+    from pmc_summary import step_bytes
+    per_step = step_bytes(pm)
     gbs = per_step / (step_ms * 1e-3) / 1e9
     return {"bytes_per_step": per_step, "GBps": round(gbs, 1),
-            "frac_of_peak": round(gbs / HBM_PEAK_GBS, 4),
+            "frac_of_peak": round(gbs / HBM_PEAK_GBS, 4), "steps_in_window": pm["steps"],
             "source": f"{os.path.relpath(pm_path, ROOT)} ({pm.get('source', '')}); step time of "
                       "this run",
-            "note": "rocprofv3 FETCH_SIZE x2 + WRITE_SIZE (gfx950 correction); counts "
-                    "Infinity-Cache hits, so an upper bound on HBM bytes"}
+            "note": "rocprofv3 FETCH_SIZE x2 + WRITE_SIZE (gfx950 correction) of the dispatches "
+                    "between the timed region's marks; counts Infinity-Cache hits, so an upper "
+                    "bound on HBM bytes"}
 
 
 def available_cores():
@@ -286,11 +316,14 @@ def kernel_summary(summ, n_instr):
     return kern
 
 
-def roofline_objects(summ, unique_edge_bytes, pmc_path):
+def roofline_objects(summ, edge_bytes, pm, n_instr, pm_path=""):
     """The two roofline objects (projection GEMM: MFMA-bound; edge pass: HBM-bound), each priced
     per launch from the live HIP-event durations, the GEMM by its flops, the edge pass by its
-    compulsory bytes (layer_dataflow). `traffic` = the PMC-measured
-    L2->fabric bytes per launch of the same kernel when a summary is committed."""
+    compulsory bytes: edge_bytes(i, info) prices the i-th edge_forward record of a step (records
+    come in layer order, one per layer; layer_dataflow). `traffic` = the PMC-measured fabric bytes
+    per step of the same kernel(s) (tools/pmc_summary.py window) divided by the records one step
+    makes, i.e. per record like `achieved` (a head-mean layer's head groups are several launches
+    inside one record)."""
     roofs = {}
     gem = summ.get("gemm", [])
     if gem:
@@ -302,35 +335,37 @@ def roofline_objects(summ, unique_edge_bytes, pmc_path):
                          "achieved": round(tfs, 2), "peak": round(gr["peak"], 1),
                          "unit": "TFLOP/s", "frac": round(tfs / gr["peak"], 4), "traffic": None,
                          "gemm_mode": gr["mode"], "flops_per_launch": fl / len(gem),
-                         "avg_launch_ms": ms_ / len(gem), "_prefix": gr["prefix"], "_ms": ms_}
+                         "avg_launch_ms": ms_ / len(gem), "_prefix": gr["prefix"], "_ms": ms_,
+                         "_per_step": len(gem) / n_instr}
     edg = summ.get("edge_forward", [])
     if edg:
-        by = sum(unique_edge_bytes(info) for info, _ in edg)
+        by = [edge_bytes(i, info) for i, (info, _) in enumerate(edg)]
         ms_ = sum(t for _, t in edg)
-        gbs = by / (ms_ * 1e-3) / 1e9
+        gbs = sum(by) / (ms_ * 1e-3) / 1e9
         roofs["edge_forward"] = {"bound": "hbm", "kernel": "edge_forward_kernel<*> (all layers)",
                                  "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                  "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
-                                 "bytes_per_launch": by / len(edg),
+                                 "bytes_per_launch": sum(by) / len(edg),
+                                 "bytes_per_layer": by[:len(edg) // n_instr],
                                  "bytes_basis": "compulsory bytes: gathered rows once per node when "
                                                 "the gathered matrix fits the 256 MB MALL, else "
                                                 "once per edge; CSR, scores, den, output (+ "
                                                 "residual) once",
                                  "avg_launch_ms": ms_ / len(edg),
-                                 "_prefix": "edge_forward_kernel", "_ms": ms_}
-    if os.path.exists(pmc_path):
-        pm = json.load(open(pmc_path))
+                                 "_prefix": "edge_forward_kernel", "_ms": ms_,
+                                 "_per_step": len(edg) / n_instr}
+    if pm is not None:
+        from pmc_summary import prefix_bytes_per_step
         for r in roofs.values():
-            ks = [v for k, v in pm["kernels"].items() if k.startswith(r["_prefix"])]
-            if ks:
-                n = sum(v["launches"] for v in ks)
-                r["traffic"] = sum((v["hbm_read_bytes"] + v["hbm_write_bytes"]) * v["launches"]
-                                   for v in ks) / n
-                r["traffic_source"] = f"{os.path.relpath(pmc_path, ROOT)} ({pm.get('source', '')})"
+            b = prefix_bytes_per_step(pm, r["_prefix"])
+            if b > 0:
+                r["traffic"] = b / r["_per_step"]
+                r["traffic_source"] = (f"{os.path.relpath(pm_path, ROOT) if pm_path else ''} "
+                                       f"({pm.get('source', '')})")
     ordered = sorted(roofs.values(), key=lambda r: -r["_ms"])
     for r in ordered:
-        r.pop("_prefix")
-        r.pop("_ms")
+        for k in ("_prefix", "_ms", "_per_step"):
+            r.pop(k)
     return ordered
 
 
@@ -368,8 +403,9 @@ def run_rmat(args, world, rank, dev):
         + graph_build_bytes(E, E2, N) / (HBM_PEAK_GBS * 1e9)
     b_gemm, _, b_edge = survey_bytes(N, E2, FIN, NH, F, True)
     edge_b = [b for k, b, _ in flow if k == "edge_forward"][0]
-    roofs = roofline_objects(summ, lambda info: edge_b, os.path.join(ROOT, "profiles",
-                                                                    "pmc_rmat.json"))
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_rmat.json")
+    pm = load_pmc(pmc_path)
+    roofs = roofline_objects(summ, lambda i, info: edge_b, pm, n_instr, pmc_path)
     result = {
         "metric": "GAT-layer edges/sec + achieved HBM GB/s, RMAT 1-layer fwd",
         "value": round(E2 * world / step_s, 1), "unit": "layer-edges/s",
@@ -385,8 +421,7 @@ def run_rmat(args, world, rank, dev):
         "unique_GBps": round(uniq / step_s / 1e9, 1),
         "roofline_time_frac": round(t_roof / step_s, 4),
         "l2_gather_GBps": round((b_gemm + b_edge) / step_s / 1e9, 1),
-        "hbm_measured": pmc_step_bytes(os.path.join(ROOT, "profiles", "pmc_rmat.json"),
-                                       step_s * 1e3),
+        "hbm_measured": pmc_step_bytes(pm, step_s * 1e3, pmc_path),
         "roofline": roofs[0] if roofs else None,
         "roofline_other": roofs[1] if len(roofs) > 1 else None,
         "kernels": kernel_summary(summ, n_instr),
@@ -396,6 +431,33 @@ def run_rmat(args, world, rank, dev):
                                                    layer.a.weight.detach().cpu().numpy(), NH, F)
     if rank == 0:
         print(json.dumps(result), flush=True)
+
+
+def launch_command(nproc: int, argv, port: int):
+    """The torch.distributed.run command that starts `nproc` ranks of this script with the same
+    arguments (one process per GPU, rendezvous on 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={nproc}", "--master-addr=127.0.0.1", f"--master-port={port}",
+            os.path.abspath(__file__), *argv]
+
+
+def launch_ranks(nproc: int, argv) -> int:
+    """`bench.py --gpus N` started as ONE process (the driver's command form): start N fresh rank
+    processes under torch.distributed.run as children, before this process touches the GPU (no
+    exec: it would be forbidden after GPU init, and is not needed), relay their stdout (rank 0's
+    JSON line) and return their exit status (non-zero if any rank failed)."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    proc = subprocess.run(launch_command(nproc, argv, port), stdout=subprocess.PIPE, text=True)
+    sys.stdout.write(proc.stdout)
+    sys.stdout.flush()
+    if proc.returncode != 0:
+        print(f"bench.py: {nproc}-rank run failed with exit status {proc.returncode}",
+              file=sys.stderr)
+    return proc.returncode
 
 
 def main():
@@ -429,13 +491,21 @@ def main():
                          "steps, and PATTERN training on one GPU")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # one process per GPU over RCCL. Test-only overrides (exercise the multi-rank logic on a
     # one-GPU box): GATX_BENCH_BACKEND=gloo, GATX_BENCH_ONE_DEVICE=1 (every rank on cuda:0).
-    dev_idx = 0 if os.environ.get("GATX_BENCH_ONE_DEVICE") == "1" else local
+    one_device = os.environ.get("GATX_BENCH_ONE_DEVICE") == "1"
+    dev_idx = 0 if one_device else local
     backend = os.environ.get("GATX_BENCH_BACKEND", "nccl")
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if not one_device and torch.cuda.device_count() < world:
+        raise SystemExit(f"bench.py: {world} ranks need {world} visible GPUs, "
+                         f"{torch.cuda.device_count()} visible")
     if world > 1:
         torch.cuda.set_device(dev_idx)
         if backend == "nccl":
@@ -452,7 +522,7 @@ def main():
     from gatx import GATModel, clear_graph_cache
     from gatx import data as gd
     from gatx.config import data_config
-    from gatx.distributed import GradientAllReducer, count_weight
+    from gatx.distributed import GradientAllReducer, count_weights
 
     ds = {"pattern": "PATTERN", "ppi": "PPI", "cora": "Cora", "citeseer": "Citeseer",
           "pubmed": "Pubmed"}[args.workload]
@@ -503,12 +573,21 @@ def main():
         loss_fn = torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([1 / 0.1765], device=dev))
         y = y[:, 0]
     reducer = None
-    w_loss = 1.0
+    w_main = w_norm = 1.0
     if args.mode == "train" and world > 1:
         # DDP-style: buckets all-reduced (SUM) over RCCL as backward produces them; each rank's
-        # mean loss weighted by its share of the union batch's nodes
+        # mean loss terms weighted by its share of the union batch's counts:
+        # nodes (labelled rows for Planetoid) for the BCE / CE, edges E' for the attention norm
+        # (a per-edge mean). Counted once here, outside the timed / captured step.
+        from gatx.graph import graph_cache as _gc
+        e_local = _gc.get(ei, b.num_nodes, True).num_edges
+        n_local = int(train_mask.sum()) if planetoid else b.num_nodes
         reducer = GradientAllReducer(model.parameters(), average=False)
-        w_loss = count_weight(b.num_nodes, device=dev if backend == "nccl" else "cpu")
+        w_main, w_norm = count_weights([n_local, e_local],
+                                       device=dev if backend == "nccl" else "cpu")
+
+    def _w(t, w):   # no extra launch for the single-rank weight 1
+        return t if w == 1.0 else t * w
 
     def step():
         if not args.cached_graph:
@@ -519,21 +598,21 @@ def main():
         opt.zero_grad(set_to_none=True)
         if ds == "PATTERN":   # PatternGAT.training_step (models/pattern_gat.py:18-25)
             out = model(x, ei).squeeze(-1)
-            loss = loss_fn(out, y)
+            loss = _w(loss_fn(out, y), w_main)
         elif planetoid:       # PlanetoidGAT.training_step (models/planetoid_gat.py:15-31)
             out, ei2, atts = model.forward_and_return_attention(x, ei)
             attention_norm = model.calc_attention_norm(ei2, atts)
-            loss = (loss_fn(out.index_select(0, train_idx), y_train)
-                    + args.attention_reward * attention_norm)
+            loss = (_w(loss_fn(out.index_select(0, train_idx), y_train), w_main)
+                    + args.attention_reward * w_norm * attention_norm)
         else:
             # PPI_GAT.training_step (models/ppi_gat.py:15-33): BCE + the attention norm, computed
             # every step (logged; added to the loss only with a non-zero attention_penalty)
             out, ei2, atts = model.forward_and_return_attention(x, ei)
-            loss = loss_fn(out, y)
+            loss = _w(loss_fn(out, y), w_main)
             attention_norm = model.calc_attention_norm(ei2, atts)
             if args.attention_penalty != 0.0:
-                loss = loss + args.attention_penalty * attention_norm
-        (loss * w_loss if w_loss != 1.0 else loss).backward()
+                loss = loss + args.attention_penalty * w_norm * attention_norm
+        loss.backward()
         if reducer is not None:
             reducer.finish()
         opt.step()
@@ -570,16 +649,12 @@ def main():
     surv = [survey_bytes(N, E2, fin, nh, f, cc) for (fin, nh, f, cc) in dims]
     l2_gather = sum(bg + be for bg, _, be in surv)
 
-    def edge_unique(info):
-        n, e2, nh, f, mode = info
-        for (fin, nh_, f_, cc), fl in zip(dims, flows):
-            if nh_ == nh and (f_ == f or (mode == "x" and _r4(fin) == f)):
-                return [bb for k, bb, _ in fl if k == "edge_forward"][0]
-        raise KeyError(info)
+    edge_unique = edge_pricer(dims, flows)
     pmc_path = os.path.join(ROOT, "profiles",
                             "pmc_latest.json" if (ds == "PPI" and args.mode == "fwd"
                                                   and args.graphs == 20) else "_none_")
-    ordered = roofline_objects(summ, edge_unique, pmc_path)
+    pm = load_pmc(pmc_path)
+    ordered = roofline_objects(summ, edge_unique, pm, n_instr, pmc_path)
 
     result = {
         "metric": f"GAT-layer edges/sec + achieved HBM GB/s, {ds} {len(dims)}-layer fwd"
@@ -603,11 +678,14 @@ def main():
                               if args.wiring == "gatx" else
                               "reference GATModel.forward around gatx GATLayers (drop-in)")},
         "unique_GBps": round(uniq / step_s / 1e9, 1),
-        "roofline_time_frac": round(t_roof / step_s, 4),
-        "roofline_time_basis": "sum over the forward's kernels of max(unique bytes / 8 TB/s, "
-                               "flops / GEMM peak) + graph build bytes / 8 TB/s, over step time",
+        # forward dataflow only: not defined for a train step (its backward is not priced)
+        "roofline_time_frac": round(t_roof / step_s, 4) if args.mode == "fwd" else None,
+        "roofline_time_basis": ("sum over the forward's kernels of max(unique bytes / 8 TB/s, "
+                                "flops / GEMM peak) + graph build bytes / 8 TB/s, over step time"
+                                if args.mode == "fwd" else "omitted: only the forward dataflow "
+                                "is priced"),
         "l2_gather_GBps": round(l2_gather / step_s / 1e9, 1),
-        "hbm_measured": pmc_step_bytes(pmc_path, ms) if args.mode == "fwd" else None,
+        "hbm_measured": pmc_step_bytes(pm, ms, pmc_path) if args.mode == "fwd" else None,
         "roofline": ordered[0] if ordered else None,
         "roofline_other": ordered[1] if len(ordered) > 1 else None,
         "kernels": kernel_summary(summ, n_instr),

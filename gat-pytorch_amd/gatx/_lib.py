@@ -28,6 +28,7 @@ P = ctypes.c_void_p
 SIGNATURES = {
     "gatx_last_error": (ctypes.c_char_p, []),
     "gatx_version": (c_i, []),
+    "gatx_region_mark": (c_i, [ctypes.c_uint32, P]),
     "gatx_graph_meta_workspace_bytes": (c_sz, []),
     "gatx_graph_meta": (c_i, [P, c_i, c_i64, c_i64, c_i, c_i64, P, P, P]),
     "gatx_graph_build_workspace_bytes": (c_sz, [c_i64, c_i64, c_i64]),

@@ -21,6 +21,7 @@ loop built on it.
 """
 from __future__ import annotations
 
+import contextlib
 from typing import Iterable, List, Sequence
 
 import torch
@@ -53,11 +54,18 @@ def collate_graphs(graphs: Sequence[tuple]):
 class DeviceGraphLoader:
     """Per-rank batches of whole graphs, resident on the device: each epoch shuffles the graph ids
     with a seed shared by every rank (DistributedSampler semantics: same permutation everywhere,
-    rank r takes every world-th id), then collates `batch_size` graphs at a time on the device.
-    `graphs` is a list of (x, edge_index, y) already on the device."""
+    the id list padded by wrapping around to a multiple of `world` — or truncated to one with
+    drop_last — then rank r takes every world-th id), and collates `batch_size` graphs at a time
+    on the device. Every rank therefore yields the same number of batches, so every rank issues
+    the same collectives per epoch. `graphs` is a list of (x, edge_index, y) already on the
+    device."""
 
     def __init__(self, graphs, batch_size: int, rank: int = 0, world: int = 1,
                  shuffle: bool = True, seed: int = 0, drop_last: bool = False):
+        if not graphs:
+            raise ValueError("DeviceGraphLoader: no graphs")
+        if not 0 <= rank < world:
+            raise ValueError(f"DeviceGraphLoader: rank {rank} outside world {world}")
         self.graphs, self.batch_size = graphs, batch_size
         self.rank, self.world, self.shuffle, self.seed = rank, world, shuffle, seed
         self.drop_last = drop_last
@@ -73,7 +81,12 @@ class DeviceGraphLoader:
             order = torch.randperm(n, generator=g).tolist()
         else:
             order = list(range(n))
-        return [order[i] for i in shard_graphs(n, self.rank, self.world)]
+        if self.drop_last:
+            order = order[:n - n % self.world] if n >= self.world else order[:0]
+        else:   # wrap around (repeating as often as needed when n < world)
+            total = -(-n // self.world) * self.world
+            order = (order * (-(-total // n)))[:total]
+        return [order[i] for i in shard_graphs(len(order), self.rank, self.world)]
 
     def __iter__(self):
         ids = self._ids()
@@ -87,16 +100,29 @@ class DeviceGraphLoader:
         return n // self.batch_size if self.drop_last else -(-n // self.batch_size)
 
 
-def count_weight(n_local: int | float, group=None, device=None) -> float:
-    """n_local / sum over ranks of n_local: the factor that turns this rank's mean loss into its
-    share of the union batch's mean (SUM the gradients afterwards)."""
-    if not dist.is_initialized() or dist.get_world_size(group) == 1:
-        return 1.0
+def count_weights(counts, group=None, device=None, always_reduce: bool = False):
+    """[n_local / sum over ranks of n_local] for each count in `counts`, with ONE all-reduce of
+    the vector: the factors that turn this rank's mean loss terms into their shares of the union
+    batch's means (SUM the gradients afterwards). Weight each term by its own count — nodes (or
+    labelled rows) for BCE / cross-entropy, edges E' for calc_attention_norm (a per-edge mean,
+    `models/GATModel.py:224`) — and compute the weights once, outside a captured or timed step
+    (this blocks on the result). `always_reduce` runs the collective even at world size 1 (tests
+    exercising the RCCL path on a one-GPU box)."""
+    counts = [float(c) for c in counts]
+    if not dist.is_initialized() or (dist.get_world_size(group) == 1 and not always_reduce):
+        return [1.0] * len(counts)
     if device is None:
         device = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
-    t = torch.tensor([float(n_local)], dtype=torch.float64, device=device)
+    t = torch.tensor(counts, dtype=torch.float64, device=device)
     dist.all_reduce(t, group=group)
-    return float(n_local) / float(t.item())
+    tot = t.cpu().tolist()
+    return [c / s if s else 0.0 for c, s in zip(counts, tot)]
+
+
+def count_weight(n_local: int | float, group=None, device=None,
+                 always_reduce: bool = False) -> float:
+    """count_weights for a single loss term (a node-mean loss such as PatternGAT's BCE)."""
+    return count_weights([n_local], group, device, always_reduce)[0]
 
 
 def _all_reduce_flat(flat: torch.Tensor, group, async_op: bool):
@@ -156,11 +182,15 @@ class GradientAllReducer:
     produced one)."""
 
     def __init__(self, params: Iterable[torch.nn.Parameter], bucket_bytes: int = 4 << 20,
-                 group=None, average: bool = True):
+                 group=None, average: bool = True, always_reduce: bool = False):
         self.params = [p for p in params if p.requires_grad]
         self.group = group
         self.average = average
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        # always_reduce: hooks and collectives even at world size 1 (tests of the RCCL path on
+        # a one-GPU box; a one-rank all-reduce is the identity)
+        self.active = self.world > 1 or (always_reduce and dist.is_initialized())
+        self._sync = True
         self.buckets: List[dict] = []
         cur, size = [], 0
         for p in reversed(self.params):
@@ -177,7 +207,7 @@ class GradientAllReducer:
             for pi, p in enumerate(b["params"]):
                 self._slot[id(p)] = (bi, pi)
         self._hooks = []
-        if self.world > 1:
+        if self.active:
             for p in self.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
         self._reset()
@@ -201,9 +231,28 @@ class GradientAllReducer:
             b["flat"] = torch.zeros(b["numel"], dtype=like.dtype, device=like.device)
         return b["flat"]
 
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Gradient accumulation (DDP's no_sync): backward passes inside the context only
+        accumulate into .grad; the first backward after it reduces the accumulated gradients.
+        Call finish() once, after that backward."""
+        prev, self._sync = self._sync, False
+        try:
+            yield
+        finally:
+            self._sync = prev
+
     def _on_grad(self, p):
+        if not self._sync:
+            return
         bi, pi = self._slot[id(p)]
         b = self.buckets[bi]
+        if b["launched"]:
+            # a second backward before finish(): the bucket's all-reduce is already in flight
+            # (or done) on the old values; refilling its buffer would race with it and the new
+            # contribution would never be reduced
+            raise RuntimeError("GradientAllReducer: backward ran twice before finish(); use "
+                               "no_sync() for the accumulation steps")
         flat = self._flat(b, p.grad)
         o = b["offsets"][pi]
         flat[o:o + p.numel()].copy_(p.grad.reshape(-1))
@@ -216,7 +265,7 @@ class GradientAllReducer:
 
     def finish(self):
         """Wait for every bucket's all-reduce and write the results into .grad."""
-        if self.world == 1:
+        if not self.active:
             return
         dev = next((p.grad.device for p in self.params if p.grad is not None), None)
         for b in self.buckets:

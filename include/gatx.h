@@ -36,6 +36,11 @@ typedef struct ihipStream_t* gatx_stream_t; /* == hipStream_t */
 
 const char* gatx_last_error(void);
 int gatx_version(void);
+/* Profiling aid (not on the reference path): enqueue one empty dispatch of
+ * gatx_region_mark_kernel with `tag` (1..2^20) one-wave workgroups, so the trace's grid size
+ * carries the tag. bench.py brackets its timed steps with two of them (the first tagged with the
+ * step count), so a rocprofv3 counter pass can select exactly those steps' dispatches by id. */
+int gatx_region_mark(uint32_t tag, gatx_stream_t stream);
 
 /* ---------------------------------------------------------------- graph (models/utils.py) */
 

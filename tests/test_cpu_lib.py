@@ -58,7 +58,7 @@ def _ctype_of(decl: str):
     if "*" in decl or "gatx_stream_t" in t:
         return C.c_void_p
     return {"int": C.c_int, "int64_t": C.c_int64, "uint64_t": C.c_uint64, "float": C.c_float,
-            "size_t": C.c_size_t}[t.replace("const ", "").strip()]
+            "size_t": C.c_size_t, "uint32_t": C.c_uint32}[t.replace("const ", "").strip()]
 
 
 def test_ctypes_signatures_match_header_prototypes():
@@ -72,6 +72,18 @@ def test_ctypes_signatures_match_header_prototypes():
         assert len(got) == len(decls), (name, len(got), len(decls))
         for i, (d, g) in enumerate(zip(decls, got)):
             assert _ctype_of(d) is g, (name, i, d, g)
+
+
+def test_integration_example_matches_header():
+    """INTEGRATION.md's hand-written ctypes binding of gatx_edge_forward (what a maintainer would
+    copy into the reference) has the header's arity and parameter kinds."""
+    import ctypes as C
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    m = re.search(r"lib\.gatx_edge_forward\.argtypes = (.*?)\n(?!\s)", text, flags=re.S)
+    assert m, "INTEGRATION.md lost its gatx_edge_forward binding example"
+    got = eval(m.group(1).replace("\\\n", " "), {"ctypes": C})
+    want = [_ctype_of(d) for d in _declared_params()["gatx_edge_forward"]]
+    assert got == want
 
 
 def test_library_is_gfx950_code_object():

@@ -117,13 +117,130 @@ def test_overlapped_allreduce_equals_union_batch(bucket):
 
 
 def test_device_graph_loader_partitions_epoch():
+    """DistributedSampler semantics: 7 graphs over 3 ranks pad to 9 ids by wrapping around, so
+    every rank yields the same number of batches (same collectives per epoch) and every graph is
+    seen at least once."""
     from gatx.distributed import DeviceGraphLoader
     graphs = [(torch.full((2, 1), float(i)), torch.tensor([[0], [1]]), None) for i in range(7)]
-    seen = []
+    seen, lens, nbatches = [], [], []
     for r in range(3):
         ld = DeviceGraphLoader(graphs, batch_size=2, rank=r, world=3, seed=4)
         ld.set_epoch(1)
+        lens.append(len(ld))
+        k = 0
         for x, ei, _, offs in ld:
             seen += x[::2, 0].int().tolist()
             assert ei.shape[1] == len(offs) - 1
-    assert sorted(seen) == list(range(7))
+            k += 1
+        nbatches.append(k)
+    assert len(set(lens)) == 1 and lens == nbatches == [2, 2, 2]
+    assert sorted(set(seen)) == list(range(7)) and len(seen) == 9
+
+
+@pytest.mark.parametrize("n,world,bs", [(7, 3, 2), (2, 4, 1), (8, 3, 3), (5, 5, 2)])
+def test_device_graph_loader_equal_lengths(n, world, bs):
+    from gatx.distributed import DeviceGraphLoader
+    graphs = [(torch.full((1, 1), float(i)), torch.zeros((2, 0), dtype=torch.int64), None)
+              for i in range(n)]
+    for drop_last in (False, True):
+        lens = [len(DeviceGraphLoader(graphs, bs, r, world, drop_last=drop_last))
+                for r in range(world)]
+        assert len(set(lens)) == 1, (drop_last, lens)
+        got = [len(list(DeviceGraphLoader(graphs, bs, r, world, drop_last=drop_last)))
+               for r in range(world)]
+        assert got == lens
+        if drop_last:
+            ids = sorted(int(x[0, 0]) for r in range(world)
+                         for x, _, _, _ in DeviceGraphLoader(graphs, 1, r, world,
+                                                             drop_last=True))
+            assert len(ids) == len(set(ids)) == n - n % world
+
+
+def _accum_worker(rank, world, port, out):
+    """Gradient accumulation: two micro-batches under no_sync + a third outside it, one
+    finish(); and a second backward before finish() must raise (not silently mix gradients)."""
+    from gatx.distributed import GradientAllReducer, count_weights
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(5, 7), torch.nn.ELU(), torch.nn.Linear(7, 1))
+    reducer = GradientAllReducer(model.parameters(), bucket_bytes=64, average=False)
+    x, y = _union_data()
+    # rank r's micro-batches: rows r, r+world, ... cut into three
+    rows = list(range(rank, 13, world))
+    parts = [rows[0::3], rows[1::3], rows[2::3]]
+    w = count_weights([len(rows)])[0]
+    model.zero_grad(set_to_none=True)
+    for i, part in enumerate(parts):
+        loss = torch.nn.functional.binary_cross_entropy_with_logits(
+            model(x[part]).squeeze(-1), y[part], reduction="sum") / len(rows)
+        if i < 2:
+            with reducer.no_sync():
+                (loss * w).backward()
+        else:
+            (loss * w).backward()
+    reducer.finish()
+    out[rank] = torch.cat([p.grad.reshape(-1) for p in model.parameters()]).clone()
+    model(x[rows]).sum().backward()
+    try:
+        model(x[rows]).sum().backward()
+    except RuntimeError as e:
+        out[f"err{rank}"] = "twice before finish" in str(e)
+    else:
+        out[f"err{rank}"] = False
+    reducer.remove()
+    dist.destroy_process_group()
+
+
+def test_gradient_accumulation_no_sync_world3():
+    world = 3
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_accum_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(5, 7), torch.nn.ELU(), torch.nn.Linear(7, 1))
+    x, y = _union_data()
+    torch.nn.functional.binary_cross_entropy_with_logits(model(x).squeeze(-1), y).backward()
+    ref = torch.cat([p.grad.reshape(-1) for p in model.parameters()])
+    for r in range(world):
+        assert torch.allclose(out[r], ref, atol=1e-6), (r, (out[r] - ref).abs().max())
+        assert out[f"err{r}"], r
+
+
+def _two_term_worker(rank, world, port, out):
+    """Two mean terms over different counts (a node-mean BCE plus an edge-mean term, as
+    PPI_GAT's BCE + attention_penalty * calc_attention_norm): each weighted by its own count."""
+    from gatx.distributed import GradientAllReducer, count_weights
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(5, 7), torch.nn.ELU(), torch.nn.Linear(7, 1))
+    reducer = GradientAllReducer(model.parameters(), average=False)
+    x, y = _union_data()
+    rows = [list(range(0, 3)), list(range(3, 8)), list(range(8, 13))][rank]
+    edges = [list(range(0, 2)), list(range(2, 9)), list(range(9, 13))][rank]   # uneven, != rows
+    w_n, w_e = count_weights([len(rows), len(edges)])
+    bce = torch.nn.functional.binary_cross_entropy_with_logits(model(x[rows]).squeeze(-1), y[rows])
+    pen = model(x[edges]).abs().mean()
+    (bce * w_n + 0.3 * pen * w_e).backward()
+    reducer.finish()
+    out[rank] = torch.cat([p.grad.reshape(-1) for p in model.parameters()]).clone()
+    reducer.remove()
+    dist.destroy_process_group()
+
+
+def test_per_term_count_weights_world3():
+    world = 3
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_two_term_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(5, 7), torch.nn.ELU(), torch.nn.Linear(7, 1))
+    x, y = _union_data()
+    (torch.nn.functional.binary_cross_entropy_with_logits(model(x).squeeze(-1), y)
+     + 0.3 * model(x).abs().mean()).backward()
+    ref = torch.cat([p.grad.reshape(-1) for p in model.parameters()])
+    for r in range(world):
+        assert torch.allclose(out[r], ref, atol=1e-6), (r, (out[r] - ref).abs().max())

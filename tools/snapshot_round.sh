@@ -13,8 +13,8 @@ for p in fwd train rmat; do
   cp "$S/prof_$p/run_kernel_stats.csv" "$D/${p}_kernel_stats.csv"
   cp "$S/prof_$p/run_domain_stats.csv" "$D/${p}_domain_stats.csv" 2>/dev/null || true
 done
-PMC_STEPS=4 PMC_SOURCE="bench.py --steps 3 --warmup 1" \
+PMC_SOURCE="bench.py --steps 3 --warmup 1" \
   python tools/pmc_summary.py "$S/pmc" profiles/pmc_latest.json > "$D/fwd_pmc_summary.txt"
-PMC_STEPS=3 PMC_SOURCE="bench.py --workload rmat --steps 1 --warmup 2" \
+PMC_SOURCE="bench.py --workload rmat --steps 1 --warmup 2" \
   python tools/pmc_summary.py "$S/pmcr" profiles/pmc_rmat.json > "$D/rmat_pmc_summary.txt"
 echo "snapshot in $D"
