@@ -143,7 +143,34 @@ struct BwdArgs {
   int64_t row_stride4;     // dst pass: float4s per gathered row (Wh: Dp/4; x rows: Fin_p/4)
   int64_t head_stride4;    // float4s between heads in a gathered row (0: one row for all heads)
   int64_t gs_off;          // column of g_s_src in G_aug (g_s_dst at gs_off + NH)
+  // hub splitting (hub_T > 0): segments of more than hub_T edges are skipped by their own item
+  // and processed as pieces of hub_T edges (gatx_graph_hub_plan over this pass's CSR) by the
+  // waves of the first hub_blocks blocks (dispatched first, dealt over the XCDs), each leaving a
+  // partial in hub_part; follow-up kernels combine a hub's pieces in piece order.
+  int hub_T;
+  const int32_t* hubs;     // [hub_bound][4]: node, piece, pieces, first slot
+  const int32_t* hub_count;
+  int64_t hub_bound;
+  float* hub_part;         // dst: [2][hub_bound][NH]; src: [hub_bound][NH][Fp + 4]
+  int64_t hub_blocks;
 };
+
+// Work of one wave of a hub-split pass: a regular item (slot < 0) or one piece of a hub (slot =
+// its plan entry). Returns false when the wave has nothing to do.
+__device__ inline bool hub_piece(const BwdArgs& g, int wave, int64_t& n, int& h, int& beg,
+                                 int& end, int64_t& slot) {
+  const int64_t hi = (int64_t)blockIdx.x * 4 + wave;
+  h = (int)(hi / g.hub_bound);
+  const int64_t pc = hi - (int64_t)h * g.hub_bound;
+  if (h >= g.NH || pc >= uni(*g.hub_count)) return false;
+  const int32_t* hp = g.hubs + 4 * pc;
+  n = uni(hp[0]);
+  const int p = uni(hp[1]);
+  slot = pc;
+  beg = uni(g.rowptr[n]) + p * g.hub_T;
+  end = min(uni(g.rowptr[n + 1]), beg + g.hub_T);
+  return true;
+}
 
 // dst pass: one wave per (destination n, head h); LPE lanes per edge over the head's Fp/4
 // chunks (CPL per lane), 64/LPE edges per step.
@@ -154,11 +181,20 @@ __global__ void __launch_bounds__(256) edge_bwd_dst_kernel(BwdArgs g) {
   const int lane = threadIdx.x & 63;
   const int wave = uni(threadIdx.x >> 6);
   const int grp = lane / LPE, li = lane % LPE;
-  const int64_t item = xcd_contiguous(blockIdx.x, gridDim.x) * 4 + wave;
-  if (item >= g.n_items) return;
-  int64_t n;
-  int h;
-  if (!decode_item(item, g.N, g.NH, g.chunk, n, h)) return;
+  const int64_t hb = g.hub_blocks;
+  int64_t n, slot = -1;
+  int h, beg, end;
+  if ((int64_t)blockIdx.x < hb) {   // one piece of a hub: sweep 1 only (g_alpha, partial c)
+    if (!hub_piece(g, wave, n, h, beg, end, slot)) return;
+  } else {
+    const int64_t item = xcd_contiguous(blockIdx.x - hb, gridDim.x - hb) * 4 + wave;
+    if (item >= g.n_items) return;
+    if (!decode_item(item, g.N, g.NH, g.chunk, n, h)) return;
+    beg = uni(g.rowptr[n]);
+    end = uni(g.rowptr[n + 1]);
+    if (g.hub_T > 0 && end - beg > g.hub_T) return;   // done in pieces
+  }
+  const bool keep0 = slot < 0;   // a piece stores every g_alpha for the hub kernels
   const int NH = g.NH, Fp = g.Fp, F4 = Fp / 4, S2 = 2 * NH;
   const int64_t E2 = g.E2;
   const float M = ord_to_float(*g.M_ord);
@@ -186,7 +222,6 @@ __global__ void __launch_bounds__(256) edge_bwd_dst_kernel(BwdArgs g) {
   int* src_lds = src_sh[wave];
   float* dot_lds = dot_sh[wave];
 
-  const int beg = uni(g.rowptr[n]), end = uni(g.rowptr[n + 1]);
   // sweep 1: g_alpha per edge, c = sum g_alpha * alpha. The first 64 edges' g_alpha and exp
   // stay in registers for sweep 2 (at PPI that is every edge of nearly every node); later
   // batches go through g_raw. Besides the reload, a store ahead of sweep 2's loads would make
@@ -237,7 +272,7 @@ __global__ void __launch_bounds__(256) edge_bwd_dst_kernel(BwdArgs g) {
       float ga = my_dot;
       if (drop) ga = dropout_keep(seed, (int64_t)g.perm[e] * NH + h, g.p_drop) ? ga * drop_scale : 0.f;
       if (g.g_alpha_ret) ga += g.g_alpha_ret[(int64_t)g.perm[e] * NH + h];
-      if (base == beg) {
+      if (base == beg && keep0) {
         ga0 = ga;
         ex0 = ex;
       } else {
@@ -247,6 +282,10 @@ __global__ void __launch_bounds__(256) edge_bwd_dst_kernel(BwdArgs g) {
     }
   }
   const float cc = group_sum<64>(c_acc);
+  if (!keep0) {   // the piece's share of c; edge_bwd_dst_hub_kernel finishes the hub
+    if (lane == 0) g.hub_part[slot * NH + h] = cc;
+    return;
+  }
   // sweep 2 (same lane <-> edge map, so each lane re-reads only its own stores)
   float gsum = 0.f;
   for (int base = beg; base < end; base += 64) {
@@ -260,6 +299,54 @@ __global__ void __launch_bounds__(256) edge_bwd_dst_kernel(BwdArgs g) {
     }
   }
   gsum = group_sum<64>(gsum);
+  if (lane == 0) {
+    g.G_aug[n * g.ldg + g.gs_off + NH + h] = gsum;
+    g.gsd[n * NH + h] = gsum;
+  }
+}
+
+// Sweep 2 of a hub-split destination segment, one wave per piece: c = the hub's piece partials
+// summed in piece order, then g_raw' of the piece's edges (from the g_alpha sweep 1 stored) and
+// the piece's share of g_s_dst into hub_part[hub_bound + slot].
+__global__ void __launch_bounds__(256) edge_bwd_dst_hub_kernel(BwdArgs g) {
+  const int lane = threadIdx.x & 63;
+  const int wave = uni(threadIdx.x >> 6);
+  int64_t n, slot;
+  int h, beg, end;
+  if (!hub_piece(g, wave, n, h, beg, end, slot)) return;
+  const int NH = g.NH, S2 = 2 * NH;
+  const int32_t* hp = g.hubs + 4 * slot;
+  const int pieces = uni(hp[2]), first = uni(hp[3]);
+  float cc = 0.f;
+  for (int q = 0; q < pieces; ++q) cc += g.hub_part[(int64_t)(first + q) * NH + h];
+  const float M = ord_to_float(*g.M_ord);
+  const float sdst = g.S[n * S2 + NH + h];
+  const float dinv = 1.f / (g.den[n * NH + h] + kSoftmaxEps);
+  float* __restrict__ graw = g.g_raw + (int64_t)h * g.E2;
+  float gsum = 0.f;
+  for (int e = beg + lane; e < end; e += 64) {
+    const float ex = att_exp(g.S[(int64_t)g.col[e] * S2 + h] + sdst, M);
+    const float gr = kLeakySlope * ex * (graw[e] - cc) * dinv;
+    graw[e] = gr;
+    gsum += gr;
+  }
+  gsum = group_sum<64>(gsum);
+  if (lane == 0) g.hub_part[g.hub_bound * NH + slot * NH + h] = gsum;
+}
+
+// g_s_dst of a hub: its pieces' shares summed in piece order (one wave per hub and head: the
+// wave of the hub's first piece).
+__global__ void __launch_bounds__(256) edge_bwd_dst_hub_finish_kernel(BwdArgs g) {
+  const int lane = threadIdx.x & 63;
+  const int wave = uni(threadIdx.x >> 6);
+  int64_t n, slot;
+  int h, beg, end;
+  if (!hub_piece(g, wave, n, h, beg, end, slot)) return;
+  const int32_t* hp = g.hubs + 4 * slot;
+  if (uni(hp[1]) != 0) return;
+  const int NH = g.NH, pieces = uni(hp[2]);
+  float gsum = 0.f;
+  for (int q = 0; q < pieces; ++q) gsum += g.hub_part[g.hub_bound * NH + (slot + q) * NH + h];
   if (lane == 0) {
     g.G_aug[n * g.ldg + g.gs_off + NH + h] = gsum;
     g.gsd[n * NH + h] = gsum;
@@ -385,11 +472,19 @@ __global__ void __launch_bounds__(256) edge_bwd_src_kernel(BwdArgs g) {
   const int lane = threadIdx.x & 63;
   const int wave = uni(threadIdx.x >> 6);
   const int grp = lane / LPE, li = lane % LPE;
-  const int64_t item = xcd_contiguous(blockIdx.x, gridDim.x) * 4 + wave;
-  if (item >= g.n_items) return;
-  int64_t s;
-  int h;
-  if (!decode_item(item, g.N, g.NH, g.chunk, s, h)) return;
+  const int64_t hb = g.hub_blocks;
+  int64_t s, slot = -1;
+  int h, beg, end;
+  if ((int64_t)blockIdx.x < hb) {   // one piece of a hub source: a partial row
+    if (!hub_piece(g, wave, s, h, beg, end, slot)) return;
+  } else {
+    const int64_t item = xcd_contiguous(blockIdx.x - hb, gridDim.x - hb) * 4 + wave;
+    if (item >= g.n_items) return;
+    if (!decode_item(item, g.N, g.NH, g.chunk, s, h)) return;
+    beg = uni(g.rowptr[s]);
+    end = uni(g.rowptr[s + 1]);
+    if (g.hub_T > 0 && end - beg > g.hub_T) return;   // done in pieces
+  }
   const int NH = g.NH, Fp = g.Fp, F4 = Fp / 4, S2 = 2 * NH;
   const int64_t Dp = (int64_t)NH * Fp, E2 = g.E2;
   const float M = g.const_att ? 0.f : ord_to_float(*g.M_ord);
@@ -417,7 +512,6 @@ __global__ void __launch_bounds__(256) edge_bwd_src_kernel(BwdArgs g) {
   float gs = 0.f;
   const float* __restrict__ graw = g.g_raw ? g.g_raw + (int64_t)h * E2 : nullptr;
 
-  const int beg = uni(g.rowptr[s]), end = uni(g.rowptr[s + 1]);
   for (int base = beg; base < end; base += 64) {
     const int cnt = min(64, end - base);
     const bool valid = lane < cnt;
@@ -482,6 +576,21 @@ __global__ void __launch_bounds__(256) edge_bwd_src_kernel(BwdArgs g) {
 #pragma unroll
     for (int c = 0; c < CPL; ++c) acc[c] = add4(acc[c], shfl_xor4(acc[c], off));
   }
+  if (slot >= 0) {   // a hub piece: [Fp row | g_s_src share] partial for the combine kernel
+    float* part = g.hub_part + (slot * NH + h) * (int64_t)(Fp + 4);
+    if (grp == 0) {
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) {
+        const int q = c * LPE + li;
+        if (q < F4) *(float4*)(part + 4 * q) = acc[c];
+      }
+    }
+    if (!g.const_att) {
+      gs = group_sum<64>(gs);
+      if (lane == 0) part[Fp] = gs;
+    }
+    return;
+  }
   float* row = g.G_aug + s * g.ldg;
   if (grp == 0) {
 #pragma unroll
@@ -493,6 +602,32 @@ __global__ void __launch_bounds__(256) edge_bwd_src_kernel(BwdArgs g) {
   if (!g.const_att) {
     gs = group_sum<64>(gs);
     if (lane == 0) row[Dp + h] = gs + (g.g_corr ? g.g_corr[s * NH + h] : 0.f);
+  }
+}
+
+// A hub source's row of G_aug: its pieces' partial rows summed in piece order (one wave per hub
+// and head: the wave of the hub's first piece), plus max()'s share.
+__global__ void __launch_bounds__(256) edge_bwd_src_hub_combine_kernel(BwdArgs g) {
+  const int lane = threadIdx.x & 63;
+  const int wave = uni(threadIdx.x >> 6);
+  int64_t s, slot;
+  int h, beg, end;
+  if (!hub_piece(g, wave, s, h, beg, end, slot)) return;
+  const int32_t* hp = g.hubs + 4 * slot;
+  if (uni(hp[1]) != 0) return;
+  const int NH = g.NH, Fp = g.Fp, F4 = Fp / 4, pieces = uni(hp[2]);
+  const int64_t W = Fp + 4, Dp = (int64_t)NH * Fp;
+  const float* part = g.hub_part + (slot * NH + h) * W;
+  float* row = g.G_aug + s * g.ldg;
+  for (int q = lane; q < F4; q += 64) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int p = 0; p < pieces; ++p) acc = add4(acc, *(const float4*)(part + p * NH * W + 4 * q));
+    *(float4*)(row + (int64_t)h * Fp + 4 * q) = acc;
+  }
+  if (!g.const_att && lane == 0) {
+    float gs = 0.f;
+    for (int p = 0; p < pieces; ++p) gs += part[p * NH * W + Fp];
+    row[Dp + h] = gs + (g.g_corr ? g.g_corr[s * NH + h] : 0.f);
   }
 }
 
@@ -760,15 +895,41 @@ extern "C" int gatx_prepare_go(const float* g_out, const float* out, int64_t N, 
                             concat ? (int64_t)NH * F : F, 0.f, nullptr, s);
 }
 
-extern "C" int gatx_edge_backward_dst_ex(const float* rows, int64_t row_stride,
-                                         int64_t head_stride, const float* S,
-                                         const uint32_t* M_ord, const float* den,
-                                         const int32_t* rowptr, const int32_t* col,
-                                         const int32_t* perm, int64_t N, int64_t E2, int NH, int F,
-                                         const float* go, int64_t go_stride, int64_t go_head,
-                                         float p, const uint64_t* seed, const float* g_alpha,
-                                         float* g_raw, float* gsd, float* G, int64_t ldg,
-                                         int64_t gs_off, gatx_stream_t s) {
+extern "C" size_t gatx_edge_backward_hub_part_bytes(int64_t hub_bound, int NH, int F,
+                                                    int src_pass) {
+  const int64_t Fp = round_up(F, 4);
+  return (size_t)hub_bound * NH * (src_pass ? Fp + 4 : 2) * sizeof(float);
+}
+
+namespace gatx {
+namespace {
+// Hub fields of BwdArgs; false when the buffers are missing.
+bool set_hubs(BwdArgs& a, int hub_edges, const int32_t* hubs, const int32_t* hub_count,
+              int64_t hub_bound, float* hub_part) {
+  a.hub_T = 0; a.hubs = nullptr; a.hub_count = nullptr; a.hub_bound = 0; a.hub_part = nullptr;
+  a.hub_blocks = 0;
+  if (hub_edges <= 0 || hub_bound <= 0) return true;
+  if (!hubs || !hub_count || !hub_part) return false;
+  a.hub_T = hub_edges; a.hubs = hubs; a.hub_count = hub_count; a.hub_bound = hub_bound;
+  a.hub_part = hub_part;
+  // a multiple of 8 blocks: dealt round-robin over the XCDs, dispatched first
+  a.hub_blocks = round_up(ceil_div(hub_bound * a.NH, 4), 8);
+  return true;
+}
+}  // namespace
+}  // namespace gatx
+
+extern "C" int gatx_edge_backward_dst_hubs(const float* rows, int64_t row_stride,
+                                           int64_t head_stride, const float* S,
+                                           const uint32_t* M_ord, const float* den,
+                                           const int32_t* rowptr, const int32_t* col,
+                                           const int32_t* perm, int64_t N, int64_t E2, int NH,
+                                           int F, const float* go, int64_t go_stride,
+                                           int64_t go_head, float p, const uint64_t* seed,
+                                           const float* g_alpha, float* g_raw, float* gsd,
+                                           float* G, int64_t ldg, int64_t gs_off, int hub_edges,
+                                           const int32_t* hubs, const int32_t* hub_count,
+                                           int64_t hub_bound, float* hub_part, gatx_stream_t s) {
   hipStream_t st = (hipStream_t)s;
   if (N == 0) return 0;
   const int Fp = (int)round_up(F, 4);
@@ -789,10 +950,34 @@ extern "C" int gatx_edge_backward_dst_ex(const float* rows, int64_t row_stride,
   a.g_alpha_ret = g_alpha; a.g_raw = g_raw; a.gsd = gsd; a.G_aug = G; a.ldg = ldg;
   a.chunk = kChunk;
   a.n_items = ceil_div(N, kChunk) * kChunk * NH;
-  const unsigned grid = (unsigned)ceil_div(a.n_items, 4);
+  GATX_REQUIRE(set_hubs(a, hub_edges, hubs, hub_count, hub_bound, hub_part),
+               "edge_backward_dst: hub splitting needs its plan and partial buffer");
+  const unsigned grid = (unsigned)(a.hub_blocks + ceil_div(a.n_items, 4));
   GATX_DISPATCH_HEAD(gm, edge_bwd_dst_kernel, grid, a);
   GATX_LAUNCH_CHECK("edge_bwd_dst");
+  if (a.hub_T > 0) {
+    const unsigned hg = (unsigned)ceil_div(a.hub_bound * NH, 4);
+    edge_bwd_dst_hub_kernel<<<hg, 256, 0, st>>>(a);
+    GATX_LAUNCH_CHECK("edge_bwd_dst_hub");
+    edge_bwd_dst_hub_finish_kernel<<<hg, 256, 0, st>>>(a);
+    GATX_LAUNCH_CHECK("edge_bwd_dst_hub_finish");
+  }
   return 0;
+}
+
+extern "C" int gatx_edge_backward_dst_ex(const float* rows, int64_t row_stride,
+                                         int64_t head_stride, const float* S,
+                                         const uint32_t* M_ord, const float* den,
+                                         const int32_t* rowptr, const int32_t* col,
+                                         const int32_t* perm, int64_t N, int64_t E2, int NH, int F,
+                                         const float* go, int64_t go_stride, int64_t go_head,
+                                         float p, const uint64_t* seed, const float* g_alpha,
+                                         float* g_raw, float* gsd, float* G, int64_t ldg,
+                                         int64_t gs_off, gatx_stream_t s) {
+  return gatx_edge_backward_dst_hubs(rows, row_stride, head_stride, S, M_ord, den, rowptr, col,
+                                     perm, N, E2, NH, F, go, go_stride, go_head, p, seed, g_alpha,
+                                     g_raw, gsd, G, ldg, gs_off, 0, nullptr, nullptr, 0, nullptr,
+                                     s);
 }
 
 extern "C" int gatx_edge_backward_dst(const float* Wh, const float* S, const uint32_t* M_ord,
@@ -853,13 +1038,16 @@ extern "C" int gatx_max_backward(const int64_t* argmax, const float* gsd, const 
   return 0;
 }
 
-extern "C" int gatx_edge_backward_src(const float* S, const uint32_t* M_ord, const float* den,
-                                      const int32_t* srowptr, const int32_t* scol,
-                                      const int32_t* seid, const int32_t* perm, int64_t N,
-                                      int64_t E2, int NH, int F, int concat, int const_att,
-                                      float p, const uint64_t* seed, const float* go,
-                                      const float* g_raw, const float* g_corr_src, float* G_aug,
-                                      int64_t ldg, gatx_stream_t s) {
+extern "C" int gatx_edge_backward_src_hubs(const float* S, const uint32_t* M_ord,
+                                           const float* den, const int32_t* srowptr,
+                                           const int32_t* scol, const int32_t* seid,
+                                           const int32_t* perm, int64_t N, int64_t E2, int NH,
+                                           int F, int concat, int const_att, float p,
+                                           const uint64_t* seed, const float* go,
+                                           const float* g_raw, const float* g_corr_src,
+                                           float* G_aug, int64_t ldg, int hub_edges,
+                                           const int32_t* hubs, const int32_t* hub_count,
+                                           int64_t hub_bound, float* hub_part, gatx_stream_t s) {
   hipStream_t st = (hipStream_t)s;
   if (N == 0) return 0;
   const int Fp = (int)round_up(F, 4);
@@ -875,21 +1063,41 @@ extern "C" int gatx_edge_backward_src(const float* S, const uint32_t* M_ord, con
   a.p_drop = p; a.seed = seed; a.g_raw = const_att ? nullptr : (float*)g_raw;
   a.g_corr = g_corr_src; a.G_aug = G_aug; a.ldg = ldg;
   a.chunk = kChunk;
+  GATX_REQUIRE(set_hubs(a, hub_edges, hubs, hub_count, hub_bound, hub_part),
+               "edge_backward_src: hub splitting needs its plan and partial buffer");
   static const bool per_head = [] {   // A/B switch: GATX_SRC_MEAN=0 keeps per-head items
     const char* e = getenv("GATX_SRC_MEAN");
     return e && e[0] == '0';
   }();
-  if (!concat && NH <= 8 && !per_head) {   // head-mean: one item per source, all heads
+  // head-mean: one item per source, all heads (hub-split graphs take the per-head items, which
+  // also serve head-mean layers: go_head4 = 0)
+  if (!concat && NH <= 8 && !per_head && a.hub_T == 0) {
     const unsigned grid = (unsigned)ceil_div(N, 4);
     GATX_DISPATCH_HEAD(gm, edge_bwd_src_mean_kernel, grid, a);
     GATX_LAUNCH_CHECK("edge_bwd_src_mean");
     return 0;
   }
   a.n_items = ceil_div(N, kChunk) * kChunk * NH;
-  const unsigned grid = (unsigned)ceil_div(a.n_items, 4);
+  const unsigned grid = (unsigned)(a.hub_blocks + ceil_div(a.n_items, 4));
   GATX_DISPATCH_HEAD(gm, edge_bwd_src_kernel, grid, a);
   GATX_LAUNCH_CHECK("edge_bwd_src");
+  if (a.hub_T > 0) {
+    edge_bwd_src_hub_combine_kernel<<<(unsigned)ceil_div(a.hub_bound * NH, 4), 256, 0, st>>>(a);
+    GATX_LAUNCH_CHECK("edge_bwd_src_hub_combine");
+  }
   return 0;
+}
+
+extern "C" int gatx_edge_backward_src(const float* S, const uint32_t* M_ord, const float* den,
+                                      const int32_t* srowptr, const int32_t* scol,
+                                      const int32_t* seid, const int32_t* perm, int64_t N,
+                                      int64_t E2, int NH, int F, int concat, int const_att,
+                                      float p, const uint64_t* seed, const float* go,
+                                      const float* g_raw, const float* g_corr_src, float* G_aug,
+                                      int64_t ldg, gatx_stream_t s) {
+  return gatx_edge_backward_src_hubs(S, M_ord, den, srowptr, scol, seid, perm, N, E2, NH, F,
+                                     concat, const_att, p, seed, go, g_raw, g_corr_src, G_aug,
+                                     ldg, 0, nullptr, nullptr, 0, nullptr, s);
 }
 
 extern "C" int gatx_weight_grads(const float* gW_aug, const float* W, const float* a, int NH,

@@ -87,6 +87,12 @@ SIGNATURES = {
     "gatx_edge_backward_dst_ex": (c_i, [P, c_i64, c_i64, P, P, P, P, P, P, c_i64, c_i64, c_i,
                                         c_i, P, c_i64, c_i64, c_f, P, P, P, P, P, c_i64,
                                         c_i64, P]),
+    "gatx_edge_backward_hub_part_bytes": (c_sz, [c_i64, c_i, c_i, c_i]),
+    "gatx_edge_backward_dst_hubs": (c_i, [P, c_i64, c_i64, P, P, P, P, P, P, c_i64, c_i64, c_i,
+                                          c_i, P, c_i64, c_i64, c_f, P, P, P, P, P, c_i64,
+                                          c_i64, c_i, P, P, c_i64, P, P]),
+    "gatx_edge_backward_src_hubs": (c_i, [P, P, P, P, P, P, P, c_i64, c_i64, c_i, c_i, c_i, c_i,
+                                          c_f, P, P, P, P, P, c_i64, c_i, P, P, c_i64, P, P]),
     "gatx_edge_backward_src_scores": (c_i, [P, P, c_i64, c_i64, c_i, P, P, P, c_i64, c_i64, P]),
     "gatx_gemm_splitk_batched_workspace_bytes": (c_sz, [c_i64, c_i64, c_i64, c_i64]),
     "gatx_gemm_f32_splitk_batched": (c_i, [c_i64, c_i64, c_i64, c_i64, P, c_i64, c_i64, c_i64, P,

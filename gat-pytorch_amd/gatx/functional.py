@@ -264,6 +264,20 @@ def hub_args(graph: Graph, sh: LayerShape, hs: int, group_count: int, dev):
     return (T, ptr(hubs), ptr(count), bound, ptr(part))
 
 
+def bwd_hub_args(graph: Graph, NH: int, F: int, dev, source: bool):
+    """The trailing hub-splitting arguments of gatx_edge_backward_{dst,src}_hubs: the same rule
+    as the forward (hub_args), over the destination CSR (source=False) or the transpose
+    (source=True). GATX_BWD_HUBS=0 keeps one wave per segment (A/B tests)."""
+    T = _env_int("GATX_HUB_EDGES", 8192)
+    if (T <= 0 or _env_int("GATX_BWD_HUBS", 1) == 0
+            or graph.num_input_edges <= _env_int("GATX_HUB_MIN_EDGES", 1 << 22)):
+        return (0, None, None, 0, None)
+    hubs, count, bound = graph.hub_plan(T, source)
+    nb = lib.gatx_edge_backward_hub_part_bytes(bound, NH, F, int(source))
+    part = torch.empty(max(nb, 4), dtype=torch.uint8, device=dev)
+    return (T, ptr(hubs), ptr(count), bound, ptr(part))
+
+
 def fold_scores_into_gemm(sh: LayerShape) -> bool:
     """Compute S as 2NH extra GEMM columns only when they fit the last column tile for free;
     otherwise (e.g. Dp = 1024: a whole extra 128-wide tile, +12% GEMM time) project Wh alone and
@@ -465,15 +479,16 @@ def layer_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShape, 
     if not sh.const:
         g_raw = torch.empty((sh.NH, max(E2, 1)), **f32)
         gsd = torch.empty((N, sh.NH), **f32)
-        call("gatx_edge_backward_dst", ptr(saved["Wh"]), ptr(saved["S"]), ptr(saved["M_ord"]),
-             ptr(saved["den"]), ptr(graph.rowptr), ptr(graph.col), ptr(graph.perm), N, E2,
-             sh.NH, sh.F, int(sh.concat), float(p), ptr(seed), ptr(go),
+        call("gatx_edge_backward_dst_hubs", ptr(saved["Wh"]), sh.Dp, sh.Fp, ptr(saved["S"]),
+             ptr(saved["M_ord"]), ptr(saved["den"]), ptr(graph.rowptr), ptr(graph.col),
+             ptr(graph.perm), N, E2, sh.NH, sh.F, ptr(go), sh.Dp if sh.concat else sh.Fp,
+             sh.Fp if sh.concat else 0, float(p), ptr(seed),
              ptr(g_alpha.contiguous()) if g_alpha is not None else None, ptr(g_raw), ptr(gsd),
-             ptr(G_aug), ldg, s)
-    call("gatx_edge_backward_src", ptr(saved["S"]), ptr(saved["M_ord"]), ptr(saved["den"]),
+             ptr(G_aug), ldg, sh.Dp, *bwd_hub_args(graph, sh.NH, sh.F, dev, False), s)
+    call("gatx_edge_backward_src_hubs", ptr(saved["S"]), ptr(saved["M_ord"]), ptr(saved["den"]),
          ptr(graph.srowptr), ptr(graph.scol), ptr(graph.seid), ptr(graph.perm), N, E2, sh.NH,
          sh.F, int(sh.concat), int(sh.const), float(p), ptr(seed), ptr(go), ptr(g_raw), None,
-         ptr(G_aug), ldg, s)
+         ptr(G_aug), ldg, *bwd_hub_args(graph, sh.NH, sh.F, dev, True), s)
     if not sh.const:   # max()'s share, added into both logit-gradient columns of G_aug
         mws = torch.empty(lib.gatx_max_backward_workspace_bytes(), dtype=torch.uint8, device=dev)
         call("gatx_max_backward", ptr(saved["argmax"]), ptr(gsd), ptr(saved["S"]),
@@ -552,11 +567,11 @@ def _reassoc_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShap
          F * Fin_p, ptr(g_Z), NH * Fin_p, Fin_p, 0, None, 0, None, 0, 0, 0, s)
     g_raw = torch.empty((NH, max(E2, 1)), **f32)
     gsd = torch.empty((N, NH), **f32)
-    call("gatx_edge_backward_dst_ex", ptr(x_rows), Fin_p, 0, ptr(saved["S"]), ptr(saved["M_ord"]),
-         ptr(saved["den"]), ptr(graph.rowptr), ptr(graph.col), ptr(graph.perm), N, E2, NH, Fin_p,
-         ptr(g_Z), NH * Fin_p, Fin_p, float(p), ptr(seed),
+    call("gatx_edge_backward_dst_hubs", ptr(x_rows), Fin_p, 0, ptr(saved["S"]),
+         ptr(saved["M_ord"]), ptr(saved["den"]), ptr(graph.rowptr), ptr(graph.col),
+         ptr(graph.perm), N, E2, NH, Fin_p, ptr(g_Z), NH * Fin_p, Fin_p, float(p), ptr(seed),
          ptr(g_alpha.contiguous()) if g_alpha is not None else None, ptr(g_raw), ptr(gsd),
-         ptr(G_s), lds, 0, s)
+         ptr(G_s), lds, 0, *bwd_hub_args(graph, NH, Fin_p, dev, False), s)
     call("gatx_edge_backward_src_scores", ptr(graph.srowptr), ptr(graph.seid), N, E2, NH,
          ptr(g_raw), None, ptr(G_s), lds, 0, s)
     mws = torch.empty(lib.gatx_max_backward_workspace_bytes(), dtype=torch.uint8, device=dev)

@@ -188,17 +188,21 @@ class Graph:
         call("gatx_graph_transpose", ptr(self.col), ptr(self.rowidx), N, Eb, self.e2_ptr,
              ptr(self.srowptr), ptr(self.scol), ptr(self.seid), ptr(ws), ws_bytes, stream())
 
-    def hub_plan(self, hub_edges: int):
+    def hub_plan(self, hub_edges: int, source: bool = False):
         """(hubs, hub_count, hub_bound) of gatx_graph_hub_plan for this CSR: destination segments
-        longer than hub_edges listed as pieces (device-side count; built once per graph)."""
-        plan = self._hub_plans.get(hub_edges)
+        (source=True: source segments of the transpose, for the backward's source pass) longer
+        than hub_edges listed as pieces (device-side count; built once per graph)."""
+        key = (hub_edges, source)
+        plan = self._hub_plans.get(key)
         if plan is None:
+            if source:
+                self.ensure_transpose()
             bound = int(_lib.lib.gatx_graph_hub_bound(self.edge_bound, hub_edges))
             hubs = torch.empty((max(bound, 1), 4), dtype=torch.int32, device=self.device)
             count = torch.empty(1, dtype=torch.int32, device=self.device)
-            call("gatx_graph_hub_plan", ptr(self.rowptr), self.num_nodes, hub_edges, ptr(hubs),
-                 bound, ptr(count), stream())
-            plan = self._hub_plans[hub_edges] = (hubs, count, bound)
+            call("gatx_graph_hub_plan", ptr(self.srowptr if source else self.rowptr),
+                 self.num_nodes, hub_edges, ptr(hubs), bound, ptr(count), stream())
+            plan = self._hub_plans[key] = (hubs, count, bound)
         return plan
 
     def csr_host(self):

@@ -348,6 +348,24 @@ int gatx_edge_backward_dst_ex(const float* rows, int64_t row_stride, int64_t hea
                               int64_t go_stride, int64_t go_head, float p, const uint64_t* seed,
                               const float* g_alpha_ret, float* g_raw, float* gsd, float* G,
                               int64_t ldg, int64_t gs_off, gatx_stream_t stream);
+/* gatx_edge_backward_dst_ex with hub splitting (SURVEY §7 "degree skew"; the backward of the
+ * reference's scatter_add_, models/utils.py:17-20 via gat_layer.py:99-127, has no per-degree
+ * cliff): destination segments longer than hub_edges (a plan from gatx_graph_hub_plan over the
+ * same rowptr) are walked as pieces by parallel waves; the softmax-backward constant c and
+ * g_s_dst are combined from per-piece partials in piece order (deterministic) by two follow-up
+ * kernels. hub_part: gatx_edge_backward_hub_part_bytes(hub_bound, NH, F, 0). hub_edges = 0: no
+ * splitting (exactly gatx_edge_backward_dst_ex). */
+size_t gatx_edge_backward_hub_part_bytes(int64_t hub_bound, int num_heads, int out_features,
+                                         int src_pass);
+int gatx_edge_backward_dst_hubs(const float* rows, int64_t row_stride, int64_t head_stride,
+                                const float* S, const uint32_t* M_ord, const float* den,
+                                const int32_t* rowptr, const int32_t* col, const int32_t* perm,
+                                int64_t num_nodes, int64_t E2, int NH, int F, const float* go,
+                                int64_t go_stride, int64_t go_head, float p, const uint64_t* seed,
+                                const float* g_alpha_ret, float* g_raw, float* gsd, float* G,
+                                int64_t ldg, int64_t gs_off, int hub_edges, const int32_t* hubs,
+                                const int32_t* hub_count, int64_t hub_bound, float* hub_part,
+                                gatx_stream_t stream);
 /* Source-side logit gradients only: G[s][gs_off + h] = sum over s's out-edges (src-CSR) of
  * g_raw'[h][e] + g_corr[s][h] (NULL allowed). No message gradient. NH <= 8. */
 int gatx_edge_backward_src_scores(const int32_t* srowptr, const int32_t* seid, int64_t num_nodes,
@@ -376,6 +394,19 @@ int gatx_edge_backward_src(const float* S, const uint32_t* M_ord, const float* d
                            int concat, int const_attention, float dropout_p, const uint64_t* seed,
                            const float* go, const float* g_raw, const float* g_corr_src,
                            float* G_aug, int64_t ldg, gatx_stream_t stream);
+
+/* gatx_edge_backward_src with hub splitting: source segments (srowptr) longer than hub_edges
+ * (a gatx_graph_hub_plan over srowptr) are accumulated as pieces by parallel waves into partial
+ * rows, summed in piece order by a combine kernel (deterministic). hub_part:
+ * gatx_edge_backward_hub_part_bytes(hub_bound, NH, F, 1). hub_edges = 0: no splitting. */
+int gatx_edge_backward_src_hubs(const float* S, const uint32_t* M_ord, const float* den,
+                                const int32_t* srowptr, const int32_t* scol, const int32_t* seid,
+                                const int32_t* perm, int64_t num_nodes, int64_t E2, int NH, int F,
+                                int concat, int const_attention, float dropout_p,
+                                const uint64_t* seed, const float* go, const float* g_raw,
+                                const float* g_corr_src, float* G_aug, int64_t ldg, int hub_edges,
+                                const int32_t* hubs, const int32_t* hub_count, int64_t hub_bound,
+                                float* hub_part, gatx_stream_t stream);
 
 /* From g_W_aug [(Dp+2NH) x F_in] (= G_aug^T x): g_W [NH*F x F_in] and g_a [NH x NH*2F]
  * (a may be NULL for const_attention; then g_a is untouched). */

@@ -1,8 +1,11 @@
-"""Hub splitting of the edge pass (gatx_graph_hub_plan + gatx_edge_forward_hubs): destination
-segments longer than GATX_HUB_EDGES are aggregated in pieces by parallel waves and combined in
-piece order. Checked against the oracle (the reference's dataflow) on graphs with hubs of a few
-to many pieces, every epilogue kind (concat, one-pass and multi-pass head mean, the reassociated
-first layer, dropout), and against the unsplit kernel."""
+"""Hub splitting of the edge passes (gatx_graph_hub_plan + gatx_edge_forward_hubs, and in the
+backward gatx_edge_backward_dst_hubs / gatx_edge_backward_src_hubs): destination segments (and,
+in the backward's source pass, source segments) longer than GATX_HUB_EDGES are processed in
+pieces by parallel waves and combined in piece order. Checked against the oracle (the reference's
+dataflow, whose scatter_add_ backward `models/utils.py:17-20` has no per-degree cliff) on graphs
+with destination AND source hubs of a few to many pieces, every epilogue kind (concat, one-pass
+and multi-pass head mean, the reassociated first layer, dropout), against the unsplit kernels,
+and for bitwise repeatability."""
 import numpy as np
 import pytest
 import torch
@@ -16,14 +19,19 @@ OUT_TOL = 1e-4
 GRAD_TOL = 1e-4
 
 
-def _hub_graph(n=3000, e=20000, hubs=(30000, 9000, 1001, 1000, 999), fin=16, seed=11):
-    """Uniform random edges plus hub destinations receiving the given in-degrees."""
+def _hub_graph(n=3000, e=20000, hubs=(30000, 9000, 1001, 1000, 999), fin=16, seed=11,
+               src_hubs=(12000, 2500, 1000)):
+    """Uniform random edges plus hub destinations receiving the given in-degrees and hub sources
+    sending the given out-degrees."""
     rng = np.random.default_rng(seed)
     src = [rng.integers(0, n, e)]
     dst = [rng.integers(0, n, e)]
     for i, d in enumerate(hubs):
         src.append(rng.integers(0, n, d))
         dst.append(np.full(d, 17 + 101 * i))
+    for i, d in enumerate(src_hubs):
+        src.append(np.full(d, 29 + 97 * i))
+        dst.append(rng.integers(0, n, d))
     ei = np.stack([np.concatenate(src), np.concatenate(dst)]).astype(np.int64)
     x = rng.standard_normal((n, fin)).astype(np.float32)
     return x, ei
@@ -51,6 +59,7 @@ def _run(device, x, ei, W, a, NH, F, concat, dropout=0.0, grads=True):
          + (alpha * torch.from_numpy(g_alpha).to(device)).sum()).backward()
         r["grad_x"] = xt.grad.cpu().numpy()
         r["grad_W"] = layer.W.weight.grad.cpu().numpy()
+        r["grad_a"] = layer.a.weight.grad.cpu().numpy()
     return r
 
 
@@ -86,16 +95,23 @@ def test_hub_split_vs_oracle(name, T, device, monkeypatch):
     assert np.abs(r["alpha"] - alpha).max() <= OUT_TOL
     g_out, g_alpha = grad_seeds(out.shape, alpha.shape)
     gr = orc.gat_layer_backward(cache, g_out, g_alpha)
-    for k in ("x", "W"):
+    for k in ("x", "W", "a"):
         err = np.abs(r[f"grad_{k}"] - gr[k]).max()
         assert err <= GRAD_TOL * max(1.0, np.abs(gr[k]).max()), (k, err)
+    # split backward is deterministic: a second run is bitwise identical
+    r1 = _run(device, x, ei, W, a, NH, F, concat, dropout)
+    for k in ("out", "alpha", "grad_x", "grad_W", "grad_a"):
+        np.testing.assert_array_equal(r[k], r1[k], err_msg=k)
     # the same layer without splitting: same result to fp32 summation-order noise
     monkeypatch.setenv("GATX_HUB_EDGES", "0")
     from gatx import functional
     functional.reset_tuning()
-    r0 = _run(device, x, ei, W, a, NH, F, concat, dropout, grads=False)
+    r0 = _run(device, x, ei, W, a, NH, F, concat, dropout)
     assert np.abs(r["out"] - r0["out"]).max() <= 1e-5
     assert np.abs(r["alpha"] - r0["alpha"]).max() <= 1e-5
+    for k in ("x", "W", "a"):
+        err = np.abs(r[f"grad_{k}"] - r0[f"grad_{k}"]).max()
+        assert err <= 1e-5 * max(1.0, np.abs(r0[f"grad_{k}"]).max()), (k, err)
 
 
 def test_hub_plan(device, monkeypatch):
@@ -127,3 +143,21 @@ def test_hub_plan(device, monkeypatch):
         assert f == pos
         pos += pieces
     assert pos == c
+
+
+def test_source_hub_plan(device):
+    """The backward's source-side plan lists the transpose's long segments (source hubs)."""
+    from gatx import clear_graph_cache
+    from gatx.graph import graph_cache
+    x, ei = _hub_graph()
+    clear_graph_cache()
+    g = graph_cache.get(torch.from_numpy(ei).to(device), x.shape[0], True)
+    hubs, count, bound = g.hub_plan(1000, source=True)
+    torch.cuda.synchronize()
+    deg = np.diff(g.srowptr.cpu().numpy())
+    want = {int(n): int(-(-d // 1000)) for n, d in enumerate(deg) if d > 1000}
+    assert {29: 13, 126: 3}.items() <= want.items()
+    c = int(count.item())
+    h = hubs[:c].cpu().numpy()
+    assert c == sum(want.values())
+    assert {int(node): int(pieces) for node, _, pieces, _ in h} == want
