@@ -566,12 +566,15 @@ def main():
     opt = torch.optim.Adam(model.parameters(), lr=cfg["learning_rate"], fused=True,
                            weight_decay=cfg["l2_reg"],
                            capturable=use_graph and args.mode == "train")
-    loss_fn = torch.nn.BCEWithLogitsLoss()
+    # PPI_GAT's nn.BCEWithLogitsLoss (models/ppi_gat.py:11,19) on gatx's fused loss kernels
+    # (gatx.losses: one launch forward, one backward, instead of ~19 torch launches)
+    from gatx.losses import BCEWithLogitsLoss
+    loss_fn = BCEWithLogitsLoss()
     if planetoid:
         loss_fn = torch.nn.CrossEntropyLoss(reduction="mean")
     if ds == "PATTERN":   # PatternGAT (models/pattern_gat.py:11-15): class-balanced BCE
-        loss_fn = torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([1 / 0.1765], device=dev))
-        y = y[:, 0]
+        loss_fn = BCEWithLogitsLoss(pos_weight=1 / 0.1765)
+        y = y[:, 0].contiguous()
     reducer = None
     w_main = w_norm = 1.0
     if args.mode == "train" and world > 1:

@@ -805,6 +805,119 @@ __global__ void __launch_bounds__(256) ga_kernel(const float* __restrict__ gW_au
   }
 }
 
+// gw_kernel and ga_kernel as ONE launch (small layers are launch-bound): blocks [0, ngw) do the
+// g_W elements grid-stride over those blocks, blocks ngw.. one W row each of g_a.
+template <int H2C>
+__global__ void __launch_bounds__(256) weight_grads_kernel(const float* __restrict__ gW_aug,
+                                                           const float* __restrict__ W,
+                                                           const float* __restrict__ a, int NH,
+                                                           int F, int Fp, int64_t F_in, int ngw,
+                                                           float* __restrict__ g_W,
+                                                           float* __restrict__ g_a) {
+  const int D = NH * F;
+  const int64_t Dp = (int64_t)NH * Fp;
+  if ((int)blockIdx.x < ngw) {
+    const int64_t total = (int64_t)D * F_in;
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+         t += (int64_t)ngw * blockDim.x) {
+      const int64_t c = t / F_in, i = t - c * F_in;
+      const int k = (int)(c / F), f = (int)(c - (int64_t)k * F);
+      float v = gW_aug[((int64_t)k * Fp + f) * F_in + i];
+      if (a) {
+        for (int h = 0; h < NH; ++h) {
+          const float* ar = a + (int64_t)h * 2 * D + k * 2 * F + f;
+          v = fmaf(ar[0], gW_aug[(Dp + h) * F_in + i], v);
+          v = fmaf(ar[F], gW_aug[(Dp + NH + h) * F_in + i], v);
+        }
+      }
+      g_W[t] = v;
+    }
+    return;
+  }
+  // g_a[h][k*2F + f (+F)] = sum_i gW_aug[Dp + h (+NH)][i] * W[c][i], c = k*F + f (ga_kernel)
+  __shared__ float red[4][H2C];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int H2 = 2 * NH;
+  const int c = (int)blockIdx.x - ngw;
+  const int k = c / F, f = c - k * F;
+  float acc[H2C];
+#pragma unroll
+  for (int h = 0; h < H2C; ++h) acc[h] = 0.f;
+  for (int64_t i = threadIdx.x; i < F_in; i += 256) {
+    const float w = W[(int64_t)c * F_in + i];
+#pragma unroll
+    for (int h = 0; h < H2C; ++h)
+      if (h < H2) acc[h] = fmaf(gW_aug[(Dp + h) * F_in + i], w, acc[h]);
+  }
+#pragma unroll
+  for (int h = 0; h < H2C; ++h) {
+    const float v = group_sum<64>(acc[h]);
+    if (lane == 0) red[wave][h] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < H2) {
+    const int h = threadIdx.x;
+    const float v = (red[0][h] + red[1][h]) + (red[2][h] + red[3][h]);
+    const int hh = h < NH ? h : h - NH;
+    g_a[(int64_t)hh * 2 * D + k * 2 * F + (h < NH ? 0 : F) + f] = v;
+  }
+}
+
+// max() backward for small graphs in ONE launch (sum_partial + max_bwd + the tie-overflow scan):
+// one 1024-thread block sums g_s_dst in a fixed order (thread-strided sums, then a fixed tree),
+// applies the share to the recorded argmax entries, and rescans the edges itself in the rare
+// case of more than GATX_ARGMAX_CAP ties.
+__global__ void __launch_bounds__(1024) max_bwd_small_kernel(
+    const float* __restrict__ gsd, int64_t n, const long long* __restrict__ argmax,
+    const float* __restrict__ S, const uint32_t* __restrict__ M_ord,
+    const int32_t* __restrict__ col, const int32_t* __restrict__ rowidx, int64_t E2b,
+    const long long* e2p, int NH, float* __restrict__ g_corr_src, float* __restrict__ G_aug,
+    int64_t ldg, int64_t Dp, float* __restrict__ gm_out) {
+  __shared__ float red[16];
+  __shared__ float share_s;
+  float sum = 0.f;
+  for (int64_t i = threadIdx.x; i < n; i += 1024) sum += gsd[i];
+  sum = group_sum<64>(sum);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sum;
+  __syncthreads();
+  const long long k = argmax[0];
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < 16; ++w) t += red[w];
+    share_s = k > 0 ? -t / (float)k : 0.f;
+    if (k > 0) gm_out[0] = share_s;
+  }
+  __syncthreads();
+  if (k <= 0) return;
+  const float share = share_s;
+  if (k <= GATX_ARGMAX_CAP) {
+    if (threadIdx.x == 0) {
+      for (long long j = 0; j < k; ++j) {   // sequential: k is small (ties)
+        const long long ent = argmax[1 + j];
+        const long long e = ent / NH;
+        const int h = (int)(ent - e * NH);
+        if (g_corr_src) g_corr_src[(int64_t)col[e] * NH + h] += share;
+        else G_aug[(int64_t)col[e] * ldg + Dp + h] += share;
+        G_aug[(int64_t)rowidx[e] * ldg + Dp + NH + h] += share;
+      }
+    }
+    return;
+  }
+  const int64_t E2 = e2p ? min(E2b, (int64_t)*e2p) : E2b;
+  const float M = ord_to_float(*M_ord);
+  const int S2 = 2 * NH;
+  for (int64_t t = threadIdx.x; t < E2 * NH; t += 1024) {
+    const int64_t e = t / NH;
+    const int h = (int)(t - e * NH);
+    const int64_t s = col[e], d = rowidx[e];
+    if (S[s * S2 + h] + S[d * S2 + NH + h] == M) {
+      if (g_corr_src) atomicAdd(&g_corr_src[s * NH + h], share);
+      else atomicAdd(&G_aug[s * ldg + Dp + h], share);
+      atomicAdd(&G_aug[d * ldg + Dp + NH + h], share);
+    }
+  }
+}
+
 __global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ X, int64_t nrows,
                                                      int64_t ncols, int64_t ld,
                                                      float* __restrict__ out) {
@@ -1025,6 +1138,13 @@ extern "C" int gatx_max_backward(const int64_t* argmax, const float* gsd, const 
   // the g_M share is parked right after the argmax records (the buffer holds CAP + 2 int64s)
   float* gm = (float*)(argmax + 1 + GATX_ARGMAX_CAP);
   float* part = (float*)workspace;
+  if (N * NH <= (1 << 16)) {   // small graphs: one launch instead of three
+    max_bwd_small_kernel<<<1, 1024, 0, st>>>(gsd, N * NH, (const long long*)argmax, S, M_ord, col,
+                                             rowidx, E2, (const long long*)e2, NH, g_corr_src,
+                                             G_aug, ldg, Dp, gm);
+    GATX_LAUNCH_CHECK("max_bwd_small");
+    return 0;
+  }
   const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(N * NH, 256), kSumBlocks));
   sum_partial_kernel<<<nb, 256, 0, st>>>(gsd, N * NH, part);
   GATX_LAUNCH_CHECK("gsd_sum");
@@ -1105,6 +1225,15 @@ extern "C" int gatx_weight_grads(const float* gW_aug, const float* W, const floa
   hipStream_t st = (hipStream_t)s;
   const int Fp = (int)round_up(F, 4);
   GATX_REQUIRE(!a || 2 * NH <= 32, "weight_grads: num_heads > 16 unsupported");
+  if (a && (int64_t)NH * F * F_in <= (1 << 22)) {   // small layers: one launch for both
+    const int ngw = (int)grid_for((int64_t)NH * F * F_in, 256, 1024);
+    const unsigned grid = (unsigned)(ngw + NH * F);
+    if (2 * NH <= 8) weight_grads_kernel<8><<<grid, 256, 0, st>>>(gW_aug, W, a, NH, F, Fp, F_in, ngw, g_W, g_a);
+    else if (2 * NH <= 16) weight_grads_kernel<16><<<grid, 256, 0, st>>>(gW_aug, W, a, NH, F, Fp, F_in, ngw, g_W, g_a);
+    else weight_grads_kernel<32><<<grid, 256, 0, st>>>(gW_aug, W, a, NH, F, Fp, F_in, ngw, g_W, g_a);
+    GATX_LAUNCH_CHECK("weight_grads");
+    return 0;
+  }
   gw_kernel<<<grid_for((int64_t)NH * F * F_in), 256, 0, st>>>(gW_aug, a, NH, F, Fp, F_in, g_W);
   GATX_LAUNCH_CHECK("gw");
   if (a) {

@@ -472,6 +472,174 @@ __global__ void __launch_bounds__(256) edge_forward_kernel(EdgeFwdArgs g) {
   finish_item<LPE, CPL>(g, n, h0, lane, grp, q, vq, hl, acc, row_lds, den_lds);
 }
 
+// The edge pass over source rows SHARED by every head (head_stride 0: the reassociated first
+// layer aggregates x rows, Z[n,h,:] = sum_e alpha~[e,h] x[src_e,:]). edge_forward_kernel would give
+// each (head, chunk) pair its own lane, so the HS lanes of one chunk load the same float4; here a
+// lane owns one float4 chunk of the row for ALL HS heads of the item (HS accumulators), so one
+// load instruction moves 64/LPE distinct edges' chunks. Per-edge weights of the HS heads sit in
+// LDS as one float4 row per edge (a single ds_read_b128 per edge for HS <= 4). Plain epilogue
+// (no bias / skip / ELU / output dropout: the reassociated layer's epilogue runs in its output
+// GEMM); hub pieces write the generic partial layout [h * Fp + f | den], finished by
+// edge_hub_combine_kernel.
+template <int LPE, int HSC>
+__global__ void __launch_bounds__(256) edge_forward_shared_kernel(EdgeFwdArgs g) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int EPW = 64 / LPE, U = 4;
+  constexpr int HSP = HSC <= 4 ? 4 : 8;   // weights per edge row in LDS (float4 granules)
+  const int lane = threadIdx.x & 63;
+  const int wave = uni(threadIdx.x >> 6);
+  const int grp = lane / LPE, li = lane % LPE;
+  const int64_t hb = g.hub_blocks;
+  const bool hub_block = (int64_t)blockIdx.x < hb;
+  const int64_t item = hub_block ? g.n_items_main + (int64_t)blockIdx.x * 4 + wave
+                                 : xcd_contiguous(blockIdx.x - hb, gridDim.x - hb) * 4 + wave;
+  if (!hub_block && item >= g.n_items_main) return;
+  const int NG = g.g_count;
+  int64_t n;
+  int hgl, beg, end;
+  int64_t hub_slot = -1;
+  if (!hub_block) {
+    const int64_t per_chunk = g.chunk * NG;
+    const int64_t ck = item / per_chunk, rem = item - ck * per_chunk;
+    hgl = (int)(rem / g.chunk);
+    n = ck * g.chunk + (rem - (int64_t)hgl * g.chunk);
+    if (n >= g.N) return;
+    beg = uni(g.rowptr[n]);
+    end = uni(g.rowptr[n + 1]);
+    if (g.hub_T > 0 && end - beg > g.hub_T) return;
+  } else {
+    const int64_t hi = item - g.n_items_main;
+    hgl = (int)(hi / g.hub_bound);
+    const int64_t pc = hi - (int64_t)hgl * g.hub_bound;
+    if (hgl >= NG || pc >= uni(*g.hub_count)) return;
+    const int32_t* hp = g.hubs + 4 * pc;
+    n = uni(hp[0]);
+    const int p = uni(hp[1]);
+    hub_slot = (int64_t)uni(hp[3]) + p;
+    beg = uni(g.rowptr[n]) + p * g.hub_T;
+    end = min(uni(g.rowptr[n + 1]), beg + g.hub_T);
+  }
+  const int h0 = (g.g_begin + hgl) * HSC;
+  const int NH = g.NH, Fp = g.Fp, F4 = Fp / 4, S2 = 2 * NH;
+  // per-wave LDS: [64 src ids][64 x HSP edge weights][HSC den]
+  int* src_lds = (int*)(smem + wave * g.lds_row);
+  float* w_lds = (float*)(src_lds + 64);
+  float* den_lds = w_lds + 64 * HSP;
+  const float M = g.const_att ? 0.f : ord_to_float(*g.M_ord);
+  const bool drop = g.p_drop > 0.f;
+  const float drop_scale = drop ? 1.f / (1.f - g.p_drop) : 1.f;
+  const uint64_t seed = drop ? *g.seed : 0ull;
+  const float4* __restrict__ rows4 = (const float4*)g.rows;
+  const bool vq = li < F4;
+  const int off4 = vq ? li : 0;
+  float sdst[HSC], dnl[HSC];
+#pragma unroll
+  for (int h = 0; h < HSC; ++h) {
+    sdst[h] = g.const_att ? 0.f : g.S[n * S2 + NH + h0 + h];
+    dnl[h] = 0.f;
+  }
+  float4 acc[HSC];
+#pragma unroll
+  for (int h = 0; h < HSC; ++h) acc[h] = make_float4(0.f, 0.f, 0.f, 0.f);
+
+  for (int base = beg; base < end; base += 64) {
+    const int cnt = min(64, end - base);
+    const bool valid = lane < cnt;
+    const int e = base + min(lane, cnt - 1);
+    const int my_src = g.col[e];
+    {
+      float w[HSP];
+      const int64_t ep = drop ? (int64_t)g.perm[e] : 0;
+#pragma unroll
+      for (int h = 0; h < HSP; ++h) {
+        w[h] = 0.f;
+        if (h < HSC) {
+          const float ss = g.const_att ? 0.f : g.S[(int64_t)my_src * S2 + h0 + h];
+          float ex = g.const_att ? 1.f : att_exp(ss + sdst[h], M);
+          ex = valid ? ex : 0.f;
+          dnl[h] += ex;
+          w[h] = ex;
+          if (drop) w[h] = dropout_keep(seed, ep * NH + h0 + h, g.p_drop) ? ex * drop_scale : 0.f;
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < HSP; h += 4)
+        *(float4*)(w_lds + lane * HSP + h) = make_float4(w[h], w[h + 1], w[h + 2], w[h + 3]);
+      src_lds[lane] = my_src;
+    }
+    wave_lds_sync();
+    for (int j0 = grp; j0 < cnt; j0 += EPW * U) {
+      int sv[U];
+      bool live[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int j = j0 + u * EPW;
+        live[u] = j < cnt;
+        sv[u] = src_lds[live[u] ? j : cnt - 1];
+      }
+      float4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = rows4[(int64_t)sv[u] * g.row_stride4 + off4];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int j = live[u] ? j0 + u * EPW : 0;
+        float wv[HSP];
+#pragma unroll
+        for (int h = 0; h < HSP; h += 4) {
+          const float4 t = *(const float4*)(w_lds + j * HSP + h);
+          wv[h] = t.x; wv[h + 1] = t.y; wv[h + 2] = t.z; wv[h + 3] = t.w;
+        }
+#pragma unroll
+        for (int h = 0; h < HSC; ++h) acc[h] = fma4(live[u] ? wv[h] : 0.f, v[u], acc[h]);
+      }
+    }
+    wave_lds_sync();
+  }
+#pragma unroll
+  for (int h = 0; h < HSC; ++h) {
+    float t = dnl[h];
+    for (int o = 1; o < 64; o <<= 1) t += __shfl_xor(t, o);
+    dnl[h] = t;
+  }
+#pragma unroll
+  for (int o = LPE; o < 64; o <<= 1) {
+#pragma unroll
+    for (int h = 0; h < HSC; ++h) acc[h] = add4(acc[h], shfl_xor4(acc[h], o));
+  }
+  if (hub_slot >= 0) {   // one piece of a hub: the generic partial layout
+    float* part = g.hub_part + (hub_slot * NG + hgl) * (int64_t)(HSC * Fp + HSC);
+    if (grp == 0 && vq) {
+#pragma unroll
+      for (int h = 0; h < HSC; ++h) *(float4*)(part + h * Fp + 4 * li) = acc[h];
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int h = 0; h < HSC; ++h) part[HSC * Fp + h] = dnl[h];
+    }
+    return;
+  }
+  if (grp == 0 && vq) {
+    float* orow = g.out + n * g.out_ld;
+#pragma unroll
+    for (int h = 0; h < HSC; ++h) {
+      const float4 o = acc[h] * (1.f / (dnl[h] + kSoftmaxEps));
+      const int64_t cb = (int64_t)(h0 + h) * g.F + 4 * li;
+      if (g.vec_out) {
+        *(float4*)(orow + cb) = o;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (4 * li + j < g.F) orow[cb + j] = get4(o, j);
+      }
+    }
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int h = 0; h < HSC; ++h) g.den[n * NH + h0 + h] = dnl[h];
+  }
+  (void)den_lds;
+}
+
 // Sum a hub's pieces (slots first .. first + pieces - 1, in that order) and finish the item:
 // one wave per (hub, head group), the lane layout of edge_forward_kernel<LPE, CPL>.
 template <int LPE, int CPL>
@@ -589,6 +757,54 @@ __global__ void __launch_bounds__(256) waug_assemble_kernel(const float* __restr
       const int h2 = (int)(r - Dp);
       v = 0.f;
       for (int cb = 0; cb < n_cb; ++cb) v += partial[((int64_t)cb * H2 + h2) * F_in + i];
+    }
+    W_aug[t] = v;
+  }
+}
+
+// W_aug in ONE launch for small layers (D = NH*F <= 256): the score rows' sums over all D rows
+// of W per element instead of split-K partials + assembly (two launches, small layers are
+// launch-bound): one sequential fma chain over c per element — deterministic, and within fp32
+// rounding of the split path.
+__global__ void __launch_bounds__(256) waug_direct_kernel(const float* __restrict__ W,
+                                                          const float* __restrict__ a, int NH,
+                                                          int F, int Fp, int H2, int64_t F_in,
+                                                          float* __restrict__ W_aug,
+                                                          const float* __restrict__ W_skip,
+                                                          int skip_heads, int64_t skip_cols) {
+  const int64_t Dp = (int64_t)NH * Fp;
+  const int D = NH * F;
+  const int64_t nmain = (Dp + H2) * F_in, sk = skip_cols * F_in;
+  const int64_t total = nmain + sk;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = t / F_in, i = t - r * F_in;
+    float v;
+    if (t >= nmain) {
+      const int64_t q = t - nmain;
+      v = W_skip[q];
+      for (int h = 1; h < skip_heads; ++h) v += W_skip[(int64_t)h * sk + q];
+      if (skip_heads > 1) v /= (float)skip_heads;
+    } else if (r < Dp) {
+      const int h = (int)(r / Fp), f = (int)(r - (int64_t)h * Fp);
+      v = (f < F) ? W[((int64_t)h * F + f) * F_in + i] : 0.f;
+    } else {
+      const int h2 = (int)(r - Dp);
+      const int hh = h2 < NH ? h2 : h2 - NH;
+      const float* ah = a + (int64_t)hh * 2 * D + (h2 < NH ? 0 : F);
+      // four independent chains (loads in flight), combined in a fixed order
+      float v4[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int c0 = 0; c0 < D; c0 += 4) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int c = c0 + j;
+          if (c < D) {
+            const int k = c / F, f = c - k * F;
+            v4[j] = fmaf(ah[k * 2 * F + f], W[(int64_t)c * F_in + i], v4[j]);
+          }
+        }
+      }
+      v = (v4[0] + v4[1]) + (v4[2] + v4[3]);
     }
     W_aug[t] = v;
   }
@@ -951,6 +1167,12 @@ extern "C" int gatx_prepare_weights_skip(const float* W, const float* a, int NH,
   GATX_REQUIRE(H2 <= kMaxH2, "prepare_weights: num_heads > %d unsupported", kMaxH2 / 2);
   const int D = NH * F;
   const int n_cb = (int)ceil_div(D, kWeffRows);
+  if (D <= 256) {   // small layers: one launch (launch-bound at PATTERN size)
+    waug_direct_kernel<<<grid_for(((int64_t)NH * Fp + H2 + skip_cols) * F_in), 256, 0, st>>>(
+        W, a, NH, F, Fp, H2, F_in, W_aug, W_skip, skip_heads, skip_cols);
+    GATX_LAUNCH_CHECK("waug_direct");
+    return 0;
+  }
   float* partial = nullptr;
   if (H2) {
     // split-K partials are staged in the tail of the caller's buffer, which holds
@@ -1040,7 +1262,11 @@ extern "C" int gatx_attention_alpha(const int32_t* col, const int32_t* rowidx,
     else attention_alpha_kernel<C, false><<<grid, 256, 0, st>>>(                               \
         col, rowidx, perm, E2, S, M_ord, den, NH, alpha, (long long*)argmax);                  \
   } while (0)
-  switch (NH) {
+  // the head-count variants load score / den rows and store alpha rows as vectors: only for
+  // 16-byte aligned buffers (an offset view falls back to the scalar variant)
+  const bool al = ((uintptr_t)S % 16) == 0 && ((uintptr_t)den % 16) == 0 &&
+                  ((uintptr_t)alpha % 16) == 0;
+  switch (al ? NH : 0) {
     case 1: GATX_AL(1); break; case 2: GATX_AL(2); break; case 4: GATX_AL(4); break;
     case 6: GATX_AL(6); break; case 8: GATX_AL(8); break; default: GATX_AL(0); break;
   }
@@ -1206,6 +1432,54 @@ extern "C" int gatx_edge_forward_drop(
   const int64_t blocks = g.hub_blocks + ceil_div(g.n_items_main, 4);
   GATX_REQUIRE(blocks < (1ll << 31), "edge_forward: too many work items");
   const unsigned grid = (unsigned)blocks;
+  // rows shared by every head (the reassociated first layer): one lane per chunk for all heads
+  static const bool shared_on = [] {   // A/B switch: GATX_SHARED_ROWS=0 keeps the generic kernel
+    const char* e = getenv("GATX_SHARED_ROWS");
+    return !(e && e[0] == '0');
+  }();
+  if (shared_on && head_stride == 0 && concat && !resid && !elu && !bias && out_p == 0.f &&
+      Fp / 4 <= 64 && (HS == 1 || HS == 2 || HS == 4 || HS == 8)) {
+    int lpe = 1;
+    while (lpe < Fp / 4) lpe <<= 1;
+    EdgeFwdArgs gs = g;
+    const int hsp = HS <= 4 ? 4 : 8;
+    gs.lds_row = 64 + 64 * hsp + 8;
+    const size_t slds = (size_t)4 * gs.lds_row * sizeof(float);
+#define GATX_SH(L)                                                                             \
+  do {                                                                                         \
+    if (HS == 1) edge_forward_shared_kernel<L, 1><<<grid, 256, slds, st>>>(gs);                \
+    else if (HS == 2) edge_forward_shared_kernel<L, 2><<<grid, 256, slds, st>>>(gs);           \
+    else if (HS == 4) edge_forward_shared_kernel<L, 4><<<grid, 256, slds, st>>>(gs);           \
+    else edge_forward_shared_kernel<L, 8><<<grid, 256, slds, st>>>(gs);                        \
+  } while (0)
+    switch (lpe) {
+      case 1: GATX_SH(1); break; case 2: GATX_SH(2); break; case 4: GATX_SH(4); break;
+      case 8: GATX_SH(8); break; case 16: GATX_SH(16); break; case 32: GATX_SH(32); break;
+      default: GATX_SH(64); break;
+    }
+#undef GATX_SH
+    GATX_LAUNCH_CHECK("edge_forward_shared");
+    if (g.hub_T > 0) {   // the generic combine over the generic partial layout
+      const unsigned cg = (unsigned)ceil_div(g.hub_bound * g.g_count, 4);
+#define GATX_HC(L, C) edge_hub_combine_kernel<L, C><<<cg, 256, lds, st>>>(g)
+      if (rg.lpe == 64) {
+        switch (rg.cpl) {
+          case 1: GATX_HC(64, 1); break; case 2: GATX_HC(64, 2); break;
+          case 3: GATX_HC(64, 3); break; case 4: GATX_HC(64, 4); break;
+          case 5: GATX_HC(64, 5); break; case 6: GATX_HC(64, 6); break;
+          case 7: GATX_HC(64, 7); break; default: GATX_HC(64, 8); break;
+        }
+      } else {
+        switch (rg.lpe) {
+          case 1: GATX_HC(1, 1); break; case 2: GATX_HC(2, 1); break; case 4: GATX_HC(4, 1); break;
+          case 8: GATX_HC(8, 1); break; case 16: GATX_HC(16, 1); break; default: GATX_HC(32, 1); break;
+        }
+      }
+#undef GATX_HC
+      GATX_LAUNCH_CHECK("edge_hub_combine");
+    }
+    return 0;
+  }
 #define GATX_EF(L, C) return launch_edge_forward<L, C>(grid, lds, st, g)
   if (rg.lpe == 64) {
     switch (rg.cpl) {

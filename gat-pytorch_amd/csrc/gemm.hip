@@ -21,8 +21,6 @@
 
 #include <string.h>
 
-#include <string.h>
-
 namespace gatx {
 namespace {
 using namespace gk;
@@ -37,6 +35,59 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(GemmArgs g, int batc
     for (int z = 0; z < g.splits; ++z) v += g.partial[((int64_t)z * batch + b) * MN + mn];
     store_out(g, b, row, col, v);
   }
+}
+
+// Tiny products (M N K <= 2^25 multiply-adds: PATTERN's layers, the weight gradients of small
+// batches) on the VALU in plain fp32: the tiled MFMA kernels spend 10-14 us there on prologue,
+// barriers and a handful of K-tiles for a few MFLOP, while this is launch-bound (~3 us). Each
+// output (b, m, n) is owned by a group of L lanes splitting K (k = li, li + L, ...; fma chain per
+// lane, then a fixed-order group_sum<L>), so the result is deterministic and fp32-faithful (exact
+// fp32 products). Control flow is wave-uniform: a wave walks its outputs together and the lanes
+// of finished groups contribute zeros.
+template <int L>
+__global__ void __launch_bounds__(256) gemm_tiny_kernel(GemmArgs g, int batch, int a_kc,
+                                                        int b_kc) {
+  constexpr int GPW = 64 / L;   // output groups per wave
+  const int64_t MN = g.M * g.N, total = MN * batch;
+  const int lane = threadIdx.x & 63, grp = lane / L, li = lane % L;
+  const int64_t wave = blockIdx.x * 4ll + (threadIdx.x >> 6), nwaves = gridDim.x * 4ll;
+  for (int64_t base = wave * GPW; base < total; base += nwaves * GPW) {
+    const int64_t o = base + grp;
+    const bool valid = o < total;
+    const int64_t oc = valid ? o : total - 1;
+    const int64_t b = oc / MN, mn = oc - b * MN, m = mn / g.N, n = mn - m * g.N;
+    const float* __restrict__ A = g.A + b * g.a_bs;
+    const float* __restrict__ B = g.B + b * g.b_bs;
+    float acc = 0.f;
+    if (valid) {
+      for (int64_t k = li; k < g.K; k += L) {
+        const float av = a_kc ? A[m * g.lda + k] : A[k * g.lda + m];
+        const float bv = b_kc ? B[n * g.ldb + k] : B[k * g.ldb + n];
+        acc = fmaf(av, bv, acc);
+      }
+    }
+    acc = group_sum<L>(acc);
+    if (valid && li == 0) store_out(g, b, m, n, acc);
+  }
+}
+
+int launch_gemm_tiny(const GemmArgs& g, int batch, bool a_kc, bool b_kc, hipStream_t stream) {
+  const int64_t total = g.M * g.N * batch;
+  int64_t L = 1;
+  while (L < 64 && total * L * 2 <= (1 << 17) && L < g.K) L <<= 1;   // ~2^17 lanes busy
+  const int64_t groups_per_block = 256 / L;
+  const unsigned grid = (unsigned)std::max<int64_t>(
+      1, std::min<int64_t>(ceil_div(total, groups_per_block), 4096));
+#define GATX_TINY(LL) \
+  gemm_tiny_kernel<LL><<<grid, 256, 0, stream>>>(g, batch, (int)a_kc, (int)b_kc)
+  switch (L) {
+    case 1: GATX_TINY(1); break; case 2: GATX_TINY(2); break; case 4: GATX_TINY(4); break;
+    case 8: GATX_TINY(8); break; case 16: GATX_TINY(16); break; case 32: GATX_TINY(32); break;
+    default: GATX_TINY(64); break;
+  }
+#undef GATX_TINY
+  GATX_LAUNCH_CHECK("gemm_tiny");
+  return 0;
 }
 
 // Tail fix-up: the last tail_rem tiles, each the sum of tail_s K-slices in slice order.
@@ -399,6 +450,15 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
   };
   g.a_vec = aligned(A, g.lda, a_bs);
   g.b_vec = aligned(B, g.ldb, b_bs);
+  static const bool tiny_on = [] {   // A/B switch: GATX_TINY_GEMM=0 keeps the MFMA kernels
+    const char* e = getenv("GATX_TINY_GEMM");
+    return !(e && strcmp(e, "0") == 0);
+  }();
+  if (tiny_on && M * N * K * batch <= (int64_t(1) << 25)) {
+    g.splits = 1; g.tail_s = 1; g.tiles_m = g.tiles_n = 1; g.dp_blocks = g.tail_rem = 0;
+    g.bm = g.bn = 32; g.tail_partial = nullptr;
+    return launch_gemm_tiny(g, batch, a_kc, b_kc, stream);
+  }
   static const bool smallk_on = [] {   // A/B switch: GATX_SMALLK=0 keeps the tiled kernel
     const char* e = getenv("GATX_SMALLK");
     return !(e && strcmp(e, "0") == 0);

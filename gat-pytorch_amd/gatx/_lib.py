@@ -105,6 +105,9 @@ SIGNATURES = {
                                      P, P, P, P, P, c_i64, P]),
     "gatx_weight_grads": (c_i, [P, P, P, c_i, c_i, c_i64, P, P, P]),
     "gatx_colsum": (c_i, [P, c_i64, c_i64, c_i64, P, P]),
+    "gatx_bce_logits_workspace_bytes": (c_sz, []),
+    "gatx_bce_logits": (c_i, [P, P, c_i64, c_f, P, P, P, P]),
+    "gatx_scale_by_scalar": (c_i, [P, P, c_i64, P, P]),
     "gatx_attention_norm_workspace_bytes": (c_sz, []),
     "gatx_attention_norm": (c_i, [P, c_i64, c_i, P, c_i, P, c_f, c_i, P, P, P]),
     "gatx_attention_norm_backward": (c_i, [P, c_i64, c_i, P, c_i, P, P, c_f, P, P]),

@@ -377,6 +377,7 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
         with _span("attention_alpha", (E2, sh.NH)):
             _attention_alpha(graph, S, M_ord, den, sh, alpha, argmax, s)
         Wp = padded_weight(W, Fin_p, sh.cache_weights)   # float4-readable rows
+        saved["Wp"] = Wp   # the backward's batched GEMMs read the same padded copy
         with _span("gemm_out", (N, sh.F, sh.F_in, sh.NH)):
             call("gatx_gemm_f32_batched", sh.NH, N, sh.F, sh.F_in, ptr(Z), sh.NH * Fin_p, 1,
                  Fin_p, ptr(Wp), 1, Fin_p, sh.F * Fin_p, ptr(out), sh.NH * sh.F, sh.F, 0,
@@ -504,13 +505,18 @@ def layer_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShape, 
     fold = resid_is_x and need_x and g_pre is not None
     if need_x:
         g_x = g_pre if fold else torch.empty((N, sh.F_in), **f32)
-        # W_aug^T (F_in x K_aug, 4 MB at PPI): both GEMM operands k-contiguous (the n-contiguous
-        # B staging of W_aug as stored ran this product ~25% slower)
-        W_augT = torch.empty((sh.F_in, ldg), **f32)
-        call("gatx_transpose_f32", KC, sh.F_in, ptr(W_aug), sh.F_in, ptr(W_augT), ldg, s)
-        call("gatx_gemm_f32", N, sh.F_in, KC, ptr(G_aug), ldg, 1, ptr(W_augT), 1,
-             ldg, ptr(g_x), sh.F_in, sh.F_in, None, 0, int(fold),
-             *gemm_workspace(N, sh.F_in, KC, dev), s)
+        if N * sh.F_in * KC >= (1 << 27):
+            # W_aug^T (F_in x K_aug, 4 MB at PPI): both GEMM operands k-contiguous (the
+            # n-contiguous B staging of W_aug as stored ran this product ~25% slower)
+            W_augT = torch.empty((sh.F_in, ldg), **f32)
+            call("gatx_transpose_f32", KC, sh.F_in, ptr(W_aug), sh.F_in, ptr(W_augT), ldg, s)
+            call("gatx_gemm_f32", N, sh.F_in, KC, ptr(G_aug), ldg, 1, ptr(W_augT), 1,
+                 ldg, ptr(g_x), sh.F_in, sh.F_in, None, 0, int(fold),
+                 *gemm_workspace(N, sh.F_in, KC, dev), s)
+        else:   # small layers are launch-bound: read W_aug as stored (no transpose launch)
+            call("gatx_gemm_f32", N, sh.F_in, KC, ptr(G_aug), ldg, 1, ptr(W_aug), sh.F_in,
+                 1, ptr(g_x), sh.F_in, sh.F_in, None, 0, int(fold),
+                 *gemm_workspace(N, sh.F_in, KC, dev), s)
     if need_W or need_a or need_skip:
         gW_aug = torch.empty((KC, sh.F_in), **f32)
         ws_bytes = lib.gatx_gemm_splitk_workspace_bytes(KC, sh.F_in, N)
@@ -561,7 +567,9 @@ def _reassoc_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShap
         pre_p = ptr(g_pre)
     call("gatx_prepare_go_ex", ptr(g_out), ptr(out) if elu else None, N, NH, F, 1, int(elu),
          ptr(go), pre_p, pre_ld, 0.0, None, s)
-    Wp = padded_weight(W, Fin_p, sh.cache_weights)    # [NH*F][Fin_p], zero tail
+    Wp = saved.get("Wp")    # [NH*F][Fin_p], zero tail: the forward's copy
+    if Wp is None:
+        Wp = padded_weight(W, Fin_p, sh.cache_weights)
     g_Z = torch.empty((N, NH * Fin_p), **f32)
     call("gatx_gemm_f32_batched", NH, N, Fin_p, F, ptr(go), sh.Dp, 1, Fp, ptr(Wp), Fin_p, 1,
          F * Fin_p, ptr(g_Z), NH * Fin_p, Fin_p, 0, None, 0, None, 0, 0, 0, s)
@@ -614,6 +622,9 @@ class GATLayerFunction(torch.autograd.Function):
         ctx.resid_is_x = resid is not None and resid is x
         ctx.has_skip = skip_W is not None
         ctx.save_for_backward(x, W, a, bias, out if elu else None, skip_W)
+        # an unused output (alpha, when only out feeds the loss) arrives as None in backward
+        # instead of a materialised (E', NH) zero tensor: no fill launch, no zero reads
+        ctx.set_materialize_grads(False)
         return out, alpha
 
     @staticmethod

@@ -432,6 +432,18 @@ int gatx_attention_norm_backward(const float* alpha, int64_t E2, int NH, const v
                                  int dst_is64, const int32_t* rowptr, const float* g,
                                  float scale, float* g_alpha, gatx_stream_t stream);
 
+/* ---- the task modules' loss (models/ppi_gat.py:11,19; models/pattern_gat.py:11-15) ---- */
+/* BCEWithLogitsLoss, mean reduction, pos_weight (1 = none): loss[0] = mean over n of
+ * (1 - y) x + lw softplus(-x), lw = 1 + (pos_weight - 1) y; grad[i] = d loss / d x[i] =
+ * (lw sigmoid(x) - pos_weight y) / n, written by the same pass for the backward. One launch for
+ * n <= 65536, two above (workspace: gatx_bce_logits_workspace_bytes()). Fixed-order sums. */
+size_t gatx_bce_logits_workspace_bytes(void);
+int gatx_bce_logits(const float* x, const float* y, int64_t n, float pos_weight, float* loss,
+                    float* grad, void* workspace, gatx_stream_t stream);
+/* out[i] = g[0] * v[i] (g a device scalar: the loss's upstream gradient). */
+int gatx_scale_by_scalar(const float* g, const float* v, int64_t n, float* out,
+                         gatx_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

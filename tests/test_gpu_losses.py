@@ -1,0 +1,40 @@
+"""gatx.losses.bce_with_logits (csrc/loss.hip) against torch's binary_cross_entropy_with_logits —
+the task modules' loss (PPI_GAT `models/ppi_gat.py:11,19`; PatternGAT with pos_weight
+`models/pattern_gat.py:11-15`): loss value and input gradient, one-launch and two-launch sizes,
+extreme logits, bitwise repeatability."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("n", [1, 952, 65536, 65537, 44900 * 121])
+@pytest.mark.parametrize("pw", [None, 1 / 0.1765])
+def test_bce_matches_torch(n, pw, device):
+    from gatx.losses import bce_with_logits
+    g = torch.Generator(device=device).manual_seed(n)
+    x = (torch.randn(n, device=device, generator=g) * 6).requires_grad_(True)
+    x.data[: min(n, 4)] = torch.tensor([80.0, -80.0, 0.0, 1e-3], device=device)[: min(n, 4)]
+    y = (torch.rand(n, device=device, generator=g) > 0.5).float()
+    pwt = None if pw is None else torch.tensor([pw], device=device)
+    ref = torch.nn.functional.binary_cross_entropy_with_logits(x.double(), y.double(),
+                                                               pos_weight=pwt and pwt.double())
+    gref, = torch.autograd.grad(ref, x)
+    x2 = x.detach().clone().requires_grad_(True)
+    got = bce_with_logits(x2, y, pw)
+    (got * 3.0).backward()
+    assert abs(got.item() - ref.item()) <= 1e-5 * max(1.0, abs(ref.item()))
+    err = (x2.grad.double() - 3.0 * gref).abs().max().item()
+    assert err <= 1e-6 * max(1.0, (3.0 * gref).abs().max().item()) + 1e-9, err
+    # fixed-order reductions: a second evaluation is bitwise identical
+    again = bce_with_logits(x2.detach(), y, pw)
+    assert again.item() == got.item()
+
+
+def test_bce_module_and_shape_check(device):
+    from gatx.losses import BCEWithLogitsLoss
+    loss = BCEWithLogitsLoss(pos_weight=torch.tensor([2.0]))
+    x = torch.zeros(3, 4, device=device)
+    assert abs(loss(x, torch.ones(3, 4, device=device)).item() - 2.0 * 0.6931471805599453) < 1e-6
+    with pytest.raises(ValueError):
+        loss(x, torch.ones(4, 3, device=device))
