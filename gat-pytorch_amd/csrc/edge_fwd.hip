@@ -762,52 +762,54 @@ __global__ void __launch_bounds__(256) waug_assemble_kernel(const float* __restr
   }
 }
 
-// W_aug in ONE launch for small layers (D = NH*F <= 256): the score rows' sums over all D rows
-// of W per element instead of split-K partials + assembly (two launches, small layers are
-// launch-bound): one sequential fma chain over c per element — deterministic, and within fp32
-// rounding of the split path.
+// W_aug in ONE launch for small layers (D = NH*F <= 256; split-K partials + assembly are two
+// launches, and small layers are launch-bound). Blocks [0, ncopy) copy the head-padded W rows
+// (and the folded skip's rows); the blocks after them give each score-row element
+// W_aug[Dp + h2][i] = sum_c A2[h2][c] W[c][i] one wave, lanes over c, fixed-order wave sum.
 __global__ void __launch_bounds__(256) waug_direct_kernel(const float* __restrict__ W,
                                                           const float* __restrict__ a, int NH,
                                                           int F, int Fp, int H2, int64_t F_in,
-                                                          float* __restrict__ W_aug,
+                                                          int ncopy, float* __restrict__ W_aug,
                                                           const float* __restrict__ W_skip,
                                                           int skip_heads, int64_t skip_cols) {
   const int64_t Dp = (int64_t)NH * Fp;
   const int D = NH * F;
-  const int64_t nmain = (Dp + H2) * F_in, sk = skip_cols * F_in;
-  const int64_t total = nmain + sk;
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = t / F_in, i = t - r * F_in;
-    float v;
-    if (t >= nmain) {
-      const int64_t q = t - nmain;
-      v = W_skip[q];
-      for (int h = 1; h < skip_heads; ++h) v += W_skip[(int64_t)h * sk + q];
-      if (skip_heads > 1) v /= (float)skip_heads;
-    } else if (r < Dp) {
-      const int h = (int)(r / Fp), f = (int)(r - (int64_t)h * Fp);
-      v = (f < F) ? W[((int64_t)h * F + f) * F_in + i] : 0.f;
-    } else {
-      const int h2 = (int)(r - Dp);
-      const int hh = h2 < NH ? h2 : h2 - NH;
-      const float* ah = a + (int64_t)hh * 2 * D + (h2 < NH ? 0 : F);
-      // four independent chains (loads in flight), combined in a fixed order
-      float v4[4] = {0.f, 0.f, 0.f, 0.f};
-      for (int c0 = 0; c0 < D; c0 += 4) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int c = c0 + j;
-          if (c < D) {
-            const int k = c / F, f = c - k * F;
-            v4[j] = fmaf(ah[k * 2 * F + f], W[(int64_t)c * F_in + i], v4[j]);
-          }
-        }
+  if ((int)blockIdx.x < ncopy) {
+    const int64_t ncp = Dp * F_in, sk = skip_cols * F_in;
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < ncp + sk;
+         t += (int64_t)ncopy * blockDim.x) {
+      float v;
+      int64_t dst;
+      if (t >= ncp) {   // folded skip rows: mean over the skip's head blocks (a copy for 1)
+        const int64_t q = t - ncp;
+        v = W_skip[q];
+        for (int h = 1; h < skip_heads; ++h) v += W_skip[(int64_t)h * sk + q];
+        if (skip_heads > 1) v /= (float)skip_heads;
+        dst = (Dp + H2) * F_in + q;
+      } else {
+        const int64_t r = t / F_in, i = t - r * F_in;
+        const int h = (int)(r / Fp), f = (int)(r - (int64_t)h * Fp);
+        v = (f < F) ? W[((int64_t)h * F + f) * F_in + i] : 0.f;
+        dst = t;
       }
-      v = (v4[0] + v4[1]) + (v4[2] + v4[3]);
+      W_aug[dst] = v;
     }
-    W_aug[t] = v;
+    return;
   }
+  const int lane = threadIdx.x & 63;
+  const int64_t o = ((int64_t)blockIdx.x - ncopy) * 4 + (threadIdx.x >> 6);
+  if (o >= (int64_t)H2 * F_in) return;
+  const int h2 = (int)(o / F_in);
+  const int64_t i = o - (int64_t)h2 * F_in;
+  const int hh = h2 < NH ? h2 : h2 - NH;
+  const float* ah = a + (int64_t)hh * 2 * D + (h2 < NH ? 0 : F);
+  float v = 0.f;
+  for (int c = lane; c < D; c += 64) {
+    const int k = c / F, f = c - k * F;
+    v = fmaf(ah[k * 2 * F + f], W[(int64_t)c * F_in + i], v);
+  }
+  v = group_sum<64>(v);
+  if (lane == 0) W_aug[(Dp + h2) * F_in + i] = v;
 }
 
 // Its gradient: g_W[(h * cols + c)][i] = g_eff[c][i] / heads for every head block.
@@ -1168,8 +1170,11 @@ extern "C" int gatx_prepare_weights_skip(const float* W, const float* a, int NH,
   const int D = NH * F;
   const int n_cb = (int)ceil_div(D, kWeffRows);
   if (D <= 256) {   // small layers: one launch (launch-bound at PATTERN size)
-    waug_direct_kernel<<<grid_for(((int64_t)NH * Fp + H2 + skip_cols) * F_in), 256, 0, st>>>(
-        W, a, NH, F, Fp, H2, F_in, W_aug, W_skip, skip_heads, skip_cols);
+    const int ncopy = (int)grid_for(((int64_t)NH * Fp + skip_cols) * F_in, 256, 1024);
+    const int64_t nscore = ceil_div((int64_t)H2 * F_in, 4);
+    GATX_REQUIRE(ncopy + nscore < (1ll << 31), "prepare_weights: too many blocks");
+    waug_direct_kernel<<<(unsigned)(ncopy + nscore), 256, 0, st>>>(
+        W, a, NH, F, Fp, H2, F_in, ncopy, W_aug, W_skip, skip_heads, skip_cols);
     GATX_LAUNCH_CHECK("waug_direct");
     return 0;
   }

@@ -37,8 +37,8 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(GemmArgs g, int batc
   }
 }
 
-// Tiny products (M N K <= 2^25 multiply-adds: PATTERN's layers, the weight gradients of small
-// batches) on the VALU in plain fp32: the tiled MFMA kernels spend 10-14 us there on prologue,
+// Tiny products (K <= 64, M N K <= 2^25 multiply-adds: PATTERN's projections) on the VALU in
+// plain fp32: the tiled MFMA kernels spend 10-14 us there on prologue,
 // barriers and a handful of K-tiles for a few MFLOP, while this is launch-bound (~3 us). Each
 // output (b, m, n) is owned by a group of L lanes splitting K (k = li, li + L, ...; fma chain per
 // lane, then a fixed-order group_sum<L>), so the result is deterministic and fp32-faithful (exact
@@ -60,6 +60,7 @@ __global__ void __launch_bounds__(256) gemm_tiny_kernel(GemmArgs g, int batch, i
     const float* __restrict__ B = g.B + b * g.b_bs;
     float acc = 0.f;
     if (valid) {
+#pragma unroll 4
       for (int64_t k = li; k < g.K; k += L) {
         const float av = a_kc ? A[m * g.lda + k] : A[k * g.lda + m];
         const float bv = b_kc ? B[n * g.ldb + k] : B[k * g.ldb + n];
@@ -73,8 +74,11 @@ __global__ void __launch_bounds__(256) gemm_tiny_kernel(GemmArgs g, int batch, i
 
 int launch_gemm_tiny(const GemmArgs& g, int batch, bool a_kc, bool b_kc, hipStream_t stream) {
   const int64_t total = g.M * g.N * batch;
+  // lanes per output: at most ~12 k per lane (the loop is load-latency bound), more while the
+  // chip is short of lanes (< 2^16 busy), never more than K
   int64_t L = 1;
-  while (L < 64 && total * L * 2 <= (1 << 17) && L < g.K) L <<= 1;   // ~2^17 lanes busy
+  while (L < 64 && L * 12 < g.K) L <<= 1;
+  while (L < 64 && total * L < (1 << 16) && L < g.K) L <<= 1;
   const int64_t groups_per_block = 256 / L;
   const unsigned grid = (unsigned)std::max<int64_t>(
       1, std::min<int64_t>(ceil_div(total, groups_per_block), 4096));
@@ -454,7 +458,9 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
     const char* e = getenv("GATX_TINY_GEMM");
     return !(e && strcmp(e, "0") == 0);
   }();
-  if (tiny_on && M * N * K * batch <= (int64_t(1) << 25)) {
+  // (only short K: every output re-reads its A row and B column, so a long K turns the VALU
+  // kernel TA-bound — PATTERN's K = 952-node weight gradients ran 28 us vs 12 us tiled)
+  if (tiny_on && K <= 64 && M * N * K * batch <= (int64_t(1) << 25)) {
     g.splits = 1; g.tail_s = 1; g.tiles_m = g.tiles_n = 1; g.dp_blocks = g.tail_rem = 0;
     g.bm = g.bn = 32; g.tail_partial = nullptr;
     return launch_gemm_tiny(g, batch, a_kc, b_kc, stream);

@@ -25,14 +25,22 @@ __device__ inline int64_t ld_idx(const void* p, int64_t i) {
 }
 
 constexpr int kStatsBlocks = 1024;
+// stats / compaction block ranges: >= 256 blocks' worth of input when there is enough, at most
+// kStatsBlocks, each a multiple of 256 edges
+inline int64_t stats_chunk(int64_t E) {
+  return std::max<int64_t>(256, round_up(ceil_div(E > 0 ? E : 1, kStatsBlocks), 256));
+}
+inline int stats_blocks(int64_t E) { return (int)ceil_div(E > 0 ? E : 1, stats_chunk(E)); }
 
-// Per-block {min, max, self-loops} partials (no 64-bit atomics), reduced by graph_meta_kernel.
+// Per-block {min, max, self-loops, kept edges} partials (no 64-bit atomics), reduced by
+// graph_meta_kernel. Block b covers the contiguous input range [b chunk, (b+1) chunk) so that
+// its kept-edge count is the block's share of the compaction (graph_meta_kernel scans them).
 template <typename I>
 __global__ void __launch_bounds__(256) edge_stats_kernel(const void* ei, int64_t E, int64_t ld,
-                                                         long long* part) {
+                                                         int64_t chunk, long long* part) {
   long long mn = LLONG_MAX, mx = LLONG_MIN, loops = 0;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < E;
-       i += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t lo = (int64_t)blockIdx.x * chunk, hi = min(E, lo + chunk);
+  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
     long long s = ld_idx<I>(ei, i), d = ld_idx<I>(ei, ld + i);
     mn = min(mn, min(s, d));
     mx = max(mx, max(s, d));
@@ -51,22 +59,25 @@ __global__ void __launch_bounds__(256) edge_stats_kernel(const void* ei, int64_t
     for (int k = 1; k < (int)(blockDim.x >> 6); ++k) {
       mn = min(mn, red[0][k]); mx = max(mx, red[1][k]); loops += red[2][k];
     }
-    part[3 * blockIdx.x + 0] = mn;
-    part[3 * blockIdx.x + 1] = mx;
-    part[3 * blockIdx.x + 2] = loops;
+    part[4 * blockIdx.x + 0] = mn;
+    part[4 * blockIdx.x + 1] = mx;
+    part[4 * blockIdx.x + 2] = loops;
+    part[4 * blockIdx.x + 3] = (hi > lo ? hi - lo : 0) - loops;   // kept by the rewrite
   }
 }
 
 // Device-side sizing of the rewrite from the stats partials: meta = {E2, num_loops, status, min,
-// max, n_selfloops, 0, 0}. status 1 / 2 (a negative id / an id >= num_nodes) zeroes E2 and
-// num_loops, so every later kernel sees an empty graph and nothing indexes out of bounds; the
-// host raises when it reads the meta (the reference raises in index_select / scatter_add_).
+// max, n_selfloops, nb, chunk} followed by the exclusive scan of the blocks' kept-edge counts
+// (int32, meta + 8: the compaction's block offsets). status 1 / 2 (a negative id / an id >=
+// num_nodes) zeroes E2 and num_loops, so every later kernel sees an empty graph and nothing
+// indexes out of bounds; the host raises when it reads the meta (the reference raises in
+// index_select / scatter_add_).
 __global__ void __launch_bounds__(256) graph_meta_kernel(const long long* part, int nb, int64_t E,
-                                                         int add_loops, int64_t num_nodes,
-                                                         long long* meta) {
+                                                         int64_t chunk, int add_loops,
+                                                         int64_t num_nodes, long long* meta) {
   long long mn = LLONG_MAX, mx = LLONG_MIN, loops = 0;
   for (int b = threadIdx.x; b < nb; b += blockDim.x) {
-    mn = min(mn, part[3 * b]); mx = max(mx, part[3 * b + 1]); loops += part[3 * b + 2];
+    mn = min(mn, part[4 * b]); mx = max(mx, part[4 * b + 1]); loops += part[4 * b + 2];
   }
   for (int o = 32; o > 0; o >>= 1) {
     mn = min(mn, (long long)__shfl_xor(mn, o));
@@ -74,9 +85,33 @@ __global__ void __launch_bounds__(256) graph_meta_kernel(const long long* part, 
     loops += __shfl_xor(loops, o);
   }
   __shared__ long long red[3][4];
+  __shared__ int wsum[4];
   int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   if (l == 0) { red[0][w] = mn; red[1][w] = mx; red[2][w] = loops; }
+  // block offsets of the compaction: thread t scans blocks [4t, 4t+4) (nb <= 1024)
+  int c[4], tot = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int b = 4 * threadIdx.x + j;
+    c[j] = b < nb ? (int)part[4 * b + 3] : 0;
+    tot += c[j];
+  }
+  int x = tot;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (l >= o) x += y;
+  }
+  if (l == 63) wsum[w] = x;
   __syncthreads();
+  int run = x - tot;
+  for (int k = 0; k < w; ++k) run += wsum[k];
+  int32_t* boff = (int32_t*)(meta + 8);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int b = 4 * threadIdx.x + j;
+    if (b < nb) boff[b] = run;
+    run += c[j];
+  }
   if (threadIdx.x == 0) {
     for (int k = 1; k < (int)(blockDim.x >> 6); ++k) {
       mn = min(mn, red[0][k]); mx = max(mx, red[1][k]); loops += red[2][k];
@@ -89,61 +124,74 @@ __global__ void __launch_bounds__(256) graph_meta_kernel(const long long* part, 
     if (status) { e2 = 0; num_loops = 0; }
     meta[0] = e2; meta[1] = num_loops; meta[2] = status;
     meta[3] = E > 0 ? mn : 0; meta[4] = E > 0 ? mx : -1; meta[5] = loops;
-    meta[6] = 0; meta[7] = 0;
+    meta[6] = nb; meta[7] = chunk;
   }
 }
 
-// keep flag of input edge i (1 = survives the self-loop rewrite)
-template <typename I>
-struct KeepFlag {
-  const void* ei;
-  int64_t ld;
-  int drop_loops;
-  __device__ int operator()(int64_t i) const {
-    return drop_loops ? (ld_idx<I>(ei, i) != ld_idx<I>(ei, ld + i)) : 1;
-  }
-};
-
-// One thread per input edge t < E, then one per slot q = t - E < E_bound:
-//  * input edge t: if it survives, (src, dst) goes to slot pos[t] (its rank among survivors);
-//  * slot q in [E2 - num_loops, E2): the loop (i, i), i = q - (E2 - num_loops);
-//  * slot q >= E2 (padding up to the allocation bound): sorts after every real key (dst = N).
+// The self-loop rewrite's compaction, stable, with no separate scan: blocks [0, nb) walk their
+// stats block's contiguous input range 256 edges at a time and place each surviving edge at
+// boff[b] + (kept edges before it in the range) (wave ballots + per-round wave totals in LDS);
+// the blocks after them fill slot q in [E2 - num_loops, E2) with the loop (i, i),
+// i = q - (E2 - num_loops), and the padding slots q >= E2 (dst = N: sorts after every real key).
 // edge_index' is written flat with its exact size: sources at [p], destinations at [E2 + p],
 // so edge_index'[:2*E2].view(2, E2) is the reference's contiguous (2, E') tensor.
 template <typename I>
 __global__ void __launch_bounds__(256) compact_kernel(const void* ei, int64_t E, int64_t ld,
-                                                       int drop_loops, const int32_t* pos,
-                                                       const long long* meta, int64_t E_bound,
-                                                       int64_t num_nodes, int64_t* ei_out,
-                                                       int32_t* src32, int32_t* dst32,
-                                                       int32_t* iota) {
+                                                       int drop_loops, const long long* meta,
+                                                       int64_t E_bound, int64_t num_nodes,
+                                                       int64_t* ei_out, int32_t* src32,
+                                                       int32_t* dst32, int32_t* iota) {
   const int64_t E2 = meta[0], num_loops = meta[1];
   const bool ok = meta[2] == 0;
-  const int64_t total = E + E_bound;
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    int64_t s, d, p;
-    if (t < E) {
-      if (!ok) continue;
-      s = ld_idx<I>(ei, t);
-      d = ld_idx<I>(ei, ld + t);
-      if (drop_loops && s == d) continue;
-      p = drop_loops ? pos[t] : t;
-    } else {
-      p = t - E;
-      if (p >= E2) {   // padding slot
-        src32[p] = 0;
-        dst32[p] = (int32_t)num_nodes;
-        iota[p] = (int32_t)p;
-        continue;
+  const int nb = (int)meta[6];
+  const int64_t chunk = meta[7];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if ((int)blockIdx.x < nb) {
+    if (!ok) return;
+    __shared__ int wtot[4];
+    int64_t run = ((const int32_t*)(meta + 8))[blockIdx.x];
+    const int64_t lo = (int64_t)blockIdx.x * chunk, hi = min(E, lo + chunk);
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (int64_t base = lo; base < hi; base += 256) {
+      const int64_t t = base + tid;
+      int64_t s = 0, d = 0;
+      bool keep = false;
+      if (t < hi) {
+        s = ld_idx<I>(ei, t);
+        d = ld_idx<I>(ei, ld + t);
+        keep = !drop_loops || s != d;
       }
-      if (p < E2 - num_loops) continue;   // a surviving input edge's slot
-      s = d = p - (E2 - num_loops);
+      const uint64_t bal = __ballot(keep);
+      if (lane == 0) wtot[wave] = __popcll(bal);
+      __syncthreads();
+      int64_t p = run + __popcll(bal & lt);
+      for (int k = 0; k < wave; ++k) p += wtot[k];
+      if (keep) {
+        if (ei_out) { ei_out[p] = s; ei_out[E2 + p] = d; }
+        src32[p] = (int32_t)s;
+        dst32[p] = (int32_t)d;
+        iota[p] = (int32_t)p;
+      }
+      run += wtot[0] + wtot[1] + wtot[2] + wtot[3];
+      __syncthreads();
     }
-    if (ei_out) { ei_out[p] = s; ei_out[E2 + p] = d; }
-    src32[p] = (int32_t)s;
-    dst32[p] = (int32_t)d;
-    iota[p] = (int32_t)p;
+    return;
+  }
+  const int64_t first = E2 - num_loops;   // loop and padding slots
+  for (int64_t q = first + ((int64_t)blockIdx.x - nb) * blockDim.x + tid; q < E_bound;
+       q += ((int64_t)gridDim.x - nb) * blockDim.x) {
+    if (q < 0) continue;
+    if (q >= E2) {   // padding slot
+      src32[q] = 0;
+      dst32[q] = (int32_t)num_nodes;
+      iota[q] = (int32_t)q;
+      continue;
+    }
+    const int64_t v = q - first;
+    if (ei_out) { ei_out[q] = v; ei_out[E2 + q] = v; }
+    src32[q] = (int32_t)v;
+    dst32[q] = (int32_t)v;
+    iota[q] = (int32_t)q;
   }
 }
 
@@ -381,6 +429,63 @@ __global__ void __launch_bounds__(256) radix_scatter_lds_kernel(
   }
 }
 
+// Exclusive scan of n uint32 in ONE 1024-thread block, for the radix sort's digit-major
+// histograms up to kScan1Max entries (rocPRIM's lookback scan is two launches, ~12 us, on these
+// sizes): tiles of 16 K entries are loaded coalesced into LDS (row-padded: thread t's 16
+// consecutive entries at stride 17, conflict-free), each thread scans its 16, a block scan over
+// the 1024 thread sums links them, and the tile goes back out coalesced with a running carry.
+constexpr int kScan1Per = 16, kScan1Tile = 1024 * kScan1Per;
+constexpr int64_t kScan1Max = 1 << 17;
+__global__ void __launch_bounds__(1024) scan1_kernel(const uint32_t* __restrict__ in, int64_t n,
+                                                     uint32_t* __restrict__ out) {
+  __shared__ uint32_t buf[kScan1Tile + kScan1Tile / 16];
+  __shared__ uint32_t wsum[16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint32_t carry = 0;
+  for (int64_t t0 = 0; t0 < n; t0 += kScan1Tile) {
+#pragma unroll
+    for (int j = 0; j < kScan1Per; ++j) {
+      const int i = j * 1024 + tid;
+      const int64_t g = t0 + i;
+      buf[i + i / 16] = g < n ? in[g] : 0u;
+    }
+    __syncthreads();
+    uint32_t v[kScan1Per], sum = 0;
+#pragma unroll
+    for (int k = 0; k < kScan1Per; ++k) {
+      v[k] = buf[tid * 17 + k];
+      sum += v[k];
+    }
+    uint32_t x = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    uint32_t pre = 0, tile_total = 0;
+    for (int w = 0; w < 16; ++w) {
+      if (w < wave) pre += wsum[w];
+      tile_total += wsum[w];
+    }
+    uint32_t run = carry + pre + x - sum;
+#pragma unroll
+    for (int k = 0; k < kScan1Per; ++k) {
+      buf[tid * 17 + k] = run;
+      run += v[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kScan1Per; ++j) {
+      const int i = j * 1024 + tid;
+      const int64_t g = t0 + i;
+      if (g < n) out[g] = buf[i + i / 16];
+    }
+    carry += tile_total;
+    __syncthreads();
+  }
+}
+
 inline unsigned grid_for(int64_t n, int block = 256, int64_t cap = 16384) {
   int64_t g = ceil_div(n > 0 ? n : 1, block);
   return (unsigned)(g < cap ? g : cap);
@@ -393,15 +498,6 @@ inline unsigned bits_for(int64_t n) {  // bits to represent values in [0, n)
 }
 
 size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
-
-size_t scan_bytes(int64_t E) {
-  size_t bytes = 0;
-  KeepFlag<int64_t> f{nullptr, 0, 1};
-  auto it = rocprim::make_transform_iterator(rocprim::make_counting_iterator<int64_t>(0), f);
-  (void)rocprim::exclusive_scan(nullptr, bytes, it, (int32_t*)nullptr, 0, (size_t)(E > 0 ? E : 1),
-                          rocprim::plus<int32_t>(), (hipStream_t)0);
-  return bytes;
-}
 
 // ---- the radix sort's host side (workspace layout and passes)
 struct SortWs {
@@ -476,10 +572,15 @@ int sort_pairs(const int32_t* keys_in, const int32_t* vals_in, int32_t* keys_out
     if (wide) radix_hist_kernel<kWideBits><<<(unsigned)nb, 256, 0, stream>>>(ck, n, 0, items, nb, w.hist);
     else radix_hist_kernel<kRadixBits><<<(unsigned)nb, 256, 0, stream>>>(ck, n, shift, items, nb, w.hist);
     GATX_LAUNCH_CHECK("radix_hist");
-    size_t b = w.scan_bytes;
-    hipError_t r = rocprim::exclusive_scan(w.scan_tmp, b, w.hist, w.offs, 0u, (size_t)m,
-                                           rocprim::plus<uint32_t>(), stream);
-    if (r != hipSuccess) { set_error("radix scan: %s", hipGetErrorString(r)); return (int)r; }
+    if (m <= kScan1Max) {
+      scan1_kernel<<<1, 1024, 0, stream>>>(w.hist, m, w.offs);
+      GATX_LAUNCH_CHECK("radix_scan");
+    } else {
+      size_t b = w.scan_bytes;
+      hipError_t r = rocprim::exclusive_scan(w.scan_tmp, b, w.hist, w.offs, 0u, (size_t)m,
+                                             rocprim::plus<uint32_t>(), stream);
+      if (r != hipSuccess) { set_error("radix scan: %s", hipGetErrorString(r)); return (int)r; }
+    }
     static const bool lds_tiles = [] {   // A/B: GATX_RADIX_LDS=0 keeps the direct scatter
       const char* e = getenv("GATX_RADIX_LDS");
       return !(e && strcmp(e, "0") == 0);
@@ -518,31 +619,21 @@ int graph_build_impl(const void* ei, int64_t E, int64_t ld, int add_loops, int64
                      int64_t E_bound, const long long* meta, int64_t* ei_out, int32_t* rowptr,
                      int32_t* col, int32_t* rowidx, int32_t* perm, void* ws, size_t ws_bytes,
                      hipStream_t stream) {
-  // workspace carve: pos [E] | src32 [Eb] | dst32 [Eb] | iota [Eb] | rocprim temp
+  // workspace carve: src32 [Eb] | dst32 [Eb] | iota [Eb] | sort workspace
   char* p = (char*)ws;
-  int32_t* pos = (int32_t*)p;   p += align256(sizeof(int32_t) * (E > 0 ? E : 1));
   int32_t* src32 = (int32_t*)p; p += align256(sizeof(int32_t) * (E_bound > 0 ? E_bound : 1));
   int32_t* dst32 = (int32_t*)p; p += align256(sizeof(int32_t) * (E_bound > 0 ? E_bound : 1));
   int32_t* iota = (int32_t*)p;  p += align256(sizeof(int32_t) * (E_bound > 0 ? E_bound : 1));
   size_t used = (size_t)(p - (char*)ws);
   GATX_REQUIRE(used <= ws_bytes, "graph_build: workspace too small");
   void* tmp = p;
-  size_t tmp_bytes = ws_bytes - used;
-
-  if (add_loops && E > 0) {
-    KeepFlag<I> f{ei, ld, 1};
-    auto it = rocprim::make_transform_iterator(rocprim::make_counting_iterator<int64_t>(0), f);
-    size_t b = tmp_bytes;
-    hipError_t r = rocprim::exclusive_scan(tmp, b, it, pos, 0, (size_t)E,
-                                           rocprim::plus<int32_t>(), stream);
-    if (r != hipSuccess) { set_error("exclusive_scan: %s", hipGetErrorString(r)); return (int)r; }
-  }
-  if (E + E_bound > 0) {
-    compact_kernel<I><<<grid_for(E + E_bound), 256, 0, stream>>>(
-        ei, E, ld, add_loops, pos, meta, E_bound, N, ei_out, src32, dst32, iota);
-    GATX_LAUNCH_CHECK("compact");
-  }
   if (E_bound > 0) {
+    // the stats launch's block count (meta[6]) is <= kStatsBlocks: that many range blocks, then
+    // the loop / padding slot blocks
+    const int64_t slot_blocks = std::max<int64_t>(1, std::min<int64_t>(ceil_div(E_bound, 256), 4096));
+    compact_kernel<I><<<(unsigned)(stats_blocks(E) + slot_blocks), 256, 0, stream>>>(
+        ei, E, ld, add_loops, meta, E_bound, N, ei_out, src32, dst32, iota);
+    GATX_LAUNCH_CHECK("compact");
     // src ids ride along as a second value: col comes out of the sort (no gather through perm)
     GATX_CALL(sort_pairs(dst32, iota, rowidx, perm, E_bound, bits_for(N + 1), tmp, stream, src32,
                          col));
@@ -578,7 +669,7 @@ __global__ void __launch_bounds__(256) hub_plan_kernel(const int32_t* __restrict
 using namespace gatx;
 
 extern "C" size_t gatx_graph_meta_workspace_bytes(void) {
-  return (size_t)3 * sizeof(long long) * kStatsBlocks;
+  return (size_t)4 * sizeof(long long) * kStatsBlocks;
 }
 
 extern "C" int gatx_graph_meta(const void* edge_index, int is64, int64_t E, int64_t ld,
@@ -586,24 +677,24 @@ extern "C" int gatx_graph_meta(const void* edge_index, int is64, int64_t E, int6
                                void* workspace, gatx_stream_t s) {
   GATX_REQUIRE(E >= 0 && num_nodes >= 0, "graph_meta: negative size");
   hipStream_t stream = (hipStream_t)s;
-  const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(E, 256), kStatsBlocks));
+  const int nb = stats_blocks(E);
+  const int64_t chunk = stats_chunk(E);
   long long* part = (long long*)workspace;
   if (is64)
-    edge_stats_kernel<int64_t><<<nb, 256, 0, stream>>>(edge_index, E, ld, part);
+    edge_stats_kernel<int64_t><<<nb, 256, 0, stream>>>(edge_index, E, ld, chunk, part);
   else
-    edge_stats_kernel<int32_t><<<nb, 256, 0, stream>>>(edge_index, E, ld, part);
+    edge_stats_kernel<int32_t><<<nb, 256, 0, stream>>>(edge_index, E, ld, chunk, part);
   GATX_LAUNCH_CHECK("edge_stats");
-  graph_meta_kernel<<<1, 256, 0, stream>>>(part, nb, E, add_self_loops, num_nodes,
+  graph_meta_kernel<<<1, 256, 0, stream>>>(part, nb, E, chunk, add_self_loops, num_nodes,
                                            (long long*)meta);
   GATX_LAUNCH_CHECK("graph_meta");
   return 0;
 }
 
 extern "C" size_t gatx_graph_build_workspace_bytes(int64_t E, int64_t E_bound, int64_t N) {
-  size_t b = align256(sizeof(int32_t) * (E > 0 ? E : 1)) +
-             3 * align256(sizeof(int32_t) * (E_bound > 0 ? E_bound : 1));
-  size_t t = std::max(scan_bytes(E), sort_bytes(E_bound, bits_for(N + 1), true));
-  return b + align256(t) + 256;
+  (void)E;
+  size_t b = 3 * align256(sizeof(int32_t) * (E_bound > 0 ? E_bound : 1));
+  return b + align256(sort_bytes(E_bound, bits_for(N + 1), true)) + 256;
 }
 
 extern "C" int gatx_graph_build(const void* edge_index, int is64, int64_t E, int64_t ld,

@@ -16,6 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GATX_LIB", os.path.join(_HERE, "libgatx.so"))
 
 ARGMAX_CAP = 1024  # GATX_ARGMAX_CAP
+META_WORDS = 520   # GATX_META_WORDS
 
 c_i = ctypes.c_int
 c_i64 = ctypes.c_int64

@@ -69,12 +69,14 @@ class Graph:
             raise RuntimeError("max(): Expected reduction dim to be specified for input.numel() == 0. "
                                "Specify the reduction dim with the 'dim' argument.")
         s = stream()
-        self.meta = torch.empty(8, dtype=torch.int64, device=dev)
+        # {E2, num_loops, status, min, max, self-loops, nb, chunk} + the compaction's block
+        # offsets (GATX_META_WORDS); the host only ever reads the first 8
+        self.meta = torch.empty(_lib.META_WORDS, dtype=torch.int64, device=dev)
         ws = _meta_ws(dev)
         if num_nodes is None:   # sized by the edges themselves: the one case that must sync
             call("gatx_graph_meta", ptr(edge_index), is64, E, ld, int(add_self_loops),
                  _I32_LIMIT, ptr(self.meta), ptr(ws), s)
-            m = self.meta.cpu()
+            m = self.meta[:8].cpu()
             err = _status_error(m, _I32_LIMIT)
             if err is not None:
                 raise err
@@ -112,7 +114,7 @@ class Graph:
         self._event = None
         if not torch.cuda.is_current_stream_capturing():
             self._meta_host = torch.empty(8, dtype=torch.int64, pin_memory=True)
-            self._meta_host.copy_(self.meta, non_blocking=True)
+            self._meta_host.copy_(self.meta[:8], non_blocking=True)
             self._event = torch.cuda.Event()
             self._event.record()
             check_pending(block=False)   # surfaces errors of earlier graphs that have landed

@@ -33,6 +33,7 @@ typedef struct ihipStream_t* gatx_stream_t; /* == hipStream_t */
 
 #define GATX_EINVAL 1000
 #define GATX_ARGMAX_CAP 1024 /* argmax (edge, head) slots recorded for the max() gradient */
+#define GATX_META_WORDS 520  /* int64 words of a graph meta record (8 + 1024 int32 offsets) */
 
 const char* gatx_last_error(void);
 int gatx_version(void);
@@ -47,8 +48,10 @@ int gatx_region_mark(uint32_t tag, gatx_stream_t stream);
 /* Device-side sizing of the self-loop rewrite, no host sync (replaces the `int(index.max())` of
  * maybe_num_nodes, models/utils.py:70-72, and the `row != col` mask count of
  * add_remaining_self_loops, models/utils.py:58-60). edge_index (2, E): int64 if index_is_int64
- * else int32, rows `ld` elements apart. meta (device int64[8]) = {E2, num_loops, status, min id,
- * max id, input self-loops, 0, 0} with num_loops = max+1 when add_self_loops, E2 = |edge_index'|.
+ * else int32, rows `ld` elements apart. meta (device int64[GATX_META_WORDS]) = {E2, num_loops,
+ * status, min id, max id, input self-loops, nb, chunk} with num_loops = max+1 when
+ * add_self_loops, E2 = |edge_index'|, followed by the compaction's per-block offsets (int32, for
+ * gatx_graph_build; only the first 8 words are meant for the host).
  * status 1 = a negative id, 2 = an id >= num_nodes: then E2 = num_loops = 0, so every later kernel
  * sees an empty graph (no out-of-bounds access) and the host raises when it reads meta (the
  * reference raises in index_select / scatter_add_). workspace: gatx_graph_meta_workspace_bytes(). */
