@@ -458,9 +458,10 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
     const char* e = getenv("GATX_TINY_GEMM");
     return !(e && strcmp(e, "0") == 0);
   }();
-  // (only short K: every output re-reads its A row and B column, so a long K turns the VALU
-  // kernel TA-bound — PATTERN's K = 952-node weight gradients ran 28 us vs 12 us tiled)
-  if (tiny_on && K <= 64 && M * N * K * batch <= (int64_t(1) << 25)) {
+  // (only short K and few rows: every output re-reads its A row and B column, so the VALU
+  // kernel turns TA-bound — PATTERN's K = 952-node weight gradients ran 28 us vs 12 us tiled,
+  // PPI's 44900 x 8 x 50 score product 26 us vs 11 us on the small-K MFMA kernel)
+  if (tiny_on && K <= 64 && M <= 16384 && M * N * K * batch <= (int64_t(1) << 25)) {
     g.splits = 1; g.tail_s = 1; g.tiles_m = g.tiles_n = 1; g.dp_blocks = g.tail_rem = 0;
     g.bm = g.bn = 32; g.tail_partial = nullptr;
     return launch_gemm_tiny(g, batch, a_kc, b_kc, stream);

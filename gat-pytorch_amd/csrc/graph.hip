@@ -62,7 +62,7 @@ __global__ void __launch_bounds__(256) edge_stats_kernel(const void* ei, int64_t
     part[4 * blockIdx.x + 0] = mn;
     part[4 * blockIdx.x + 1] = mx;
     part[4 * blockIdx.x + 2] = loops;
-    part[4 * blockIdx.x + 3] = (hi > lo ? hi - lo : 0) - loops;   // kept by the rewrite
+    part[4 * blockIdx.x + 3] = hi > lo ? hi - lo : 0;   // the block's input edges
   }
 }
 
@@ -88,12 +88,13 @@ __global__ void __launch_bounds__(256) graph_meta_kernel(const long long* part, 
   __shared__ int wsum[4];
   int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   if (l == 0) { red[0][w] = mn; red[1][w] = mx; red[2][w] = loops; }
-  // block offsets of the compaction: thread t scans blocks [4t, 4t+4) (nb <= 1024)
+  // block offsets of the compaction: thread t scans blocks [4t, 4t+4) (nb <= 1024); a block
+  // keeps all its edges without the rewrite, all but its self-loops with it
   int c[4], tot = 0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int b = 4 * threadIdx.x + j;
-    c[j] = b < nb ? (int)part[4 * b + 3] : 0;
+    c[j] = b < nb ? (int)(part[4 * b + 3] - (add_loops ? part[4 * b + 2] : 0)) : 0;
     tot += c[j];
   }
   int x = tot;
@@ -212,8 +213,10 @@ __global__ void __launch_bounds__(256) rowptr_kernel(const int32_t* keys, int64_
                                                       int64_t num_rows, int32_t* rowptr) {
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e <= E2;
        e += (int64_t)gridDim.x * blockDim.x) {
-    int64_t k = (e < E2) ? keys[e] : num_rows;
-    int64_t kp = (e > 0) ? keys[e - 1] : -1;
+    // clamped: a key outside [0, num_rows] (never produced by the builders) cannot write
+    // outside rowptr
+    int64_t k = (e < E2) ? min<int64_t>(max<int64_t>(keys[e], 0), num_rows) : num_rows;
+    int64_t kp = (e > 0) ? min<int64_t>(max<int64_t>(keys[e - 1], -1), num_rows) : -1;
     for (int64_t r = kp + 1; r <= k; ++r) rowptr[r] = (int32_t)e;
   }
 }
@@ -429,63 +432,6 @@ __global__ void __launch_bounds__(256) radix_scatter_lds_kernel(
   }
 }
 
-// Exclusive scan of n uint32 in ONE 1024-thread block, for the radix sort's digit-major
-// histograms up to kScan1Max entries (rocPRIM's lookback scan is two launches, ~12 us, on these
-// sizes): tiles of 16 K entries are loaded coalesced into LDS (row-padded: thread t's 16
-// consecutive entries at stride 17, conflict-free), each thread scans its 16, a block scan over
-// the 1024 thread sums links them, and the tile goes back out coalesced with a running carry.
-constexpr int kScan1Per = 16, kScan1Tile = 1024 * kScan1Per;
-constexpr int64_t kScan1Max = 1 << 17;
-__global__ void __launch_bounds__(1024) scan1_kernel(const uint32_t* __restrict__ in, int64_t n,
-                                                     uint32_t* __restrict__ out) {
-  __shared__ uint32_t buf[kScan1Tile + kScan1Tile / 16];
-  __shared__ uint32_t wsum[16];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  uint32_t carry = 0;
-  for (int64_t t0 = 0; t0 < n; t0 += kScan1Tile) {
-#pragma unroll
-    for (int j = 0; j < kScan1Per; ++j) {
-      const int i = j * 1024 + tid;
-      const int64_t g = t0 + i;
-      buf[i + i / 16] = g < n ? in[g] : 0u;
-    }
-    __syncthreads();
-    uint32_t v[kScan1Per], sum = 0;
-#pragma unroll
-    for (int k = 0; k < kScan1Per; ++k) {
-      v[k] = buf[tid * 17 + k];
-      sum += v[k];
-    }
-    uint32_t x = sum;
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(x, o);
-      if (lane >= o) x += y;
-    }
-    if (lane == 63) wsum[wave] = x;
-    __syncthreads();
-    uint32_t pre = 0, tile_total = 0;
-    for (int w = 0; w < 16; ++w) {
-      if (w < wave) pre += wsum[w];
-      tile_total += wsum[w];
-    }
-    uint32_t run = carry + pre + x - sum;
-#pragma unroll
-    for (int k = 0; k < kScan1Per; ++k) {
-      buf[tid * 17 + k] = run;
-      run += v[k];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kScan1Per; ++j) {
-      const int i = j * 1024 + tid;
-      const int64_t g = t0 + i;
-      if (g < n) out[g] = buf[i + i / 16];
-    }
-    carry += tile_total;
-    __syncthreads();
-  }
-}
-
 inline unsigned grid_for(int64_t n, int block = 256, int64_t cap = 16384) {
   int64_t g = ceil_div(n > 0 ? n : 1, block);
   return (unsigned)(g < cap ? g : cap);
@@ -572,15 +518,12 @@ int sort_pairs(const int32_t* keys_in, const int32_t* vals_in, int32_t* keys_out
     if (wide) radix_hist_kernel<kWideBits><<<(unsigned)nb, 256, 0, stream>>>(ck, n, 0, items, nb, w.hist);
     else radix_hist_kernel<kRadixBits><<<(unsigned)nb, 256, 0, stream>>>(ck, n, shift, items, nb, w.hist);
     GATX_LAUNCH_CHECK("radix_hist");
-    if (m <= kScan1Max) {
-      scan1_kernel<<<1, 1024, 0, stream>>>(w.hist, m, w.offs);
-      GATX_LAUNCH_CHECK("radix_scan");
-    } else {
-      size_t b = w.scan_bytes;
-      hipError_t r = rocprim::exclusive_scan(w.scan_tmp, b, w.hist, w.offs, 0u, (size_t)m,
-                                             rocprim::plus<uint32_t>(), stream);
-      if (r != hipSuccess) { set_error("radix scan: %s", hipGetErrorString(r)); return (int)r; }
-    }
+    // (a single-workgroup LDS scan measured 35 us on PPI's 80 K counts: rocPRIM's lookback
+    // scan over the whole chip stays)
+    size_t b = w.scan_bytes;
+    hipError_t r = rocprim::exclusive_scan(w.scan_tmp, b, w.hist, w.offs, 0u, (size_t)m,
+                                           rocprim::plus<uint32_t>(), stream);
+    if (r != hipSuccess) { set_error("radix scan: %s", hipGetErrorString(r)); return (int)r; }
     static const bool lds_tiles = [] {   // A/B: GATX_RADIX_LDS=0 keeps the direct scatter
       const char* e = getenv("GATX_RADIX_LDS");
       return !(e && strcmp(e, "0") == 0);
