@@ -378,14 +378,27 @@ def run_rmat(args, world, rank, dev):
     NH, F, FIN = 8, 64, 512
     N, E = args.rmat_nodes, args.rmat_edges
     torch.manual_seed(0)
-    layer = GATLayer(FIN, F, NH, True, add_self_loops=True).to(dev).eval()
+    train = args.mode == "train"
+    layer = GATLayer(FIN, F, NH, True, add_self_loops=True).to(dev).train(train)
     ei = gd.rmat_edges_device(N, E, seed=42 + rank, device=dev)
     g = torch.Generator(device=dev)
     g.manual_seed(1 + rank)
     x = torch.randn(N, FIN, device=dev, generator=g)
+    gout = None
+    if train:
+        # a middle layer's backward: gradients for x, W and a from a fixed upstream gradient
+        # (the hub-split backward passes, SURVEY.md §7 degree skew, on the power-law graph)
+        x.requires_grad_(True)
+        gout = torch.randn(N, NH * F, device=dev, generator=g)
 
     def step():
         clear_graph_cache()
+        if train:
+            layer.zero_grad(set_to_none=True)
+            x.grad = None
+            out = layer(x, ei)
+            out.backward(gout)
+            return out
         with torch.no_grad():
             return layer(x, ei)
 
@@ -404,10 +417,11 @@ def run_rmat(args, world, rank, dev):
     b_gemm, _, b_edge = survey_bytes(N, E2, FIN, NH, F, True)
     edge_b = [b for k, b, _ in flow if k == "edge_forward"][0]
     pmc_path = os.path.join(ROOT, "profiles", "pmc_rmat.json")
-    pm = load_pmc(pmc_path)
+    pm = load_pmc(pmc_path) if not train else None   # the committed counters are forward-only
     roofs = roofline_objects(summ, lambda i, info: edge_b, pm, n_instr, pmc_path)
     result = {
-        "metric": "GAT-layer edges/sec + achieved HBM GB/s, RMAT 1-layer fwd",
+        "metric": "GAT-layer edges/sec + achieved HBM GB/s, RMAT 1-layer fwd"
+                  + (" (+bwd)" if train else ""),
         "value": round(E2 * world / step_s, 1), "unit": "layer-edges/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(step_s * 1e3, 4),
@@ -415,18 +429,19 @@ def run_rmat(args, world, rank, dev):
         "data": "synthetic R-MAT (a,b,c,d)=(0.57,0.19,0.19,0.05), rejected ids redrawn, ids "
                 "permuted, x ~ N(0,1), xavier weights",
         "config": {"workload": f"RMAT {N} nodes / {E} edges, GATLayer 512 -> 8x64 concat, "
-                               "self-loops, eval, CSR built per step",
+                               f"self-loops, {'fwd+bwd' if train else 'eval'}, CSR built per step",
+                   "hub_split_backward": train and os.environ.get("GATX_BWD_HUBS") != "0",
                    "nodes": N, "edges_in": int(ei.size(1)), "edges_per_layer": E2,
                    "parallelism": "replicas" if world > 1 else "single GPU"},
         "unique_GBps": round(uniq / step_s / 1e9, 1),
-        "roofline_time_frac": round(t_roof / step_s, 4),
+        "roofline_time_frac": None if train else round(t_roof / step_s, 4),
         "l2_gather_GBps": round((b_gemm + b_edge) / step_s / 1e9, 1),
-        "hbm_measured": pmc_step_bytes(pm, step_s * 1e3, pmc_path),
+        "hbm_measured": None if train else pmc_step_bytes(pm, step_s * 1e3, pmc_path),
         "roofline": roofs[0] if roofs else None,
         "roofline_other": roofs[1] if len(roofs) > 1 else None,
         "kernels": kernel_summary(summ, n_instr),
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not train:
         result["cpu_baseline"] = cpu_baseline_rmat(layer.W.weight.detach().cpu().numpy(),
                                                    layer.a.weight.detach().cpu().numpy(), NH, F)
     if rank == 0:

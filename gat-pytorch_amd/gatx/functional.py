@@ -265,10 +265,14 @@ def hub_args(graph: Graph, sh: LayerShape, hs: int, group_count: int, dev):
 
 
 def bwd_hub_args(graph: Graph, NH: int, F: int, dev, source: bool):
-    """The trailing hub-splitting arguments of gatx_edge_backward_{dst,src}_hubs: the same rule
-    as the forward (hub_args), over the destination CSR (source=False) or the transpose
-    (source=True). GATX_BWD_HUBS=0 keeps one wave per segment (A/B tests)."""
-    T = _env_int("GATX_HUB_EDGES", 8192)
+    """The trailing hub-splitting arguments of gatx_edge_backward_{dst,src}_hubs, over the
+    destination CSR (source=False) or the transpose (source=True), for graphs past the forward's
+    2^22-edge threshold. The backward's items are one head each (the forward's carry up to 8), so
+    a segment costs one wave 8x less there: on R-MAT 1e7 / 1.6e8 splitting at 8192 edges gained
+    nothing (dst pass 19.06 ms unsplit vs 17.84 + 1.18 split; profiles/r03m), so the backward
+    splits only segments past GATX_BWD_HUB_EDGES = 65536 edges — the guard against extreme skew
+    (a star graph's hub would otherwise be one wave's walk). GATX_BWD_HUBS=0: never split."""
+    T = _env_int("GATX_BWD_HUB_EDGES", 65536)
     if (T <= 0 or _env_int("GATX_BWD_HUBS", 1) == 0
             or graph.num_input_edges <= _env_int("GATX_HUB_MIN_EDGES", 1 << 22)):
         return (0, None, None, 0, None)

@@ -81,6 +81,7 @@ def test_hub_split_vs_oracle(name, T, device, monkeypatch):
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     monkeypatch.setenv("GATX_HUB_EDGES", T)
+    monkeypatch.setenv("GATX_BWD_HUB_EDGES", T)
     monkeypatch.setenv("GATX_HUB_MIN_EDGES", "0")
     from gatx import data as gd
     x, ei = _hub_graph(fin=fin)
@@ -104,6 +105,7 @@ def test_hub_split_vs_oracle(name, T, device, monkeypatch):
         np.testing.assert_array_equal(r[k], r1[k], err_msg=k)
     # the same layer without splitting: same result to fp32 summation-order noise
     monkeypatch.setenv("GATX_HUB_EDGES", "0")
+    monkeypatch.setenv("GATX_BWD_HUB_EDGES", "0")
     from gatx import functional
     functional.reset_tuning()
     r0 = _run(device, x, ei, W, a, NH, F, concat, dropout)
@@ -161,3 +163,48 @@ def test_source_hub_plan(device):
     h = hubs[:c].cpu().numpy()
     assert c == sum(want.values())
     assert {int(node): int(pieces) for node, _, pieces, _ in h} == want
+
+
+def test_rmat_scaled_backward_hub_split(device, monkeypatch):
+    """A scaled R-MAT graph (1e6 nodes, 1.6e7 edges: past the 2^22-edge threshold, so the
+    default plan splits every segment longer than 8192 edges) through forward + backward: the
+    hub-split backward passes give the unsplit passes' gradients to fp32 summation noise, and
+    the plan really has destination and source hubs."""
+    import gatx
+    from gatx import data as gd
+    from gatx.graph import graph_cache
+    N, E, NH, F, FIN = 1_000_000, 16_000_000, 8, 64, 64
+    ei = gd.rmat_edges_device(N, E, seed=5, device=device)
+    torch.manual_seed(0)
+    layer = gatx.GATLayer(FIN, F, NH, True, add_self_loops=True).to(device)
+    g = torch.Generator(device=device)
+    g.manual_seed(2)
+    x0 = torch.randn(N, FIN, device=device, generator=g)
+    gout = torch.randn(N, NH * F, device=device, generator=g)
+
+    monkeypatch.setenv("GATX_BWD_HUB_EDGES", "8192")   # split at the forward's threshold
+
+    def run(split):
+        monkeypatch.setenv("GATX_BWD_HUBS", "1" if split else "0")
+        from gatx import functional
+        functional.reset_tuning()
+        gatx.clear_graph_cache()
+        layer.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        layer(x, ei).backward(gout)
+        torch.cuda.synchronize()
+        return x.grad, layer.W.weight.grad.clone(), layer.a.weight.grad.clone()
+
+    split = run(True)
+    graph = graph_cache.get(ei, N, True)
+    d_hubs = int(graph.hub_plan(8192)[1].item())
+    s_hubs = int(graph.hub_plan(8192, source=True)[1].item())
+    assert d_hubs > 0 and s_hubs > 0, (d_hubs, s_hubs)
+    again = run(True)
+    for a_, b_ in zip(split, again):
+        assert torch.equal(a_, b_)   # bitwise repeatable
+    plain = run(False)
+    for name, a_, b_ in zip(("x", "W", "a"), split, plain):
+        scale = max(1.0, float(b_.abs().max()))
+        err = float((a_ - b_).abs().max())
+        assert err <= 1e-5 * scale, (name, err, scale)
