@@ -731,35 +731,49 @@ __global__ void __launch_bounds__(256) weff_partial_kernel(const float* __restri
   }
 }
 
+// W_aug from W and the split-K partials: blocks [0, ncopy) copy the head-padded W rows and the
+// folded skip's rows; the blocks after them give each score-row element one wave, lanes over the
+// n_cb partials, fixed-order wave sum (a thread summing its element's 64 partials alone made the
+// PPI assembly an 18 us latency chain).
 __global__ void __launch_bounds__(256) waug_assemble_kernel(const float* __restrict__ W,
                                                             const float* __restrict__ partial,
                                                             int n_cb, int NH, int F, int Fp,
-                                                            int H2, int64_t F_in,
+                                                            int H2, int64_t F_in, int ncopy,
                                                             float* __restrict__ W_aug,
                                                             const float* __restrict__ W_skip,
                                                             int skip_heads, int64_t skip_cols) {
   const int64_t Dp = (int64_t)NH * Fp;
-  const int64_t nmain = (Dp + H2) * F_in, sk = skip_cols * F_in;
-  const int64_t total = nmain + sk;
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = t / F_in, i = t - r * F_in;
-    float v;
-    if (t >= nmain) {   // folded skip rows: mean over the skip's head blocks (a copy for 1)
-      const int64_t q = t - nmain;
-      v = W_skip[q];
-      for (int h = 1; h < skip_heads; ++h) v += W_skip[(int64_t)h * sk + q];
-      if (skip_heads > 1) v /= (float)skip_heads;
-    } else if (r < Dp) {
-      const int h = (int)(r / Fp), f = (int)(r - (int64_t)h * Fp);
-      v = (f < F) ? W[((int64_t)h * F + f) * F_in + i] : 0.f;
-    } else {
-      const int h2 = (int)(r - Dp);
-      v = 0.f;
-      for (int cb = 0; cb < n_cb; ++cb) v += partial[((int64_t)cb * H2 + h2) * F_in + i];
+  if ((int)blockIdx.x < ncopy) {
+    const int64_t ncp = Dp * F_in, sk = skip_cols * F_in;
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < ncp + sk;
+         t += (int64_t)ncopy * blockDim.x) {
+      float v;
+      int64_t dst;
+      if (t >= ncp) {   // folded skip rows: mean over the skip's head blocks (a copy for 1)
+        const int64_t q = t - ncp;
+        v = W_skip[q];
+        for (int h = 1; h < skip_heads; ++h) v += W_skip[(int64_t)h * sk + q];
+        if (skip_heads > 1) v /= (float)skip_heads;
+        dst = (Dp + H2) * F_in + q;
+      } else {
+        const int64_t r = t / F_in, i = t - r * F_in;
+        const int h = (int)(r / Fp), f = (int)(r - (int64_t)h * Fp);
+        v = (f < F) ? W[((int64_t)h * F + f) * F_in + i] : 0.f;
+        dst = t;
+      }
+      W_aug[dst] = v;
     }
-    W_aug[t] = v;
+    return;
   }
+  const int lane = threadIdx.x & 63;
+  const int64_t o = ((int64_t)blockIdx.x - ncopy) * 4 + (threadIdx.x >> 6);
+  if (o >= (int64_t)H2 * F_in) return;
+  const int h2 = (int)(o / F_in);
+  const int64_t i = o - (int64_t)h2 * F_in;
+  float v = 0.f;
+  for (int cb = lane; cb < n_cb; cb += 64) v += partial[((int64_t)cb * H2 + h2) * F_in + i];
+  v = group_sum<64>(v);
+  if (lane == 0) W_aug[(Dp + h2) * F_in + i] = v;
 }
 
 // W_aug in ONE launch for small layers (D = NH*F <= 256; split-K partials + assembly are two
@@ -1187,8 +1201,13 @@ extern "C" int gatx_prepare_weights_skip(const float* W, const float* a, int NH,
     weff_partial_kernel<<<g, 256, 0, st>>>(W, a, NH, F, F_in, partial);
     GATX_LAUNCH_CHECK("weff_partial");
   }
-  waug_assemble_kernel<<<grid_for(((int64_t)NH * Fp + H2 + skip_cols) * F_in), 256, 0, st>>>(
-      W, partial, n_cb, NH, F, Fp, H2, F_in, W_aug, W_skip, skip_heads, skip_cols);
+  {
+    const int ncopy = (int)grid_for(((int64_t)NH * Fp + skip_cols) * F_in, 256, 4096);
+    const int64_t nscore = ceil_div((int64_t)H2 * F_in, 4);
+    GATX_REQUIRE(ncopy + nscore < (1ll << 31), "prepare_weights: too many blocks");
+    waug_assemble_kernel<<<(unsigned)(ncopy + nscore), 256, 0, st>>>(
+        W, partial, n_cb, NH, F, Fp, H2, F_in, ncopy, W_aug, W_skip, skip_heads, skip_cols);
+  }
   GATX_LAUNCH_CHECK("waug_assemble");
   return 0;
 }

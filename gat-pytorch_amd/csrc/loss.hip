@@ -50,19 +50,33 @@ __global__ void __launch_bounds__(1024) bce_small_kernel(const float* __restrict
   if (threadIdx.x == 0) loss[0] = t * inv_n;
 }
 
+// Four elements per thread per round, all loads issued first (the loop is load-latency bound).
 __global__ void __launch_bounds__(256) bce_partial_kernel(const float* __restrict__ x,
                                                           const float* __restrict__ y, int64_t n,
                                                           float pw, float* __restrict__ part,
                                                           float* __restrict__ grad) {
   __shared__ float red[4];
   const float inv_n = 1.f / (float)n;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   float s = 0.f;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    float l, g;
-    bce_elem(x[i], y[i], pw, inv_n, l, g);
-    grad[i] = g;
-    s += l;
+  for (int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i0 < n; i0 += 4 * stride) {
+    float xv[4], yv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = i0 + u * stride;
+      xv[u] = i < n ? x[i] : 0.f;
+      yv[u] = i < n ? y[i] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (i < n) {
+        float l, g;
+        bce_elem(xv[u], yv[u], pw, inv_n, l, g);
+        grad[i] = g;
+        s += l;
+      }
+    }
   }
   const float t = block_sum(s, red);
   if (threadIdx.x == 0) part[blockIdx.x] = t;
