@@ -49,7 +49,7 @@ __device__ inline void sk_split8(const float (&v)[8], uint4& h, uint4& m, uint4&
 
 // A row-major (k-contiguous, lda), B as rows of k (ldb: B(k, n) = B[n * ldb + k]). VEC: A rows
 // 16-byte aligned (lda % 4 == 0, aligned base), so full 8-k groups load as two float4.
-template <bool VEC>
+template <bool VEC, bool ELU>
 __global__ void __launch_bounds__(64 * SK_WAVES, 1) gemm_smallk_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) char wl[3 * SK_PLANE];
   __shared__ float bias_l[SK_NMAX];
@@ -151,20 +151,31 @@ __global__ void __launch_bounds__(64 * SK_WAVES, 1) gemm_smallk_kernel(GemmArgs 
       for (int i = 0; i < 2; ++i) {
         if (i >= nb) break;
         // epilogue (no residual / accumulate on this path): elu?(acc + bias); the bias comes
-        // from LDS, so no global load waits behind this wave's earlier stores
+        // from LDS, so no global load waits behind this wave's earlier stores. Interior blocks
+        // (every row and column inside the matrix) take a straight-line path of 16 stores with
+        // ELU a compile-time choice: per-element bound checks and a runtime ELU test had made
+        // each store its own exec-masked branch.
         const int col = (cb + i) * 32 + (lane & 31);
-        if (col >= N) continue;
-        const float bv = bias_l[col];
-        float* base = g.C0 + b * g.c0_bs + col;
+        const int colc = col < N ? col : N - 1;
+        const float bv = bias_l[colc];
+        float* base = g.C0 + b * g.c0_bs + colc;
         const int64_t row0 = rb * 32 + 4 * half;
-        const bool full = row0 + 27 < M;
+        if (row0 + 27 < M && (cb + i) * 32 + 32 <= N) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int64_t row = row0 + (r & 3) + 8 * (r >> 2);
-          if (!full && row >= M) continue;
-          float v = acc[i][r] + bv;
-          if (g.elu) v = elu_act(v);
-          base[row * g.ldc0] = v;
+          for (int r = 0; r < 16; ++r) {
+            float v = acc[i][r] + bv;
+            if (ELU) v = elu_act(v);
+            base[(row0 + (r & 3) + 8 * (r >> 2)) * g.ldc0] = v;
+          }
+        } else if (col < N) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int64_t row = row0 + (r & 3) + 8 * (r >> 2);
+            if (row >= M) continue;
+            float v = acc[i][r] + bv;
+            if (ELU) v = elu_act(v);
+            base[row * g.ldc0] = v;
+          }
         }
       }
     }
@@ -188,8 +199,10 @@ int launch_gemm_smallk(const gk::GemmArgs& g, int batch, hipStream_t stream) {
   const unsigned gx = (unsigned)std::min<int64_t>(per, ceil_div(nrb, SK_WAVES));
   dim3 grid(gx, (unsigned)batch);
   const bool vec = ((uintptr_t)g.A % 16 == 0) && g.lda % 4 == 0 && g.a_bs % 4 == 0;
-  if (vec) gemm_smallk_kernel<true><<<grid, 64 * SK_WAVES, 0, stream>>>(g);
-  else gemm_smallk_kernel<false><<<grid, 64 * SK_WAVES, 0, stream>>>(g);
+  if (vec && g.elu) gemm_smallk_kernel<true, true><<<grid, 64 * SK_WAVES, 0, stream>>>(g);
+  else if (vec) gemm_smallk_kernel<true, false><<<grid, 64 * SK_WAVES, 0, stream>>>(g);
+  else if (g.elu) gemm_smallk_kernel<false, true><<<grid, 64 * SK_WAVES, 0, stream>>>(g);
+  else gemm_smallk_kernel<false, false><<<grid, 64 * SK_WAVES, 0, stream>>>(g);
   GATX_LAUNCH_CHECK("gemm_smallk");
   return 0;
 }
