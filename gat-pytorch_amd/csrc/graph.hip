@@ -432,6 +432,112 @@ __global__ void __launch_bounds__(256) radix_scatter_lds_kernel(
   }
 }
 
+// radix_scatter_lds_kernel<8> with 16 waves per tile instead of 4: a tile of 256 * items keys
+// is ranked in items / 4 rounds of 1024 keys instead of items rounds of 256, and four times as
+// many waves per CU overlap the rounds' LDS and barrier latency (the PPI pass kept ~1.2
+// four-wave blocks per CU busy). Same stable order: ranks within a wave by ballots, across
+// waves through the per-(wave, digit) counts, across rounds through the running digit bases.
+template <bool V2>
+__global__ void __launch_bounds__(1024) radix_scatter_lds16_kernel(
+    const int32_t* __restrict__ keys, const int32_t* __restrict__ vals, int64_t n, int shift,
+    int items, int64_t nblocks, const uint32_t* __restrict__ offs,
+    const uint32_t* __restrict__ hist, int32_t* __restrict__ keys_out,
+    int32_t* __restrict__ vals_out, const int32_t* __restrict__ vals2 = nullptr,
+    int32_t* __restrict__ vals2_out = nullptr) {
+  constexpr int BITS = 8, R = 256, NW = 16, NT = 1024;
+  __shared__ uint32_t gbase[R];
+  __shared__ uint32_t lstart[R];
+  __shared__ uint32_t lrun[R];
+  __shared__ uint32_t cnt[NW][R];
+  __shared__ int32_t tk[kMaxSortItems * 256];
+  __shared__ int32_t tv[kMaxSortItems * 256];
+  __shared__ int32_t tv2[V2 ? kMaxSortItems * 256 : 1];
+  __shared__ uint32_t wsum[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint32_t c = 0, x = 0;
+  if (tid < R) {   // this block's digit counts -> exclusive prefix over the digits
+    c = hist[(int64_t)tid * nblocks + blockIdx.x];
+    gbase[tid] = offs[(int64_t)tid * nblocks + blockIdx.x];
+    x = c;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+  }
+  for (int i = tid; i < NW * R; i += NT) (&cnt[0][0])[i] = 0;
+  __syncthreads();
+  if (tid < R) {
+    uint32_t run = x - c;
+    for (int w = 0; w < wave; ++w) run += wsum[w];
+    lstart[tid] = run;
+    lrun[tid] = run;
+  }
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const int64_t tile = (int64_t)blockIdx.x * 256 * items;
+  const int tile_keys = 256 * items, rounds = (tile_keys + NT - 1) / NT;
+  for (int r = 0; r < rounds; ++r) {
+    const int li = r * NT + tid;
+    const int64_t idx = tile + li;
+    const bool valid = li < tile_keys && idx < n;
+    const int32_t key = valid ? keys[idx] : 0;
+    const int32_t val = valid ? (vals ? vals[idx] : (int32_t)idx) : 0;
+    const int32_t val2 = (V2 && valid) ? vals2[idx] : 0;
+    const int d = (key >> shift) & (R - 1);
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < BITS; ++b) {
+      const uint64_t bb = __ballot((d >> b) & 1);
+      peers &= ((d >> b) & 1) ? bb : ~bb;
+    }
+    const int rank = __popcll(peers & lt);
+    const bool lead = valid && rank == 0;
+    __syncthreads();
+    if (lead) cnt[wave][d] = (uint32_t)__popcll(peers);
+    __syncthreads();
+    if (valid) {
+      uint32_t pos = lrun[d] + rank;
+      for (int w = 0; w < wave; ++w) pos += cnt[w][d];
+      tk[pos] = key;
+      tv[pos] = val;
+      if (V2) tv2[pos] = val2;
+    }
+    __syncthreads();
+    if (lead) {
+      atomicAdd(&lrun[d], cnt[wave][d]);
+      cnt[wave][d] = 0;
+    }
+  }
+  __syncthreads();
+  const int64_t count = min((int64_t)tile_keys, n - tile);
+  for (int j = tid; j < count; j += NT) {
+    const int32_t key = tk[j];
+    const int d = (key >> shift) & (R - 1);
+    const uint32_t gpos = gbase[d] + ((uint32_t)j - lstart[d]);
+    keys_out[gpos] = key;
+    vals_out[gpos] = tv[j];
+    if (V2) vals2_out[gpos] = tv2[j];
+  }
+}
+
+// radix_hist_kernel<8> for 1024-thread blocks (the tiles of radix_scatter_lds16_kernel).
+__global__ void __launch_bounds__(1024) radix_hist16_kernel(const int32_t* __restrict__ keys,
+                                                            int64_t n, int shift, int items,
+                                                            int64_t nblocks,
+                                                            uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[256];
+  if (threadIdx.x < 256) h[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * 256 * items;
+  const int tile_keys = 256 * items;
+  for (int i = threadIdx.x; i < tile_keys; i += 1024) {
+    const int64_t idx = base + i;
+    if (idx < n) atomicAdd(&h[(keys[idx] >> shift) & 255], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < 256) hist[(int64_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+}
+
 inline unsigned grid_for(int64_t n, int block = 256, int64_t cap = 16384) {
   int64_t g = ceil_div(n > 0 ? n : 1, block);
   return (unsigned)(g < cap ? g : cap);
@@ -515,7 +621,14 @@ int sort_pairs(const int32_t* keys_in, const int32_t* vals_in, int32_t* keys_out
     int32_t* ov = to_out ? vals_out : w.tv;
     int32_t* ov2 = v2 ? (to_out ? vals2_out : w.tv2) : nullptr;
     const int shift = ps * kRadixBits;
+    // 16-wave tiles for the 8-bit passes (A/B: GATX_RADIX_WAVES=4 keeps 4-wave tiles)
+    static const bool w16 = [] {
+      const char* e = getenv("GATX_RADIX_WAVES");
+      return !(e && strcmp(e, "4") == 0);
+    }();
+    const bool big = !wide && w16 && items >= 4;
     if (wide) radix_hist_kernel<kWideBits><<<(unsigned)nb, 256, 0, stream>>>(ck, n, 0, items, nb, w.hist);
+    else if (big) radix_hist16_kernel<<<(unsigned)nb, 1024, 0, stream>>>(ck, n, shift, items, nb, w.hist);
     else radix_hist_kernel<kRadixBits><<<(unsigned)nb, 256, 0, stream>>>(ck, n, shift, items, nb, w.hist);
     GATX_LAUNCH_CHECK("radix_hist");
     // (a single-workgroup LDS scan measured 35 us on PPI's 80 K counts: rocPRIM's lookback
@@ -528,7 +641,14 @@ int sort_pairs(const int32_t* keys_in, const int32_t* vals_in, int32_t* keys_out
       const char* e = getenv("GATX_RADIX_LDS");
       return !(e && strcmp(e, "0") == 0);
     }();
-    if (v2 && wide)   // (the wide LDS tile has no room for a second value)
+    if (big && lds_tiles) {
+      if (v2)
+        radix_scatter_lds16_kernel<true><<<(unsigned)nb, 1024, 0, stream>>>(
+            ck, cv, n, shift, items, nb, w.offs, w.hist, ok, ov, cv2, ov2);
+      else
+        radix_scatter_lds16_kernel<false><<<(unsigned)nb, 1024, 0, stream>>>(
+            ck, cv, n, shift, items, nb, w.offs, w.hist, ok, ov);
+    } else if (v2 && wide)   // (the wide LDS tile has no room for a second value)
       radix_scatter_kernel<kWideBits, true><<<(unsigned)nb, 256, 0, stream>>>(
           ck, cv, n, 0, items, nb, w.offs, ok, ov, cv2, ov2);
     else if (v2 && lds_tiles)
