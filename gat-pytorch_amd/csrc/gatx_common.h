@@ -79,6 +79,23 @@ __device__ inline float elu_act(float v) {
   return v > 0.f ? v : (v > -0.0625f ? p : e);
 }
 
+// elu_act of two elements, branch-free, the polynomial in packed fp32: the same expression,
+// contracted into the same fma chain as elu_act's (fp-contract), so bit-identical per component.
+// The compiler turns the scalar form's selects into an exec-masked branch per element around the
+// exp and the polynomial; in an epilogue of 128 elements per lane that is a few hundred scalar
+// branch instructions beside the VALU work.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ inline f32x2 elu_act2(f32x2 v) {
+  const f32x2 p = v * ((f32x2)(1.f) + v * ((f32x2)(0.5f) + v * ((f32x2)(1.f / 6.f) +
+                  v * ((f32x2)(1.f / 24.f) + v * (f32x2)(1.f / 120.f)))));
+  const f32x2 w = v * (f32x2)(1.44269504088896341f);
+  const float e0 = __builtin_amdgcn_exp2f(w.x) - 1.f, e1 = __builtin_amdgcn_exp2f(w.y) - 1.f;
+  f32x2 r;
+  r.x = v.x > 0.f ? v.x : (v.x > -0.0625f ? p.x : e0);
+  r.y = v.y > 0.f ? v.y : (v.y > -0.0625f ? p.y : e1);
+  return r;
+}
+
 __device__ inline float4 operator*(float4 a, float s) {
   return make_float4(a.x * s, a.y * s, a.z * s, a.w * s);
 }

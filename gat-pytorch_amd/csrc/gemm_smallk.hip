@@ -49,10 +49,12 @@ __device__ inline void sk_split8(const float (&v)[8], uint4& h, uint4& m, uint4&
 
 // A row-major (k-contiguous, lda), B as rows of k (ldb: B(k, n) = B[n * ldb + k]). VEC: A rows
 // 16-byte aligned (lda % 4 == 0, aligned base), so full 8-k groups load as two float4.
-template <bool VEC, bool ELU>
+// VST: C rows 16-byte aligned (ldc0, c0_bs % 4 == 0, aligned base) for the float4 stores.
+// CB column blocks per pass (4 measured slower: 256 VGPRs, 74 vs 68 us on PPI layer 0).
+template <bool VEC, bool ELU, bool VST, bool FULLN = false, int CB = 2>
 __global__ void __launch_bounds__(64 * SK_WAVES, 1) gemm_smallk_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) char wl[3 * SK_PLANE];
-  __shared__ float bias_l[SK_NMAX];
+  __shared__ __attribute__((aligned(16))) float bias_l[SK_NMAX];
   const int b = blockIdx.y;
   const float* __restrict__ A = g.A + b * g.a_bs;
   const float* __restrict__ B = g.B + b * g.b_bs;
@@ -95,8 +97,13 @@ __global__ void __launch_bounds__(64 * SK_WAVES, 1) gemm_smallk_kernel(GemmArgs 
     for (int s = 0; s < SK_KMAX / 16; ++s) {
       if (s >= nks) break;
       const int k0 = 16 * s + 8 * half;
-      if (VEC && k0 + 8 <= K) {
-        const float4 p = *(const float4*)(ar + k0), q = *(const float4*)(ar + k0 + 4);
+      if (VEC) {
+        // unconditional float4 loads (a float4 starting below K stays inside the row: K <= lda,
+        // lda % 4 == 0; one starting at or past K reads k = 0 instead), the k >= K lanes zeroed
+        // in split_raw: a scalar fallback here wrote registers with vector loads still in
+        // flight, which cost an s_waitcnt vmcnt(0) — all this wave's earlier stores — per block
+        const float4 p = *(const float4*)(ar + (k0 < K ? k0 : 0));
+        const float4 q = *(const float4*)(ar + (k0 + 4 < K ? k0 + 4 : 0));
         raw[s][0] = p.x; raw[s][1] = p.y; raw[s][2] = p.z; raw[s][3] = p.w;
         raw[s][4] = q.x; raw[s][5] = q.y; raw[s][6] = q.z; raw[s][7] = q.w;
       } else {
@@ -108,11 +115,18 @@ __global__ void __launch_bounds__(64 * SK_WAVES, 1) gemm_smallk_kernel(GemmArgs 
   int64_t rb = (int64_t)blockIdx.x * SK_WAVES + wave;
   const int64_t rstep = (int64_t)gridDim.x * SK_WAVES;
   if (rb < nrb) fetch(rb);
+  // the first block's loads are waited for here, so the loop head sees only the back edge's
+  // pending loads (issued before a static number of stores when FULLN)
+  if (FULLN) __builtin_amdgcn_s_waitcnt(0);
   for (; rb < nrb; rb += rstep) {
     bf16x8 fa[SK_KMAX / 16][3];
 #pragma unroll
     for (int s = 0; s < SK_KMAX / 16; ++s) {
       if (s >= nks) break;
+      if (VEC) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) raw[s][j] = 16 * s + 8 * half + j < K ? raw[s][j] : 0.f;
+      }
       uint4 h, m, l;
       sk_split8(raw[s], h, m, l);
       fa[s][0] = __builtin_bit_cast(bf16x8, h);
@@ -120,19 +134,29 @@ __global__ void __launch_bounds__(64 * SK_WAVES, 1) gemm_smallk_kernel(GemmArgs 
       fa[s][2] = __builtin_bit_cast(bf16x8, l);
     }
     if (rb + rstep < nrb) fetch(rb + rstep);
-    for (int cb = 0; cb < ncb; cb += 2) {
-      floatx16 acc[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+    for (int cb = 0; cb < (FULLN ? SK_NMAX / 32 : ncb); cb += CB) {
+      // the bias of this lane's columns (registers 4j..4j+3 are columns cb*32 + 8j + 4*(l >> 5)
+      // + 0..3, see the epilogue), read from LDS ahead of the MFMAs. (Starting the accumulators
+      // at the bias instead cost accuracy: 8.8e-7 vs 3.3e-7 relative on tests' 5612 x 256 x 50
+      // case — the small plane products are then aligned to the bias' exponent.)
+      float4 bv[CB][4];
+#pragma unroll
+      for (int i = 0; i < CB; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bv[i][j] = *(const float4*)&bias_l[(cb + i) * 32 + 4 * half + 8 * j];
+      floatx16 acc[CB];
+#pragma unroll
+      for (int i = 0; i < CB; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
-      const int nb = cb + 1 < ncb ? 2 : 1;
+      const int nb = FULLN ? CB : (ncb - cb < CB ? ncb - cb : CB);
 #pragma unroll
       for (int s = 0; s < SK_KMAX / 16; ++s) {
         if (s >= nks) break;
-        bf16x8 fb[2][3];
+        bf16x8 fb[CB][3];
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < CB; ++i)
 #pragma unroll
           for (int p = 0; p < 3; ++p)
             fb[i][p] = *(const bf16x8*)(wl + p * SK_PLANE +
@@ -143,38 +167,47 @@ __global__ void __launch_bounds__(64 * SK_WAVES, 1) gemm_smallk_kernel(GemmArgs 
 #pragma unroll
         for (int t = 0; t < 6; ++t)
 #pragma unroll
-          for (int i = 0; i < 2; ++i)
-            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][PLA[t]], fb[i][PLB[t]], acc[i],
+          for (int i = 0; i < CB; ++i)   // C^T = B^T A^T: lane = output row, registers = columns
+            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[i][PLB[t]], fa[s][PLA[t]], acc[i],
                                                              0, 0, 0);
       }
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < CB; ++i) {
         if (i >= nb) break;
-        // epilogue (no residual / accumulate on this path): elu?(acc + bias); the bias comes
-        // from LDS, so no global load waits behind this wave's earlier stores. Interior blocks
-        // (every row and column inside the matrix) take a straight-line path of 16 stores with
-        // ELU a compile-time choice: per-element bound checks and a runtime ELU test had made
-        // each store its own exec-masked branch.
-        const int col = (cb + i) * 32 + (lane & 31);
-        const int colc = col < N ? col : N - 1;
-        const float bv = bias_l[colc];
-        float* base = g.C0 + b * g.c0_bs + colc;
-        const int64_t row0 = rb * 32 + 4 * half;
-        if (row0 + 27 < M && (cb + i) * 32 + 32 <= N) {
+        // epilogue (no residual / accumulate on this path): elu?(acc + bias). The product is
+        // formed transposed (B^T A^T), so lane l holds output row rb*32 + (l & 31) and registers
+        // 4j..4j+3 the four consecutive columns cb*32 + 8j + 4*(l >> 5) + 0..3: one 16-byte store
+        // each, four per block instead of sixteen 4-byte ones (the 4-byte stores of the untransposed
+        // layout kept the vector memory pipe busy 4x as long per output byte).
+        int64_t row = rb * 32 + (lane & 31);
+        if (FULLN) {
+          // rows past M store row M - 1's values again (fetch clamped their A rows to M - 1, so
+          // the values are identical): every block issues exactly four stores, the store count
+          // per row block is static, and the next block's A loads (issued before these stores)
+          // are waited for with vmcnt(#stores) instead of vmcnt(0) — a wait on all of this
+          // wave's stores reaching memory
+          row = row < M ? row : M - 1;
+        } else if (row >= M) {
+          continue;
+        }
+        const int c0 = (cb + i) * 32 + 4 * half;
+        float* base = g.C0 + b * g.c0_bs + row * g.ldc0;
+        if (FULLN || (VST && (cb + i) * 32 + 32 <= N)) {
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            float v = acc[i][r] + bv;
-            if (ELU) v = elu_act(v);
-            base[(row0 + (r & 3) + 8 * (r >> 2)) * g.ldc0] = v;
+          for (int j = 0; j < 4; ++j) {
+            f32x2 lo = {acc[i][4 * j] + bv[i][j].x, acc[i][4 * j + 1] + bv[i][j].y};
+            f32x2 hi = {acc[i][4 * j + 2] + bv[i][j].z, acc[i][4 * j + 3] + bv[i][j].w};
+            if (ELU) { lo = elu_act2(lo); hi = elu_act2(hi); }
+            *(float4*)(base + c0 + 8 * j) = make_float4(lo.x, lo.y, hi.x, hi.y);
           }
-        } else if (col < N) {
+        } else {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const int64_t row = row0 + (r & 3) + 8 * (r >> 2);
-            if (row >= M) continue;
-            float v = acc[i][r] + bv;
+            const int col = c0 + 8 * (r >> 2) + (r & 3);
+            if (col >= N) continue;
+            float v = acc[i][r] + bias_l[col];
             if (ELU) v = elu_act(v);
-            base[row * g.ldc0] = v;
+            base[col] = v;
           }
         }
       }
@@ -199,10 +232,19 @@ int launch_gemm_smallk(const gk::GemmArgs& g, int batch, hipStream_t stream) {
   const unsigned gx = (unsigned)std::min<int64_t>(per, ceil_div(nrb, SK_WAVES));
   dim3 grid(gx, (unsigned)batch);
   const bool vec = ((uintptr_t)g.A % 16 == 0) && g.lda % 4 == 0 && g.a_bs % 4 == 0;
-  if (vec && g.elu) gemm_smallk_kernel<true, true><<<grid, 64 * SK_WAVES, 0, stream>>>(g);
-  else if (vec) gemm_smallk_kernel<true, false><<<grid, 64 * SK_WAVES, 0, stream>>>(g);
-  else if (g.elu) gemm_smallk_kernel<false, true><<<grid, 64 * SK_WAVES, 0, stream>>>(g);
-  else gemm_smallk_kernel<false, false><<<grid, 64 * SK_WAVES, 0, stream>>>(g);
+  const bool vst = ((uintptr_t)g.C0 % 16 == 0) && g.ldc0 % 4 == 0 && g.c0_bs % 4 == 0;
+#define GATX_SK(V, E)                                                                          \
+  do {                                                                                         \
+    if (vst && g.N == SK_NMAX)                                                                 \
+      gemm_smallk_kernel<V, E, true, true><<<grid, 64 * SK_WAVES, 0, stream>>>(g);             \
+    else if (vst) gemm_smallk_kernel<V, E, true><<<grid, 64 * SK_WAVES, 0, stream>>>(g);       \
+    else gemm_smallk_kernel<V, E, false><<<grid, 64 * SK_WAVES, 0, stream>>>(g);               \
+  } while (0)
+  if (vec && g.elu) GATX_SK(true, true);
+  else if (vec) GATX_SK(true, false);
+  else if (g.elu) GATX_SK(false, true);
+  else GATX_SK(false, false);
+#undef GATX_SK
   GATX_LAUNCH_CHECK("gemm_smallk");
   return 0;
 }
