@@ -221,7 +221,9 @@ __device__ inline void x3_mainloop(const GemmArgs& g, const float* __restrict__ 
       for (int mi = 0; mi < MB; ++mi)
 #pragma unroll
         for (int ni = 0; ni < NB; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[mi][PLA[t]], fb[ni][PLB[t]],
+          // C^T = B^T A^T (operand roles swapped): lane = output row, registers = columns,
+          // see write_tile_t
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[ni][PLB[t]], fa[mi][PLA[t]],
                                                                 acc[mi][ni], 0, 0, 0);
   };
   auto load_full = [&]() {
@@ -277,6 +279,129 @@ __device__ inline void x3_mainloop(const GemmArgs& g, const float* __restrict__ 
   }
 }
 
+// Epilogue of the transposed product. acc[mi][ni] is the C^T block of output rows
+// rb = wm*MB*32 + mi*32 and columns cb = wn*NB*32 + ni*32: lane l holds row rb + (l & 31),
+// registers 4j..4j+3 the four consecutive columns cb + 8j + 4(l >> 5) + 0..3. Every group of
+// four is one 16-byte load / store where it lies inside one output range and is aligned (the
+// C layout of the untransposed product stores a dword per lane), else per element (store_out's
+// order of operations either way: ((acc + C) + bias) + resid, then ELU).
+__device__ inline float4 f4_of(const floatx16& a, int j) {
+  return make_float4(a[4 * j], a[4 * j + 1], a[4 * j + 2], a[4 * j + 3]);
+}
+
+template <int MB, int NB, int TBM, int TBN>
+__device__ inline void write_tile_t(const GemmArgs& g, floatx16 (&acc)[MB][NB], int tail_z,
+                                    int64_t tail_ti, int64_t m0, int64_t n0, int wm, int wn,
+                                    int lane) {
+  const int lr = lane & 31, lc = 4 * (lane >> 5);
+  const int64_t M = g.M, N = g.N;
+  if (tail_z >= 0) {   // tail slice: tile-local partial [TBM][TBN], summed by tail_fixup_kernel
+    float* P = g.tail_partial + ((int64_t)tail_z * g.tail_rem + tail_ti) * (TBM * TBN);
+#pragma unroll
+    for (int mi = 0; mi < MB; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NB; ++ni)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int rl = wm * (MB * 32) + mi * 32 + lr, cl = wn * (NB * 32) + ni * 32 + 8 * j + lc;
+          *(float4*)(P + rl * TBN + cl) = f4_of(acc[mi][ni], j);
+        }
+    return;
+  }
+  if (g.splits > 1) {   // partial slab z: plain [M][N], reduced by splitk_reduce_kernel
+    float* P = g.partial + ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * M * N;
+#pragma unroll
+    for (int mi = 0; mi < MB; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NB; ++ni) {
+        const int64_t row = m0 + wm * (MB * 32) + mi * 32 + lr;
+        if (row >= M) continue;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int64_t col = n0 + wn * (NB * 32) + ni * 32 + 8 * (r >> 2) + lc + (r & 3);
+          if (col < N) P[row * N + col] = acc[mi][ni][r];
+        }
+      }
+    return;
+  }
+  const int64_t b = blockIdx.y;
+#pragma unroll
+  for (int ni = 0; ni < NB; ++ni) {
+    // the block column's range, decided per 32 columns (wave-uniform): one output range,
+    // inside N, 16-byte aligned rows -> float4 groups; otherwise store_out per element
+    const int64_t cb = n0 + wn * (NB * 32) + ni * 32;
+    const bool first = cb < g.n_split;
+    float* base;
+    int64_t ldc, cc;
+    if (first) { base = g.C0 + b * g.c0_bs; ldc = g.ldc0; cc = cb; }
+    else if (cb < g.n_split2) { base = g.C1 + b * g.c1_bs; ldc = g.ldc1; cc = cb - g.n_split; }
+    else { base = g.C2; ldc = g.ldc2; cc = cb - g.n_split2; }
+    const int64_t lim = first ? g.n_split : (cb < g.n_split2 ? g.n_split2 : INT64_MAX);
+    const bool vec = cb + 32 <= N && cb + 32 <= lim && ldc % 4 == 0 &&
+                     ((uintptr_t)(base + cc) % 16) == 0;
+    if (!vec) {
+#pragma unroll
+      for (int mi = 0; mi < MB; ++mi) {
+        const int64_t row = m0 + wm * (MB * 32) + mi * 32 + lr;
+        if (row >= M) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float4 v = f4_of(acc[mi][ni], j);
+          const int64_t col = cb + 8 * j + lc;
+          if (col < N) store_out(g, b, row, col, v.x);
+          if (col + 1 < N) store_out(g, b, row, col + 1, v.y);
+          if (col + 2 < N) store_out(g, b, row, col + 2, v.z);
+          if (col + 3 < N) store_out(g, b, row, col + 3, v.w);
+        }
+      }
+      continue;
+    }
+    const bool epi = first && (g.bias || g.resid || g.elu);
+    float4 bias[4];   // loaded before this block column's stores (loads and stores share vmcnt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      bias[j] = (first && g.bias) ? *(const float4*)(g.bias + b * g.bias_bs + cc + 8 * j + lc)
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float* rbase = (first && g.resid) ? g.resid + b * g.resid_bs + cb + lc : nullptr;
+    const bool rvec = rbase && g.resid_ld % 4 == 0 && ((uintptr_t)rbase % 16) == 0;
+#pragma unroll
+    for (int mi = 0; mi < MB; ++mi) {
+      const int64_t row = m0 + wm * (MB * 32) + mi * 32 + lr;
+      if (row >= M) continue;
+      float* d = base + row * ldc + cc + lc;
+      float4 v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = f4_of(acc[mi][ni], j);
+      if (g.accumulate || rbase) {   // the block's loads before its stores
+        float4 cv[4], rv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          cv[j] = g.accumulate ? *(const float4*)(d + 8 * j) : make_float4(0.f, 0.f, 0.f, 0.f);
+          const float* rp = rbase ? rbase + row * g.resid_ld + 8 * j : nullptr;
+          rv[j] = !rp ? make_float4(0.f, 0.f, 0.f, 0.f)
+                      : (rvec ? *(const float4*)rp : make_float4(rp[0], rp[1], rp[2], rp[3]));
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {   // store_out's order: ((acc + C) + bias) + resid
+          if (g.accumulate) v[j] = add4(v[j], cv[j]);
+          if (first && g.bias) v[j] = add4(v[j], bias[j]);
+          if (rbase) v[j] = add4(v[j], rv[j]);
+        }
+      } else if (first && g.bias) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = add4(v[j], bias[j]);
+      }
+      if (epi && g.elu) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          v[j] = make_float4(elu_act(v[j].x), elu_act(v[j].y), elu_act(v[j].z), elu_act(v[j].w));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) *(float4*)(d + 8 * j) = v[j];
+    }
+  }
+}
+
 template <bool A_KC, bool B_KC, bool VEC, int TAG, int CFG, int DBG = 0>
 __global__ void __launch_bounds__(X3Cfg<CFG>::NT, X3Cfg<CFG>::MINB) gemm_x3_kernel(GemmArgs g) {
   using C = X3Cfg<CFG>;
@@ -325,7 +450,7 @@ __global__ void __launch_bounds__(X3Cfg<CFG>::NT, X3Cfg<CFG>::MINB) gemm_x3_kern
     else
       x3_mainloop<A_KC, B_KC, true, CFG, DBG>(g, A, B, m0, n0, kb, K, nk, smem, wm, wn, lane, acc);
   }
-  write_tile<C::MB, C::NB, C::TBM, C::TBN>(g, acc, tail_z, tail_ti, m0, n0, wm, wn, lane);
+  write_tile_t<C::MB, C::NB, C::TBM, C::TBN>(g, acc, tail_z, tail_ti, m0, n0, wm, wn, lane);
 }
 
 }  // namespace

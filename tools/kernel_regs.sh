@@ -8,9 +8,9 @@ cur=None; rows=[]
 for l in sys.stdin:
     m=re.search(r'Function Name: (\S+)',l)
     if m: cur={'n':m.group(1)}; rows.append(cur); continue
-    m=re.search(r'remark:\s+(VGPRs|AGPRs|VGPRs Spill|SGPRs Spill|Occupancy \[waves/SIMD\]|LDS Size \[bytes/block\]): (\d+)',l)
+    m=re.search(r'remark:\s+(VGPRs|AGPRs|VGPRs Spill|SGPRs Spill|ScratchSize \[bytes/lane\]|Occupancy \[waves/SIMD\]|LDS Size \[bytes/block\]): (\d+)',l)
     if m and cur is not None: cur[m.group(1)]=m.group(2)
 for r in rows:
     if re.search(sys.argv[1], r['n']):
-        print(f\"{r['n'][:90]:90s} v={r.get('VGPRs')} a={r.get('AGPRs')} vsp={r.get('VGPRs Spill')} ssp={r.get('SGPRs Spill')} occ={r.get('Occupancy [waves/SIMD]')} lds={r.get('LDS Size [bytes/block]')}\")
+        print(f\"{r['n'][:90]:90s} v={r.get('VGPRs')} a={r.get('AGPRs')} vsp={r.get('VGPRs Spill')} ssp={r.get('SGPRs Spill')} scr={r.get('ScratchSize [bytes/lane]')} occ={r.get('Occupancy [waves/SIMD]')} lds={r.get('LDS Size [bytes/block]')}\")
 " "$flt"
