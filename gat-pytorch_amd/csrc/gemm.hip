@@ -109,6 +109,66 @@ __global__ void __launch_bounds__(256) tail_fixup_kernel(GemmArgs g) {
   }
 }
 
+// Tail fix-up of a projection with fused scores (g.s_part): block (tail tile, 64-row chunk), a
+// wave per row, lane l the four columns 4l..4l+3; the K-slices summed in slice order exactly as
+// tail_fixup_kernel, stored, then the row's share of each score reduced over the wave in a fixed
+// butterfly into s_part[tn][row][h]. The tile's A2 columns are staged in LDS once per block.
+__global__ void __launch_bounds__(256) tail_fixup_scores_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) float a2s[16 * 256];   // [H2][bn]
+  const int BN = g.bn, H2 = g.s_h2, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t TS = (int64_t)g.bm * BN, chunks = g.bm / 64;
+  const int64_t ti = blockIdx.x / chunks, ch = blockIdx.x - ti * chunks;
+  const int64_t lin = g.dp_blocks + ti, tm = lin / g.tiles_n, tn = lin - tm * g.tiles_n;
+  for (int t = threadIdx.x; t < H2 * BN; t += 256) {
+    const int h = t / BN, c = t - h * BN;
+    const int64_t col = tn * BN + c;
+    a2s[t] = col < g.N ? score_weight(g.s_a, g.s_nh, g.s_f, g.s_fp, h, col) : 0.f;
+  }
+  __syncthreads();
+  const int cl = 4 * lane;
+  for (int r = wave; r < 64; r += 4) {
+    const int64_t rl = ch * 64 + r, row = tm * g.bm + rl;
+    if (row >= g.M) break;   // wave-uniform
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (cl < BN) {
+      for (int z = 0; z < g.tail_s; ++z) {
+        const float4 p = *(const float4*)(g.tail_partial + ((int64_t)z * g.tail_rem + ti) * TS +
+                                          rl * BN + cl);
+        v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w;
+      }
+      const int64_t col = tn * BN + cl;
+      if (col < g.N) store_out(g, 0, row, col, v.x);
+      if (col + 1 < g.N) store_out(g, 0, row, col + 1, v.y);
+      if (col + 2 < g.N) store_out(g, 0, row, col + 2, v.z);
+      if (col + 3 < g.N) store_out(g, 0, row, col + 3, v.w);
+    }
+    for (int h = 0; h < H2; ++h) {
+      float t = 0.f;
+      if (cl < BN) {
+        const float4 w = *(const float4*)(a2s + h * BN + cl);
+        t = fmaf(v.x, w.x, t);
+        t = fmaf(v.y, w.y, t);
+        t = fmaf(v.z, w.z, t);
+        t = fmaf(v.w, w.w, t);
+      }
+      for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
+      if (lane == 0) g.s_part[(tn * g.M + row) * H2 + h] = t;
+    }
+  }
+}
+
+// S = sum over the column tiles of the fused-score partials, in tile order (deterministic).
+__global__ void __launch_bounds__(256) score_combine_kernel(const float* __restrict__ part,
+                                                            int64_t MH, int tiles,
+                                                            float* __restrict__ S) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < MH;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    float v = part[t];
+    for (int k = 1; k < tiles; ++k) v += part[k * MH + t];
+    S[t] = v;
+  }
+}
+
 // A_KC: A is k-contiguous (sak == 1, ld = sam) else m-contiguous; B_KC: B is k-contiguous
 // (sbk == 1, ld = sbn) else n-contiguous. TAG only separates the symbol names of the call sites
 // in profiles (0 = forward projection, 1 = auxiliary products, 2 = split-K weight gradient).
@@ -282,7 +342,10 @@ int launch_gemm(const GemmArgs& g0, bool a_kc, bool b_kc, int batch, hipStream_t
     splitk_reduce_kernel<<<rg, 256, 0, stream>>>(g, batch);
     GATX_LAUNCH_CHECK("splitk_reduce");
   }
-  if (g.tail_s > 1) {
+  if (g.tail_s > 1 && g.s_part) {
+    tail_fixup_scores_kernel<<<(unsigned)(g.tail_rem * (g.bm / 64)), 256, 0, stream>>>(g);
+    GATX_LAUNCH_CHECK("tail_fixup_scores");
+  } else if (g.tail_s > 1) {
     const int64_t total = g.tail_rem * g.bm * g.bn;
     tail_fixup_kernel<<<(unsigned)std::min<int64_t>(ceil_div(total, 256), 8192), 256, 0, stream>>>(g);
     GATX_LAUNCH_CHECK("tail_fixup");
@@ -417,6 +480,17 @@ extern "C" int gatx_transpose_f32(int64_t rows, int64_t cols, const float* src, 
   return 0;
 }
 
+// A node-score request riding on a projection (gatx_projection_gemm_scores).
+struct ScoreReq {
+  const float* a;
+  int nh, f;
+  float* S;
+};
+// Bytes of the per-column-tile score partials (0: one column tile writes S directly).
+static size_t score_part_bytes(int64_t tiles_n, int64_t M, int nh) {
+  return tiles_n > 1 ? (size_t)tiles_n * M * 2 * nh * sizeof(float) + 256 : 0;
+}
+
 static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A, int64_t sam,
                      int64_t sak, int64_t a_bs, const float* B, int64_t sbk, int64_t sbn,
                      int64_t b_bs, float* C0, int64_t ldc0, int64_t c0_bs, int64_t n_split,
@@ -424,7 +498,8 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
                      int64_t bias_bs, const float* resid, int64_t resid_ld, int64_t resid_bs,
                      int elu, void* workspace, size_t workspace_bytes, int tag,
                      hipStream_t stream, int64_t n_split2 = -1, float* C2 = nullptr,
-                     int64_t ldc2 = 0) {
+                     int64_t ldc2 = 0, const ScoreReq* sc = nullptr, bool* fused = nullptr) {
+  if (fused) *fused = false;
   GATX_REQUIRE(M >= 0 && N >= 0 && K >= 0 && batch >= 1, "gemm: negative size");
   if (M == 0 || N == 0) return 0;
   GATX_REQUIRE(sak == 1 || sam == 1, "gemm: A needs a unit stride");
@@ -449,6 +524,7 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
   g.resid = resid; g.resid_ld = resid_ld; g.resid_bs = resid_bs;
   g.elu = elu;
   g.splits = 1; g.k_per_split = K; g.partial = nullptr;
+  g.s_a = nullptr; g.s_nh = g.s_f = g.s_fp = g.s_h2 = 0; g.s_part = nullptr;
   auto aligned = [](const void* p, int64_t ld, int64_t bs) {
     return ((uintptr_t)p % 16 == 0) && (ld % 4 == 0) && (bs % 4 == 0);
   };
@@ -483,6 +559,18 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
   g.tail_partial = nullptr;
   const int64_t tiles = g.tiles_m * g.tiles_n * batch;
   const int64_t slots = resident_blocks(kd);
+  // fused scores: x3 tiles, one batch entry, no split-K; the partials take the workspace's end
+  float* s_part = nullptr;
+  if (sc && kd.id >= 1 && batch == 1 && tag == 0 && !accumulate) {
+    const size_t pb = score_part_bytes(g.tiles_n, M, sc->nh);
+    if (pb == 0) {
+      s_part = sc->S;
+    } else if (workspace && workspace_bytes >= pb) {
+      const size_t off = (workspace_bytes - pb) / 256 * 256;
+      s_part = (float*)((char*)workspace + off);
+      workspace_bytes = off;
+    }
+  }
   if (workspace && tag == 2) {   // explicit split-K into [M][N] slabs
     int sp = choose_splits(tiles, K, slots);
     while (sp > 1 && (size_t)sp * batch * M * N * sizeof(float) > workspace_bytes) --sp;
@@ -508,9 +596,23 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
       }
     }
   }
-  if (tag == 0) return launch_gemm<0>(g, a_kc, b_kc, batch, stream);
-  if (tag == 2) return launch_gemm<2>(g, a_kc, b_kc, batch, stream);
-  return launch_gemm<1>(g, a_kc, b_kc, batch, stream);
+  if (s_part) {
+    g.s_a = sc->a; g.s_nh = sc->nh; g.s_f = sc->f; g.s_fp = (int)round_up(sc->f, 4);
+    g.s_h2 = 2 * sc->nh; g.s_part = s_part;
+  }
+  if (tag == 0) GATX_CALL(launch_gemm<0>(g, a_kc, b_kc, batch, stream));
+  else if (tag == 2) GATX_CALL(launch_gemm<2>(g, a_kc, b_kc, batch, stream));
+  else GATX_CALL(launch_gemm<1>(g, a_kc, b_kc, batch, stream));
+  if (s_part) {
+    if (s_part != sc->S) {
+      const int64_t MH = M * g.s_h2;
+      score_combine_kernel<<<(unsigned)std::min<int64_t>(ceil_div(MH, 256), 4096), 256, 0,
+                             stream>>>(s_part, MH, (int)g.tiles_n, sc->S);
+      GATX_LAUNCH_CHECK("score_combine");
+    }
+    if (fused) *fused = true;
+  }
+  return 0;
 }
 
 extern "C" void gatx_set_gemm_mode(int mode) { g_gemm_mode = mode ? 1 : 0; }
@@ -555,6 +657,36 @@ extern "C" int gatx_projection_gemm3(int64_t M, int64_t N, int64_t K, const floa
   return gemm_impl(M, N, K, 1, A, sam, sak, 0, B, sbk, sbn, 0, C0, ldc0, 0, n_split, C1, ldc1, 0,
                    0, nullptr, 0, nullptr, 0, 0, 0, workspace, workspace_bytes, 0,
                    (hipStream_t)s, n_split2, C2, ldc2);
+}
+
+extern "C" size_t gatx_projection_scores_workspace_bytes(int64_t M, int64_t N, int64_t K,
+                                                         int NH) {
+  const Kind kd = choose_kind(M, N);
+  return gatx_gemm_workspace_bytes(M, N, K) + score_part_bytes(ceil_div(N, kd.bn), M, NH);
+}
+
+extern "C" int gatx_projection_gemm_scores(int64_t M, int64_t N, int64_t K, const float* A,
+                                           int64_t sam, int64_t sak, const float* B, int64_t sbk,
+                                           int64_t sbn, float* C0, int64_t ldc0, const float* a,
+                                           int NH, int F, float* S, void* workspace,
+                                           size_t workspace_bytes, gatx_stream_t s) {
+  GATX_REQUIRE(NH >= 1 && F >= 1 && N == (int64_t)NH * round_up(F, 4) && ldc0 == N,
+               "projection_gemm_scores: C0 must be the packed [M][NH * round4(F)] Wh");
+  const ScoreReq sc{a, NH, F, S};
+  bool fused = false;
+  if (2 * NH <= 16 && M > 0) {
+    GATX_CALL(gemm_impl(M, N, K, 1, A, sam, sak, 0, B, sbk, sbn, 0, C0, ldc0, 0, N, nullptr, 0,
+                        0, 0, nullptr, 0, nullptr, 0, 0, 0, workspace, workspace_bytes, 0,
+                        (hipStream_t)s, -1, nullptr, 0, &sc, &fused));
+  } else {
+    GATX_CALL(gemm_impl(M, N, K, 1, A, sam, sak, 0, B, sbk, sbn, 0, C0, ldc0, 0, N, nullptr, 0,
+                        0, 0, nullptr, 0, nullptr, 0, 0, 0, workspace, workspace_bytes, 0,
+                        (hipStream_t)s));
+  }
+  // shapes without the fused epilogue (f32 arithmetic, small-K / tiny kernels, > 8 heads): the
+  // score pass over the stored Wh
+  if (!fused) return gatx_node_scores(C0, M, NH, F, a, S, s);
+  return 0;
 }
 
 extern "C" int gatx_gemm_f32_batched(int64_t batch, int64_t M, int64_t N, int64_t K,

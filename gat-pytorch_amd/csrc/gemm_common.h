@@ -117,7 +117,21 @@ struct GemmArgs {
   // tail split (splits == 1): blocks >= dp_blocks each take K-slice z of one of the last
   // tail_rem tiles and write a BM x BN partial; tail_fixup_kernel sums the slices in z order
   int64_t dp_blocks, tail_rem; int tail_s, bm, bn; float* tail_partial;
+  // node scores fused into the forward projection (x3 tiles, s_part != nullptr): every column
+  // tile tn adds its columns' share of S = Wh . A2^T as s_part[tn][row][s_h2], A2 read from the
+  // reference's attention vector s_a (heads s_nh, features s_f, padded s_fp per head of Wh)
+  const float* s_a; int s_nh, s_f, s_fp, s_h2; float* s_part;
 };
+
+// A2[h2][col] of the attention vector a (models/gat_layer.py:76-82 split per half): the weight of
+// Wh column col = head k, feature f (Wh rows padded to fp per head) in score h2 (< nh: source
+// half of head h2, else destination half of head h2 - nh); 0 on padding.
+__device__ inline float score_weight(const float* a, int nh, int F, int fp, int h2, int64_t col) {
+  const int k = (int)(col / fp), f = (int)(col - (int64_t)k * fp);
+  if (f >= F || k >= nh) return 0.f;
+  const int hh = h2 < nh ? h2 : h2 - nh;
+  return a[(int64_t)hh * 2 * nh * F + k * 2 * F + (h2 < nh ? 0 : F) + f];
+}
 
 // C = elu?(v (+C) + bias + resid) for one output element (columns >= n_split go to C1 raw,
 // columns >= n_split2 to C2 raw)

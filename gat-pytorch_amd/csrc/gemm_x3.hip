@@ -402,6 +402,60 @@ __device__ inline void write_tile_t(const GemmArgs& g, floatx16 (&acc)[MB][NB], 
   }
 }
 
+// Fused node scores of one finished output tile (the forward projection, g.s_part set): the
+// tile's share of S[row][h] = sum_col Wh[row][col] A2[h][col] over its TBN columns, written as
+// s_part[tn][row][h] (combined over the column tiles in a fixed order by score_combine_kernel).
+// A lane holds 16 columns of one row per block (write_tile_t's layout), so a head's partial is
+// a register dot product plus one exchange between the two lane halves; the WGN waves sharing
+// the rows are summed in wave order through LDS. Runs after the tile's stores, acc still live.
+template <int MB, int NB, int TBM, int TBN, int WGN>
+__device__ inline void scores_tile(const GemmArgs& g, const floatx16 (&acc)[MB][NB], int64_t m0,
+                                   int64_t n0, int64_t tn, int wm, int wn, int lane, char* smem) {
+  const int H2 = g.s_h2, lr = lane & 31, lc = 4 * (lane >> 5);
+  float* a2s = (float*)smem;              // [H2][TBN]
+  float* red = a2s + H2 * TBN;            // [WGN][TBM][H2]
+  for (int t = threadIdx.x; t < H2 * TBN; t += 64 * WGN * (TBM / (MB * 32))) {
+    const int h = t / TBN, c = t - h * TBN;
+    const int64_t col = n0 + c;
+    a2s[t] = col < g.N ? score_weight(g.s_a, g.s_nh, g.s_f, g.s_fp, h, col) : 0.f;
+  }
+  __syncthreads();
+  for (int h = 0; h < H2; ++h) {
+    float t[MB];
+#pragma unroll
+    for (int mi = 0; mi < MB; ++mi) t[mi] = 0.f;
+#pragma unroll
+    for (int ni = 0; ni < NB; ++ni)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float4 w = *(const float4*)(a2s + h * TBN + wn * (NB * 32) + ni * 32 + 8 * j + lc);
+#pragma unroll
+        for (int mi = 0; mi < MB; ++mi) {
+          t[mi] = fmaf(acc[mi][ni][4 * j], w.x, t[mi]);
+          t[mi] = fmaf(acc[mi][ni][4 * j + 1], w.y, t[mi]);
+          t[mi] = fmaf(acc[mi][ni][4 * j + 2], w.z, t[mi]);
+          t[mi] = fmaf(acc[mi][ni][4 * j + 3], w.w, t[mi]);
+        }
+      }
+#pragma unroll
+    for (int mi = 0; mi < MB; ++mi) {
+      const float tot = t[mi] + __shfl_xor(t[mi], 32);   // the same sum in both halves
+      if (lane < 32) red[(wn * TBM + wm * (MB * 32) + mi * 32 + lr) * H2 + h] = tot;
+    }
+  }
+  __syncthreads();
+  float* P = g.s_part + tn * g.M * H2;
+  for (int t = threadIdx.x; t < TBM * H2; t += 64 * WGN * (TBM / (MB * 32))) {
+    const int rl = t / H2, h = t - rl * H2;
+    const int64_t row = m0 + rl;
+    if (row >= g.M) continue;
+    float v = red[rl * H2 + h];
+#pragma unroll
+    for (int w = 1; w < WGN; ++w) v += red[(w * TBM + rl) * H2 + h];
+    P[row * H2 + h] = v;
+  }
+}
+
 template <bool A_KC, bool B_KC, bool VEC, int TAG, int CFG, int DBG = 0>
 __global__ void __launch_bounds__(X3Cfg<CFG>::NT, X3Cfg<CFG>::MINB) gemm_x3_kernel(GemmArgs g) {
   using C = X3Cfg<CFG>;
@@ -451,6 +505,10 @@ __global__ void __launch_bounds__(X3Cfg<CFG>::NT, X3Cfg<CFG>::MINB) gemm_x3_kern
       x3_mainloop<A_KC, B_KC, true, CFG, DBG>(g, A, B, m0, n0, kb, K, nk, smem, wm, wn, lane, acc);
   }
   write_tile_t<C::MB, C::NB, C::TBM, C::TBN>(g, acc, tail_z, tail_ti, m0, n0, wm, wn, lane);
+  // (tail slices are scored by tail_fixup_scores_kernel once summed)
+  if constexpr (TAG == 0 && DBG == 0)
+    if (g.s_part && tail_z < 0)
+      scores_tile<C::MB, C::NB, C::TBM, C::TBN, C::WGN>(g, acc, m0, n0, tn, wm, wn, lane, smem);
 }
 
 }  // namespace

@@ -61,6 +61,9 @@ SIGNATURES = {
     "gatx_pad_rows": (c_i, [P, c_i64, c_i64, c_i64, P, c_i64, P]),
     "gatx_projection_gemm": (c_i, [c_i64, c_i64, c_i64, P, c_i64, c_i64, P, c_i64, c_i64, P,
                                    c_i64, c_i64, P, c_i64, P, c_sz, P]),
+    "gatx_projection_scores_workspace_bytes": (c_sz, [c_i64, c_i64, c_i64, c_i]),
+    "gatx_projection_gemm_scores": (c_i, [c_i64, c_i64, c_i64, P, c_i64, c_i64, P, c_i64, c_i64,
+                                          P, c_i64, P, c_i, c_i, P, P, c_sz, P]),
     "gatx_projection_gemm3": (c_i, [c_i64, c_i64, c_i64, P, c_i64, c_i64, P, c_i64, c_i64, P,
                                     c_i64, c_i64, P, c_i64, c_i64, P, c_i64, P, c_sz, P]),
     "gatx_prepare_weights_skip": (c_i, [P, P, c_i, c_i, c_i64, P, c_i, c_i64, P, P]),

@@ -400,6 +400,14 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
             call("gatx_projection_gemm", N, sh.K_aug, sh.F_in, ptr(x), sh.F_in, 1, ptr(W_aug), 1,
                  sh.F_in, ptr(Wh), sh.Dp, sh.Dp, ptr(S), max(sh.H2, 1),
                  *gemm_workspace(N, sh.K_aug, sh.F_in, dev), s)
+    elif _env_int("GATX_FUSED_SCORES", 1):
+        # S reduced from the projection's accumulators in its epilogue (no second read of Wh)
+        with _span("gemm", (N, sh.Dp, sh.F_in, sh.NH, sh.F)):
+            nb = lib.gatx_projection_scores_workspace_bytes(N, sh.Dp, sh.F_in, sh.NH)
+            ws = torch.empty(max(nb, 1), dtype=torch.uint8, device=dev)
+            call("gatx_projection_gemm_scores", N, sh.Dp, sh.F_in, ptr(x), sh.F_in, 1,
+                 ptr(W_aug), 1, sh.F_in, ptr(Wh), sh.Dp, ptr(a), sh.NH, sh.F, ptr(S), ptr(ws),
+                 nb, s)
     else:
         with _span("gemm", (N, sh.Dp, sh.F_in, sh.NH, sh.F)):
             call("gatx_projection_gemm", N, sh.Dp, sh.F_in, ptr(x), sh.F_in, 1, ptr(W_aug), 1,

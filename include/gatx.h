@@ -169,6 +169,18 @@ int gatx_projection_gemm3(int64_t M, int64_t N, int64_t K, const float* A, int64
                           int64_t ldc0, int64_t n_split, float* C1, int64_t ldc1,
                           int64_t n_split2, float* C2, int64_t ldc2, void* workspace,
                           size_t workspace_bytes, gatx_stream_t stream);
+/* The projection Wh = x . W^T (C0, packed [M][NH * round4(F)], ldc0 == N) with the per-node
+ * logit factors S[m][0..2NH) = (Wh[m] . A_src^T | Wh[m] . A_dst^T) (gatx_node_scores' result,
+ * models/gat_layer.py:76-82) reduced in the GEMM's epilogue from the accumulators: no second
+ * read of Wh. `a` is the reference's attention vector [NH][2 * NH * F]. Per-column-tile partials
+ * are summed in a fixed order (deterministic). Shapes without the fused epilogue (f32
+ * arithmetic, small products, NH > 8) run the projection and then gatx_node_scores. Workspace:
+ * gatx_projection_scores_workspace_bytes (the tail split's slices plus the partials). */
+size_t gatx_projection_scores_workspace_bytes(int64_t M, int64_t N, int64_t K, int NH);
+int gatx_projection_gemm_scores(int64_t M, int64_t N, int64_t K, const float* A, int64_t sam,
+                                int64_t sak, const float* B, int64_t sbk, int64_t sbn, float* C0,
+                                int64_t ldc0, const float* a, int NH, int F, float* S,
+                                void* workspace, size_t workspace_bytes, gatx_stream_t stream);
 /* Its gradient: g_W_skip[h*cols + c][i] = g_eff[c][i] / heads for every head block h. */
 int gatx_skip_weight_grad(const float* g_eff, int heads, int64_t cols, int64_t F_in, float* g_W,
                           gatx_stream_t stream);

@@ -541,6 +541,55 @@ def test_gemm_splitk_and_node_scores(device):
         assert (S[:, NH:].double() - ref_dst).abs().max().item() < tol, (NH, F)
 
 
+def test_projection_gemm_scores(device):
+    """gatx_projection_gemm_scores (csrc/gemm.hip, gemm_x3.hip: S reduced from the projection's
+    accumulators, per-column-tile partials combined in order; tail slices scored by
+    tail_fixup_scores_kernel) against the plain projection + gatx_node_scores and fp64: Wh
+    bitwise equal to the plain projection, S within the fp32 GEMV tolerance, bitwise repeatable;
+    shapes with 256- and 128-wide tiles, a tail split, padded heads (F % 4 != 0), one column
+    tile (partials written to S directly) and the > 8 heads fallback."""
+    from gatx import data as gd
+    from gatx._lib import call, lib, ptr, stream
+    cases = [(44900, 4, 256, 1024), (5000, 4, 64, 300), (2245, 6, 121, 1024), (700, 8, 16, 96),
+             (3000, 1, 60, 50), (1500, 9, 8, 64)]
+    for (M, NH, F, K) in cases:
+        Fp = -(-F // 4) * 4
+        N = NH * Fp
+        x = torch.from_numpy(gd.normal(11, M * K).reshape(M, K)).to(device)
+        W = torch.from_numpy(gd.normal(12, N * K).reshape(N, K)).to(device) * K ** -0.5
+        W.view(NH, Fp, K)[:, F:, :] = 0
+        a = torch.from_numpy(gd.xavier_uniform(13, NH, NH * 2 * F)).to(device)
+        nb = lib.gatx_projection_scores_workspace_bytes(M, N, K, NH)
+        ws = torch.empty(max(nb, 1), dtype=torch.uint8, device=device)
+        outs = []
+        for _ in range(2):
+            Wh = torch.full((M, N), float("nan"), device=device)
+            S = torch.full((M, 2 * NH), float("nan"), device=device)
+            call("gatx_projection_gemm_scores", M, N, K, ptr(x), K, 1, ptr(W), 1, K, ptr(Wh), N,
+                 ptr(a), NH, F, ptr(S), ptr(ws), nb, stream())
+            outs.append((Wh, S))
+        nb0 = lib.gatx_gemm_workspace_bytes(M, N, K)
+        ws0 = torch.empty(max(nb0, 1), dtype=torch.uint8, device=device)
+        Wh0 = torch.full((M, N), float("nan"), device=device)
+        S0 = torch.full((M, 2 * NH), float("nan"), device=device)
+        call("gatx_projection_gemm", M, N, K, ptr(x), K, 1, ptr(W), 1, K, ptr(Wh0), N, N, None,
+             0, ptr(ws0), nb0, stream())
+        call("gatx_node_scores", ptr(Wh0), M, NH, F, ptr(a), ptr(S0), stream())
+        torch.cuda.synchronize()
+        (Wh, S), (Wh2, S2) = outs
+        assert torch.equal(Wh, Wh0), (M, NH, F, K)
+        assert torch.equal(Wh, Wh2) and torch.equal(S, S2), (M, NH, F, K)
+        A = a.view(NH, NH, 2, F).double()
+        Whv = Wh0.view(M, NH, Fp)[:, :, :F].double()
+        ref = torch.cat([torch.einsum("nkf,hkf->nh", Whv, A[:, :, 0]),
+                         torch.einsum("nkf,hkf->nh", Whv, A[:, :, 1])], dim=1)
+        scale = torch.cat([torch.einsum("nkf,hkf->nh", Whv.abs(), A[:, :, 0].abs()),
+                           torch.einsum("nkf,hkf->nh", Whv.abs(), A[:, :, 1].abs())], dim=1)
+        err = ((S.double() - ref).abs() / (scale + 1e-30)).max().item()
+        err0 = ((S0.double() - ref).abs() / (scale + 1e-30)).max().item()
+        assert err < 2e-6, (M, NH, F, K, err, err0)
+
+
 @pytest.mark.parametrize("name", MODEL_CASES)
 def test_attention_norm_matches_reference(name, device):
     """Fused calc_attention_norm (gatx_attention_norm) on the reference's own alphas and
