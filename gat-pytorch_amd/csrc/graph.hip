@@ -437,13 +437,15 @@ __global__ void __launch_bounds__(256) radix_scatter_lds_kernel(
 // many waves per CU overlap the rounds' LDS and barrier latency (the PPI pass kept ~1.2
 // four-wave blocks per CU busy). Same stable order: ranks within a wave by ballots, across
 // waves through the per-(wave, digit) counts, across rounds through the running digit bases.
-template <bool V2>
+// DS (digit scan): offs holds each digit's exclusive prefix over the blocks and dtot (256) the
+// digit totals (radix_digit_scan_kernel); the digit bases come from a scan of dtot here.
+template <bool V2, bool DS = false>
 __global__ void __launch_bounds__(1024) radix_scatter_lds16_kernel(
     const int32_t* __restrict__ keys, const int32_t* __restrict__ vals, int64_t n, int shift,
     int items, int64_t nblocks, const uint32_t* __restrict__ offs,
     const uint32_t* __restrict__ hist, int32_t* __restrict__ keys_out,
     int32_t* __restrict__ vals_out, const int32_t* __restrict__ vals2 = nullptr,
-    int32_t* __restrict__ vals2_out = nullptr) {
+    int32_t* __restrict__ vals2_out = nullptr, const uint32_t* __restrict__ dtot = nullptr) {
   constexpr int BITS = 8, R = 256, NW = 16, NT = 1024;
   __shared__ uint32_t gbase[R];
   __shared__ uint32_t lstart[R];
@@ -452,18 +454,26 @@ __global__ void __launch_bounds__(1024) radix_scatter_lds16_kernel(
   __shared__ int32_t tk[kMaxSortItems * 256];
   __shared__ int32_t tv[kMaxSortItems * 256];
   __shared__ int32_t tv2[V2 ? kMaxSortItems * 256 : 1];
-  __shared__ uint32_t wsum[4];
+  __shared__ uint32_t wsum[4], tsum[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  uint32_t c = 0, x = 0;
+  uint32_t c = 0, x = 0, dt = 0, xt = 0;
   if (tid < R) {   // this block's digit counts -> exclusive prefix over the digits
     c = hist[(int64_t)tid * nblocks + blockIdx.x];
     gbase[tid] = offs[(int64_t)tid * nblocks + blockIdx.x];
     x = c;
+    if (DS) xt = dt = dtot[tid];
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t y = __shfl_up(x, o);
       if (lane >= o) x += y;
+      if (DS) {
+        const uint32_t yt = __shfl_up(xt, o);
+        if (lane >= o) xt += yt;
+      }
     }
-    if (lane == 63) wsum[wave] = x;
+    if (lane == 63) {
+      wsum[wave] = x;
+      if (DS) tsum[wave] = xt;
+    }
   }
   for (int i = tid; i < NW * R; i += NT) (&cnt[0][0])[i] = 0;
   __syncthreads();
@@ -472,6 +482,11 @@ __global__ void __launch_bounds__(1024) radix_scatter_lds16_kernel(
     for (int w = 0; w < wave; ++w) run += wsum[w];
     lstart[tid] = run;
     lrun[tid] = run;
+    if (DS) {   // digit base = exclusive scan of the digit totals
+      uint32_t base = xt - dt;
+      for (int w = 0; w < wave; ++w) base += tsum[w];
+      gbase[tid] += base;
+    }
   }
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const int64_t tile = (int64_t)blockIdx.x * 256 * items;
@@ -518,6 +533,46 @@ __global__ void __launch_bounds__(1024) radix_scatter_lds16_kernel(
     vals_out[gpos] = tv[j];
     if (V2) vals2_out[gpos] = tv2[j];
   }
+}
+
+// Per-digit scan of the block counts (block d = digit d): P[d][b] = sum_{b' < b} hist[d][b'],
+// T[d] = the digit's total; radix_scatter_lds16_kernel<DS> adds the scan of T itself. One
+// launch instead of rocPRIM's two (lookback-state init + scan) over all 256 * nb counts; for
+// nb <= 4096 (each thread sums at most 16 consecutive counts, all loads issued first).
+__global__ void __launch_bounds__(256) radix_digit_scan_kernel(const uint32_t* __restrict__ hist,
+                                                               int64_t nb,
+                                                               uint32_t* __restrict__ P,
+                                                               uint32_t* __restrict__ T) {
+  __shared__ uint32_t wsum[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int k = (int)((nb + 255) / 256);   // <= 16
+  const uint32_t* h = hist + (int64_t)blockIdx.x * nb;
+  uint32_t v[16];
+  uint32_t sum = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int64_t b = (int64_t)tid * k + i;
+    v[i] = (i < k && b < nb) ? h[b] : 0u;
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) sum += v[i];
+  uint32_t x = sum;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wave] = x;
+  __syncthreads();
+  uint32_t run = x - sum;
+  for (int w = 0; w < wave; ++w) run += wsum[w];
+  uint32_t* p = P + (int64_t)blockIdx.x * nb;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int64_t b = (int64_t)tid * k + i;
+    if (i < k && b < nb) p[b] = run;
+    run += v[i];
+  }
+  if (tid == 255) T[blockIdx.x] = run;
 }
 
 // radix_hist_kernel<8> for 1024-thread blocks (the tiles of radix_scatter_lds16_kernel).
@@ -577,7 +632,7 @@ inline int64_t hist_entries(int64_t n, unsigned bits) {
 
 size_t sort_bytes(int64_t n, unsigned bits, bool v2 = false) {  // keys in [0, 2^bits)
   const int64_t m = hist_entries(n, bits);
-  return 2 * align256(sizeof(uint32_t) * m) + (v2 ? 3 : 2) * align256(sizeof(int32_t) * (n > 0 ? n : 1)) +
+  return 2 * align256(sizeof(uint32_t) * (m + kRadix)) + (v2 ? 3 : 2) * align256(sizeof(int32_t) * (n > 0 ? n : 1)) +
          align256(radix_scan_bytes(m)) + 256;
 }
 
@@ -585,8 +640,8 @@ SortWs carve_sort(void* ws, int64_t n, unsigned bits, bool v2 = false) {
   const int64_t m = hist_entries(n, bits);
   char* p = (char*)ws;
   SortWs w;
-  w.hist = (uint32_t*)p; p += align256(sizeof(uint32_t) * m);
-  w.offs = (uint32_t*)p; p += align256(sizeof(uint32_t) * m);
+  w.hist = (uint32_t*)p; p += align256(sizeof(uint32_t) * (m + kRadix));
+  w.offs = (uint32_t*)p; p += align256(sizeof(uint32_t) * (m + kRadix));   // + digit totals
   w.tk = (int32_t*)p; p += align256(sizeof(int32_t) * (n > 0 ? n : 1));
   w.tv = (int32_t*)p; p += align256(sizeof(int32_t) * (n > 0 ? n : 1));
   w.tv2 = nullptr;
@@ -631,17 +686,34 @@ int sort_pairs(const int32_t* keys_in, const int32_t* vals_in, int32_t* keys_out
     else if (big) radix_hist16_kernel<<<(unsigned)nb, 1024, 0, stream>>>(ck, n, shift, items, nb, w.hist);
     else radix_hist_kernel<kRadixBits><<<(unsigned)nb, 256, 0, stream>>>(ck, n, shift, items, nb, w.hist);
     GATX_LAUNCH_CHECK("radix_hist");
-    // (a single-workgroup LDS scan measured 35 us on PPI's 80 K counts: rocPRIM's lookback
-    // scan over the whole chip stays)
-    size_t b = w.scan_bytes;
-    hipError_t r = rocprim::exclusive_scan(w.scan_tmp, b, w.hist, w.offs, 0u, (size_t)m,
-                                           rocprim::plus<uint32_t>(), stream);
-    if (r != hipSuccess) { set_error("radix scan: %s", hipGetErrorString(r)); return (int)r; }
     static const bool lds_tiles = [] {   // A/B: GATX_RADIX_LDS=0 keeps the direct scatter
       const char* e = getenv("GATX_RADIX_LDS");
       return !(e && strcmp(e, "0") == 0);
     }();
-    if (big && lds_tiles) {
+    static const bool dscan_on = [] {   // A/B: GATX_RADIX_DSCAN=0 keeps rocPRIM's scan
+      const char* e = getenv("GATX_RADIX_DSCAN");
+      return !(e && strcmp(e, "0") == 0);
+    }();
+    const bool dscan = big && lds_tiles && dscan_on && nb <= 4096;
+    if (dscan) {
+      radix_digit_scan_kernel<<<kRadix, 256, 0, stream>>>(w.hist, nb, w.offs, w.offs + m);
+      GATX_LAUNCH_CHECK("radix_digit_scan");
+    } else {
+      // (a single-workgroup LDS scan over all 256 * nb counts measured 35 us on PPI's 80 K
+      // counts; rocPRIM's lookback scan over the whole chip for the general case)
+      size_t b = w.scan_bytes;
+      hipError_t r = rocprim::exclusive_scan(w.scan_tmp, b, w.hist, w.offs, 0u, (size_t)m,
+                                             rocprim::plus<uint32_t>(), stream);
+      if (r != hipSuccess) { set_error("radix scan: %s", hipGetErrorString(r)); return (int)r; }
+    }
+    if (dscan) {
+      if (v2)
+        radix_scatter_lds16_kernel<true, true><<<(unsigned)nb, 1024, 0, stream>>>(
+            ck, cv, n, shift, items, nb, w.offs, w.hist, ok, ov, cv2, ov2, w.offs + m);
+      else
+        radix_scatter_lds16_kernel<false, true><<<(unsigned)nb, 1024, 0, stream>>>(
+            ck, cv, n, shift, items, nb, w.offs, w.hist, ok, ov, nullptr, nullptr, w.offs + m);
+    } else if (big && lds_tiles) {
       if (v2)
         radix_scatter_lds16_kernel<true><<<(unsigned)nb, 1024, 0, stream>>>(
             ck, cv, n, shift, items, nb, w.offs, w.hist, ok, ov, cv2, ov2);
