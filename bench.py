@@ -58,17 +58,27 @@ MALL_BYTES = 256 << 20       # Infinity Cache (MALL) capacity: the last on-chip 
 FP32_MFMA_PEAK_TFS = 157.3   # v_mfma_f32_32x32x2_f32 dense peak (same table)
 BF16_MFMA_PEAK_TFS = 2500.0  # dense bf16 MFMA peak (same table; no sparsity)
 X3_PRODUCTS = 6              # bf16 MFMA products per fp32 multiply-add in the x3 split GEMM
+F16X3_PRODUCTS = 3           # fp16 MFMA products per fp32 multiply-add in the f16x3 split GEMM
 
 
 def gemm_roof():
     """Peak and kernel name of the projection GEMM in the library's active arithmetic mode.
 
-    "f32": v_mfma_f32_32x32x2_f32, priced at the fp32 MFMA peak. "x3" (default): each fp32
-    operand is split into three bf16 planes and every fp32 multiply-add costs six bf16 MFMA
-    products (csrc/gemm_x3.hip), so the ceiling for fp32 flops is the dense bf16 peak / 6.
+    "f32": v_mfma_f32_32x32x2_f32, priced at the fp32 MFMA peak. "x3": each fp32 operand is
+    split into three bf16 planes and every fp32 multiply-add costs six bf16 MFMA products
+    (csrc/gemm_x3.hip), so the ceiling for fp32 flops is the dense bf16 peak / 6. "f16x3"
+    (default): two fp16 planes per operand, three fp16 MFMA products per fp32 multiply-add
+    (same kernel family, in-kernel x3 fallback for out-of-range tiles): dense fp16 peak (= bf16,
+    2500 TF) / 3. Every mode's flops are fp32 GEMM flops of the same product.
     """
     from gatx import _lib
-    if _lib.lib.gatx_get_gemm_mode() == 1:
+    mode = _lib.lib.gatx_get_gemm_mode()
+    if mode == 2:
+        return dict(mode="f16x3", peak=BF16_MFMA_PEAK_TFS / F16X3_PRODUCTS,
+                    prefix="gemm_x3_kernel<true, true, true, 0,",
+                    kernel="gemm_x3_kernel, f16x3 arithmetic (fp32 as 2 fp16 planes x 3 MFMA "
+                           "products; peak = dense fp16 2500 TF / 3)")
+    if mode == 1:
         return dict(mode="x3", peak=BF16_MFMA_PEAK_TFS / X3_PRODUCTS, prefix="gemm_x3_kernel<true, true, true, 0,",
                     kernel="gemm_x3_kernel (fp32 as 3 bf16 planes x 6 MFMA products; peak = "
                            "dense bf16 2500 TF / 6)")
@@ -334,6 +344,9 @@ def roofline_objects(summ, edge_bytes, pm, n_instr, pm_path=""):
         roofs["gemm"] = {"bound": "mfma", "kernel": gr["kernel"] + ", projection x.W_aug^T",
                          "achieved": round(tfs, 2), "peak": round(gr["peak"], 1),
                          "unit": "TFLOP/s", "frac": round(tfs / gr["peak"], 4), "traffic": None,
+                         # the same fp32 flops against the native fp32 MFMA peak (context only:
+                         # the split arithmetics run on the fp16 / bf16 matrix cores)
+                         "frac_of_fp32_mfma_peak": round(tfs / FP32_MFMA_PEAK_TFS, 4),
                          "gemm_mode": gr["mode"], "flops_per_launch": fl / len(gem),
                          "avg_launch_ms": ms_ / len(gem), "_prefix": gr["prefix"], "_ms": ms_,
                          "_per_step": len(gem) / n_instr}

@@ -280,13 +280,15 @@ __global__ void __launch_bounds__(64 * WGM * WGN, MINB) gemm_f32_kernel(GemmArgs
   write_tile<MB, NB, BM, BN, false>(g, acc, tail_z, tail_ti, m0, n0, wm, wn, lane);
 }
 
-// GEMM arithmetic, env GATX_GEMM (or gatx_set_gemm_mode): "x3" (default) = the split-bf16
-// kernel of gemm_x3.hip, "f32" = v_mfma_f32_32x32x2_f32.
-int g_gemm_mode = -1;   // -1: read the environment on first use; 0: f32; 1: x3
+// GEMM arithmetic, env GATX_GEMM (or gatx_set_gemm_mode): "f16x3" (default) = the split-fp16
+// kernel of gemm_x3.hip (3 fp16 MFMA products; tiles outside its operand range fall back to the
+// bf16 split in-kernel), "x3" = the split-bf16 kernel (6 bf16 products), "f32" =
+// v_mfma_f32_32x32x2_f32.
+int g_gemm_mode = -1;   // -1: read the environment on first use; 0: f32; 1: x3; 2: f16x3
 int gemm_mode() {
   if (g_gemm_mode < 0) {
     const char* e = getenv("GATX_GEMM");
-    g_gemm_mode = (e && strcmp(e, "f32") == 0) ? 0 : 1;
+    g_gemm_mode = !e ? 2 : strcmp(e, "f32") == 0 ? 0 : strcmp(e, "x3") == 0 ? 1 : 2;
   }
   return g_gemm_mode;
 }
@@ -313,7 +315,7 @@ int launch_gemm(const GemmArgs& g0, bool a_kc, bool b_kc, int batch, hipStream_t
   const int64_t gx = g.tail_s > 1 ? g.dp_blocks + g.tail_rem * g.tail_s : tiles;
   dim3 grid((unsigned)gx, (unsigned)batch, (unsigned)g.splits);
   const int var = gemm_variant();
-  if (gemm_mode() == 1) {
+  if (gemm_mode() >= 1) {
     GATX_CALL(launch_gemm_x3(g, a_kc, b_kc, batch, TAG, stream));
   } else {
 #define GATX_GEMM_V(AK, BKC, V)                                                                 \
@@ -546,7 +548,7 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
     const char* e = getenv("GATX_SMALLK");
     return !(e && strcmp(e, "0") == 0);
   }();
-  if (smallk_on && gemm_mode() == 1 && n_split >= N &&
+  if (smallk_on && gemm_mode() >= 1 && n_split >= N &&
       gemm_smallk_fits(M, N, K, a_kc, b_kc, accumulate, resid != nullptr)) {
     g.splits = 1; g.tail_s = 1; g.tiles_m = g.tiles_n = 1; g.dp_blocks = g.tail_rem = 0;
     g.bm = g.bn = 32; g.tail_partial = nullptr;
@@ -615,7 +617,7 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
   return 0;
 }
 
-extern "C" void gatx_set_gemm_mode(int mode) { g_gemm_mode = mode ? 1 : 0; }
+extern "C" void gatx_set_gemm_mode(int mode) { g_gemm_mode = mode <= 0 ? 0 : mode == 1 ? 1 : 2; }
 
 extern "C" int gatx_get_gemm_mode(void) { return gemm_mode(); }
 

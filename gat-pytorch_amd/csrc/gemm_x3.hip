@@ -31,6 +31,24 @@ using namespace gk;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+// Two floats -> packed fp16 pair, round to nearest even (v_cvt_pk_f16_f32).
+__device__ inline uint32_t cvt_pk_f16(float a, float b) {
+  f16x2 v = {(_Float16)a, (_Float16)b};
+  uint32_t u = __builtin_bit_cast(uint32_t, v);
+  asm("" : "+v"(u));
+  return u;
+}
+
+// (x, y) -> h = fp16_rn pair and l = fp16_rn(2^11 (x - h)) pair (x in the low halves). x - h is
+// exact (Sterbenz), the scaling by 2^11 keeps l a normal fp16 down to |x - h| = 2^-25.
+__device__ inline void split_pair_f16(float x, float y, uint32_t& h, uint32_t& l) {
+  h = cvt_pk_f16(x, y);
+  const f16x2 hv = __builtin_bit_cast(f16x2, h);
+  l = cvt_pk_f16((x - (float)hv[0]) * 2048.f, (y - (float)hv[1]) * 2048.f);
+}
 
 // One bf16 plane image of a ROWS-row x BK-k operand tile (byte offsets).
 template <bool KC, int ROWS, int BK>
@@ -77,21 +95,48 @@ struct X3Tile {
   // Split the staged float4s into the three planes at img. KTAIL: zero k >= kmax (the last,
   // partial K-tile); MASK: also rows >= rmax (generic path, Tile::load's clamped addresses).
   template <bool MASK, bool KTAIL>
+  static __device__ inline void mask(float4 (&v)[NV], int64_t r0, int64_t rmax, int64_t k0,
+                                     int64_t kmax) {
+    if (!(MASK || KTAIL)) return;
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      const int idx = threadIdx.x + NT * c;
+      const int64_t r = r0 + row_of(idx), k = k0 + k_of(idx);
+      const bool ok = (!MASK || r < rmax) && k < kmax;
+      const int64_t lim = (KC || !MASK) ? (KC ? kmax - k : 4) : rmax - r;
+      v[c].x = ok ? v[c].x : 0.f;
+      v[c].y = ok && lim > 1 ? v[c].y : 0.f;
+      v[c].z = ok && lim > 2 ? v[c].z : 0.f;
+      v[c].w = ok && lim > 3 ? v[c].w : 0.f;
+    }
+  }
+  // f16x3 staging (see f16_mainloop): plane 0 = h = fp16_rn(x), plane 1 = fp16_rn(2^11 (x - h));
+  // amax tracks max |x| over the staged elements for the caller's range check.
+  template <bool MASK, bool KTAIL>
+  static __device__ inline void store_f16(char* img, float4 (&v)[NV], int64_t r0, int64_t rmax,
+                                          int64_t k0, int64_t kmax, float (&amax)[NV]) {
+    mask<MASK, KTAIL>(v, r0, rmax, k0, kmax);
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      const int idx = threadIdx.x + NT * c;
+      amax[c] = fmaxf(amax[c], fmaxf(fmaxf(fabsf(v[c].x), fabsf(v[c].y)),
+                                     fmaxf(fabsf(v[c].z), fabsf(v[c].w))));
+      uint32_t h0, l0, h1, l1;
+      split_pair_f16(v[c].x, v[c].y, h0, l0);
+      split_pair_f16(v[c].z, v[c].w, h1, l1);
+      const int o = Img::off(row_of(idx), k_of(idx));
+      *(uint2*)(img + o) = make_uint2(h0, h1);
+      *(uint2*)(img + Img::BYTES + o) = make_uint2(l0, l1);
+    }
+  }
+  template <bool MASK, bool KTAIL>
   static __device__ inline void store(char* img, float4 (&v)[NV], int64_t r0, int64_t rmax,
                                       int64_t k0, int64_t kmax) {
+    mask<MASK, KTAIL>(v, r0, rmax, k0, kmax);
 #pragma unroll
     for (int c = 0; c < NV; ++c) {
       const int idx = threadIdx.x + NT * c;
       const int row = row_of(idx), kk = k_of(idx);
-      if (MASK || KTAIL) {
-        const int64_t r = r0 + row, k = k0 + kk;
-        const bool ok = (!MASK || r < rmax) && k < kmax;
-        const int64_t lim = (KC || !MASK) ? (KC ? kmax - k : 4) : rmax - r;
-        v[c].x = ok ? v[c].x : 0.f;
-        v[c].y = ok && lim > 1 ? v[c].y : 0.f;
-        v[c].z = ok && lim > 2 ? v[c].z : 0.f;
-        v[c].w = ok && lim > 3 ? v[c].w : 0.f;
-      }
       uint32_t h0, m0, l0, h1, m1, l1;
       if (DBG == 1) {   // tuning probe: conversion only (wrong values), measures the split's cost
         h0 = m0 = l0 = cvt_pk_bf16(v[c].x, v[c].y);
@@ -279,6 +324,181 @@ __device__ inline void x3_mainloop(const GemmArgs& g, const float* __restrict__ 
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// fp32 GEMM as a two-way fp16 split ("f16x3"): x = h + l 2^-11 with h = fp16_rn(x) and
+// l = fp16_rn(2^11 (x - h)) (11 + 11 significand bits; |x - h - l 2^-11| <= 2^-23 |x|, and the
+// 2^11 keeps l a normal fp16 wherever x is), and the product as three fp16 MFMA products, all
+// carrying the same factor 2^11:
+//     2^11 a b ~= (64 a_h)(32 b_h) + a_h b_l + a_l b_h        (dropped: a_l b_l 2^-22 <= 2^-24 |ab|)
+// The 64 / 32 factors of the first product are applied to the hi fragments in registers
+// (v_pk_mul_f16, exact); fp16 products are exact in the f32 accumulator, which is scaled by 2^-11
+// (exact) at the end: fp32-GEMM accuracy (tests/test_gpu_layer.py against fp64) at 3 MFMA
+// products per step instead of the bf16 split's 6, and two LDS planes per operand instead of 3.
+// Range: 64 a_h and 32 b_h must be finite fp16, i.e. |a| <= 1023 and |b| <= 2047; and below
+// 2^-13 an element's pieces reach fp16 subnormals (absolute error up to 2^-36), harmless next to
+// the row's larger elements but not for a row that is tiny throughout. Every thread tracks
+// max |x| of its staged row slices; per operand row (an A row = an output row, a B row = an
+// output column; k-contiguous operands: the row's 4 staging lanes are adjacent) the amax must
+// be 0 or within [2^-13, limit]. A workgroup with any row outside (or holding inf) discards its
+// accumulators and recomputes its tile with the bf16 split (x3_mainloop, fp32 exponent range),
+// so accuracy never depends on the operands' magnitudes. Used for k-contiguous A and B (the
+// forward projection's layout); the other layouts run x3.
+constexpr float kF16LimA = 1023.f, kF16LimB = 2047.f, kF16Tiny = 0x1p-13f;
+
+__device__ inline bool f16_row_bad(float m, float lim) {
+  m = fmaxf(m, __shfl_xor(m, 1));
+  m = fmaxf(m, __shfl_xor(m, 2));
+  return !(m <= lim) || (m > 0.f && m < kF16Tiny);
+}
+
+template <bool A_KC, bool B_KC, bool MASK, int CFG>
+__device__ inline bool f16_mainloop(const GemmArgs& g, const float* __restrict__ A,
+                                    const float* __restrict__ B, int64_t m0, int64_t n0,
+                                    int64_t kb, int64_t K, int64_t nk, char* smem, int wm, int wn,
+                                    int lane, floatx16 (&acc)[X3Cfg<CFG>::MB][X3Cfg<CFG>::NB]) {
+  using C = X3Cfg<CFG>;
+  constexpr int NT = C::NT, BK = C::BK, MB = C::MB, NB = C::NB;
+  using TA = X3Tile<A_KC, C::TBM, BK, NT>;
+  using TB = X3Tile<B_KC, C::TBN, BK, NT>;
+  constexpr int PA = TA::Img::BYTES, PBy = TB::Img::BYTES;   // bytes per plane
+  constexpr int STAGE = 2 * (PA + PBy);                      // A planes h, l then B's
+  const int64_t M = g.M, N = g.N;
+  static_assert(A_KC && B_KC, "f16x3 staging needs k-contiguous operands (row amax lanes)");
+  float amax_a[TA::NV], amax_b[TB::NV];
+#pragma unroll
+  for (int c = 0; c < TA::NV; ++c) amax_a[c] = 0.f;
+#pragma unroll
+  for (int c = 0; c < TB::NV; ++c) amax_b[c] = 0.f;
+  float4 va[TA::NV], vb[TB::NV];
+  const float* pa[TA::NV];
+  const float* pb[TB::NV];
+  int64_t sa = 0, sb = 0;
+  if (!MASK) {
+    TA::setup(A, g.lda, m0, M, kb, pa, sa);
+    TB::setup(B, g.ldb, n0, N, kb, pb, sb);
+  }
+  auto load = [&](int64_t k0) {
+    if (MASK) {
+      TA::T::template load<false>(A, g.lda, m0, M, k0, K, va);
+      TB::T::template load<false>(B, g.ldb, n0, N, k0, K, vb);
+    } else if (k0 + BK > K) {
+#pragma unroll
+      for (int c = 0; c < TA::NV; ++c) {
+        const int64_t k = k0 + TA::k_of(threadIdx.x + NT * c);
+        va[c] = *(const float4*)(k < K ? pa[c] : pa[c] - (k - kb) * (A_KC ? 1 : g.lda));
+      }
+#pragma unroll
+      for (int c = 0; c < TB::NV; ++c) {
+        const int64_t k = k0 + TB::k_of(threadIdx.x + NT * c);
+        vb[c] = *(const float4*)(k < K ? pb[c] : pb[c] - (k - kb) * (B_KC ? 1 : g.ldb));
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < TA::NV; ++c) { va[c] = *(const float4*)pa[c]; pa[c] += sa; }
+#pragma unroll
+      for (int c = 0; c < TB::NV; ++c) { vb[c] = *(const float4*)pb[c]; pb[c] += sb; }
+    }
+  };
+  auto store = [&](char* st, int64_t k0) {
+    if (MASK) {
+      TA::template store_f16<true, true>(st, va, m0, M, k0, K, amax_a);
+      TB::template store_f16<true, true>(st + 2 * PA, vb, n0, N, k0, K, amax_b);
+    } else if (k0 + BK > K) {
+      TA::template store_f16<false, true>(st, va, m0, M, k0, K, amax_a);
+      TB::template store_f16<false, true>(st + 2 * PA, vb, n0, N, k0, K, amax_b);
+    } else {
+      TA::template store_f16<false, false>(st, va, m0, M, k0, K, amax_a);
+      TB::template store_f16<false, false>(st + 2 * PA, vb, n0, N, k0, K, amax_b);
+    }
+  };
+  f16x8 fa[MB][2], fb[NB][2];
+  auto frags = [&](const char* cur) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+#pragma unroll
+      for (int x = 0; x < MB; ++x)
+        fa[x][p] = __builtin_bit_cast(f16x8, TA::frag(cur + p * PA, wm * (MB * 32) + x * 32, 0, lane));
+#pragma unroll
+      for (int x = 0; x < NB; ++x)
+        fb[x][p] = __builtin_bit_cast(f16x8, TB::frag(cur + 2 * PA + p * PBy, wn * (NB * 32) + x * 32, 0, lane));
+    }
+  };
+  auto mfmas = [&]() {
+    // small terms first: a_h b_l, a_l b_h, then (64 a_h)(32 b_h); C^T = B^T A^T as in x3
+#pragma unroll
+    for (int mi = 0; mi < MB; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NB; ++ni)
+        acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][1], fa[mi][0], acc[mi][ni], 0, 0, 0);
+#pragma unroll
+    for (int mi = 0; mi < MB; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NB; ++ni)
+        acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][0], fa[mi][1], acc[mi][ni], 0, 0, 0);
+    f16x8 sa8[MB], sb8[NB];
+#pragma unroll
+    for (int mi = 0; mi < MB; ++mi) sa8[mi] = fa[mi][0] * (_Float16)64.0f;
+#pragma unroll
+    for (int ni = 0; ni < NB; ++ni) sb8[ni] = fb[ni][0] * (_Float16)32.0f;
+#pragma unroll
+    for (int mi = 0; mi < MB; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NB; ++ni)
+        acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(sb8[ni], sa8[mi], acc[mi][ni], 0, 0, 0);
+  };
+  int64_t kt = 0;
+  load(kb);
+  store(smem, kb);
+  __syncthreads();
+  if constexpr (!MASK && CFG == 1) {
+    // steady state as in x3_mainloop: tile kt + 1 staged into the other buffer right after this
+    // tile's fragment reads, tile kt + 2's loads issued before the MFMAs
+    const int64_t nfull = (K - kb) / BK;
+    if (nfull >= 2) {
+      load(kb + BK);
+      for (; kt + 2 < nfull; ++kt) {
+        char* cur = smem + (kt & 1) * STAGE;
+        char* nxt = smem + ((kt & 1) ^ 1) * STAGE;
+        frags(cur);
+        TA::template store_f16<false, false>(nxt, va, m0, M, 0, K, amax_a);
+        TB::template store_f16<false, false>(nxt + 2 * PA, vb, n0, N, 0, K, amax_b);
+#pragma unroll
+        for (int c = 0; c < TA::NV; ++c) { va[c] = *(const float4*)pa[c]; pa[c] += sa; }
+#pragma unroll
+        for (int c = 0; c < TB::NV; ++c) { vb[c] = *(const float4*)pb[c]; pb[c] += sb; }
+        mfmas();
+        __syncthreads();
+      }
+      char* cur = smem + (kt & 1) * STAGE;
+      char* nxt = smem + ((kt & 1) ^ 1) * STAGE;
+      frags(cur);
+      TA::template store_f16<false, false>(nxt, va, m0, M, 0, K, amax_a);
+      TB::template store_f16<false, false>(nxt + 2 * PA, vb, n0, N, 0, K, amax_b);
+      mfmas();
+      __syncthreads();
+      ++kt;
+    }
+  }
+  for (; kt < nk; ++kt) {
+    char* cur = smem + (kt & 1) * STAGE;
+    char* nxt = smem + ((kt & 1) ^ 1) * STAGE;
+    const bool more = kt + 1 < nk;
+    if (more) load(kb + (kt + 1) * BK);
+    frags(cur);
+    mfmas();
+    if (more) store(nxt, kb + (kt + 1) * BK);
+    __syncthreads();
+  }
+  // true: a row of this thread's operand slices out of range (see above)
+  static_assert(BK / 4 == 4, "a k-contiguous row is staged by 4 adjacent lanes");
+  bool bad = false;
+#pragma unroll
+  for (int c = 0; c < TA::NV; ++c) bad |= f16_row_bad(amax_a[c], kF16LimA);
+#pragma unroll
+  for (int c = 0; c < TB::NV; ++c) bad |= f16_row_bad(amax_b[c], kF16LimB);
+  return bad;
+}
+
 // Epilogue of the transposed product. acc[mi][ni] is the C^T block of output rows
 // rb = wm*MB*32 + mi*32 and columns cb = wn*NB*32 + ni*32: lane l holds row rb + (l & 31),
 // registers 4j..4j+3 the four consecutive columns cb + 8j + 4(l >> 5) + 0..3. Every group of
@@ -457,7 +677,8 @@ __device__ inline void scores_tile(const GemmArgs& g, const floatx16 (&acc)[MB][
 }
 
 template <bool A_KC, bool B_KC, bool VEC, int TAG, int CFG, int DBG = 0>
-__global__ void __launch_bounds__(X3Cfg<CFG>::NT, X3Cfg<CFG>::MINB) gemm_x3_kernel(GemmArgs g) {
+__global__ void __launch_bounds__(X3Cfg<CFG>::NT, X3Cfg<CFG>::MINB) gemm_x3_kernel(GemmArgs g,
+                                                                                   int arith) {
   using C = X3Cfg<CFG>;
   constexpr int STAGE = 3 * 2 * (C::TBM + C::TBN) * C::BK;
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
@@ -499,10 +720,25 @@ __global__ void __launch_bounds__(X3Cfg<CFG>::NT, X3Cfg<CFG>::MINB) gemm_x3_kern
 
   const int64_t nk = K > kb ? ceil_div(K - kb, C::BK) : 0;
   if (nk > 0) {
-    if (VEC)
-      x3_mainloop<A_KC, B_KC, false, CFG, DBG>(g, A, B, m0, n0, kb, K, nk, smem, wm, wn, lane, acc);
-    else
-      x3_mainloop<A_KC, B_KC, true, CFG, DBG>(g, A, B, m0, n0, kb, K, nk, smem, wm, wn, lane, acc);
+    bool x3 = true;
+    if constexpr (A_KC && B_KC && DBG == 0) if (arith == 2) {
+      const bool bad =
+          VEC ? f16_mainloop<A_KC, B_KC, false, CFG>(g, A, B, m0, n0, kb, K, nk, smem, wm, wn, lane, acc)
+              : f16_mainloop<A_KC, B_KC, true, CFG>(g, A, B, m0, n0, kb, K, nk, smem, wm, wn, lane, acc);
+      x3 = __syncthreads_or(bad);   // the workgroup's tiles out of fp16 range: redo as x3
+#pragma unroll
+      for (int i = 0; i < C::MB; ++i)
+#pragma unroll
+        for (int j = 0; j < C::NB; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] = x3 ? 0.f : acc[i][j][r] * 0x1p-11f;
+    }
+    if (x3) {
+      if (VEC)
+        x3_mainloop<A_KC, B_KC, false, CFG, DBG>(g, A, B, m0, n0, kb, K, nk, smem, wm, wn, lane, acc);
+      else
+        x3_mainloop<A_KC, B_KC, true, CFG, DBG>(g, A, B, m0, n0, kb, K, nk, smem, wm, wn, lane, acc);
+    }
   }
   write_tile_t<C::MB, C::NB, C::TBM, C::TBN>(g, acc, tail_z, tail_ti, m0, n0, wm, wn, lane);
   // (tail slices are scored by tail_fixup_scores_kernel once summed)
@@ -519,6 +755,7 @@ int launch_gemm_x3(const gk::GemmArgs& g, bool a_kc, bool b_kc, int batch, int t
   const int64_t gx = g.tail_s > 1 ? g.dp_blocks + g.tail_rem * g.tail_s : tiles;
   dim3 grid((unsigned)gx, (unsigned)batch, (unsigned)g.splits);
   const int cfg = g.bm == 256 ? 1 : 0;
+  const int arith = gatx_get_gemm_mode();   // 1: bf16 split (x3), 2: fp16 split (f16x3)
   // tuning probes only (wrong results): GATX_X3_DBG=1 conversion without the split arithmetic,
   // 2 no next-tile LDS stores, 3 no operand loads or stores, 4 MFMAs only (no LDS reads after the
   // first K-tile, no barriers)
@@ -528,21 +765,21 @@ int launch_gemm_x3(const gk::GemmArgs& g, bool a_kc, bool b_kc, int batch, int t
   }();
   if (dbg && a_kc && b_kc && g.a_vec && g.b_vec) {
     if (cfg == 1) {
-      if (dbg == 1) gemm_x3_kernel<true, true, true, 0, 1, 1><<<grid, 512, 0, stream>>>(g);
-      else if (dbg == 2) gemm_x3_kernel<true, true, true, 0, 1, 2><<<grid, 512, 0, stream>>>(g);
-      else if (dbg == 3) gemm_x3_kernel<true, true, true, 0, 1, 3><<<grid, 512, 0, stream>>>(g);
-      else gemm_x3_kernel<true, true, true, 0, 1, 4><<<grid, 512, 0, stream>>>(g);
+      if (dbg == 1) gemm_x3_kernel<true, true, true, 0, 1, 1><<<grid, 512, 0, stream>>>(g, 1);
+      else if (dbg == 2) gemm_x3_kernel<true, true, true, 0, 1, 2><<<grid, 512, 0, stream>>>(g, 1);
+      else if (dbg == 3) gemm_x3_kernel<true, true, true, 0, 1, 3><<<grid, 512, 0, stream>>>(g, 1);
+      else gemm_x3_kernel<true, true, true, 0, 1, 4><<<grid, 512, 0, stream>>>(g, 1);
     } else {
-      if (dbg == 1) gemm_x3_kernel<true, true, true, 0, 0, 1><<<grid, 256, 0, stream>>>(g);
-      else gemm_x3_kernel<true, true, true, 0, 0, 2><<<grid, 256, 0, stream>>>(g);
+      if (dbg == 1) gemm_x3_kernel<true, true, true, 0, 0, 1><<<grid, 256, 0, stream>>>(g, 1);
+      else gemm_x3_kernel<true, true, true, 0, 0, 2><<<grid, 256, 0, stream>>>(g, 1);
     }
     GATX_LAUNCH_CHECK("gemm_x3 (probe)");
     return 0;
   }
 #define GATX_X3_V(AK, BKC, V, TG)                                                             \
   do {                                                                                        \
-    if (cfg == 1) gemm_x3_kernel<AK, BKC, V, TG, 1><<<grid, 512, 0, stream>>>(g);             \
-    else gemm_x3_kernel<AK, BKC, V, TG, 0><<<grid, 256, 0, stream>>>(g);                      \
+    if (cfg == 1) gemm_x3_kernel<AK, BKC, V, TG, 1><<<grid, 512, 0, stream>>>(g, arith);         \
+    else gemm_x3_kernel<AK, BKC, V, TG, 0><<<grid, 256, 0, stream>>>(g, arith);                  \
   } while (0)
 #define GATX_X3_T(AK, BKC, V)                                                                 \
   do {                                                                                        \

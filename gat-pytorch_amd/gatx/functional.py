@@ -317,10 +317,35 @@ def fuses_output_dropout(num_heads, out_features, in_features, concat, const_att
                                             const_attention))
 
 
+class LazyAlpha:
+    """alpha of a forward that nothing has asked for yet (an inference forward without
+    return_attention_weights): the reference computes and stores it in every forward
+    (`models/gat_layer.py:106-110`); here the pass that writes it (gatx_attention_alpha_ei) runs
+    when `normalised_attention_coeffs` is first read, from the softmax state the forward left (the
+    node scores S, the global max and the denominators, all kept alive by this object) — the
+    same kernel on the same inputs, so the same values as an eager forward. Training forwards
+    stay eager: the backward's max() gradient needs the argmax entries that pass records."""
+
+    __slots__ = ("graph", "S", "M_ord", "den", "sh", "argmax")
+
+    def __init__(self, graph, S, M_ord, den, sh, argmax):
+        self.graph, self.S, self.M_ord, self.den, self.sh, self.argmax = \
+            graph, S, M_ord, den, sh, argmax
+
+    def materialize(self) -> torch.Tensor:
+        alpha = torch.empty((max(self.graph.edge_bound, 1), self.sh.NH), dtype=torch.float32,
+                            device=self.S.device)
+        with _span("attention_alpha", (self.graph.edge_bound, self.sh.NH)):
+            _attention_alpha(self.graph, self.S, self.M_ord, self.den, self.sh, alpha,
+                             self.argmax, stream())
+        return alpha
+
+
 def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: int,
-                  resid=None, elu=False, skip_W=None, out_p=0.0, out_seed=None):
-    """Returns out (= elu?(layer(x) + resid) when fused), alpha (edge_index' order) and the saved
-    state for the backward. skip_W: GATModel's Linear skip folded into the projection GEMM (its
+                  resid=None, elu=False, skip_W=None, out_p=0.0, out_seed=None,
+                  want_alpha=True):
+    """Returns out (= elu?(layer(x) + resid) when fused), alpha (edge_index' order; a LazyAlpha
+    when want_alpha is False) and the saved state for the backward. skip_W: GATModel's Linear skip folded into the projection GEMM (its
     rows appended to W_aug; the GEMM writes the skip output R as a third output range and the
     edge pass / output projection epilogue adds it): resid = x W_skip_eff^T without a launch.
     out_p / out_seed: the next layer's input dropout applied by this layer's edge-pass epilogue
@@ -332,7 +357,7 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
     f32 = dict(dtype=torch.float32, device=dev)
     chunk = _env_int("GATX_EDGE_CHUNK", 2048)
     out = torch.empty((N, sh.out_cols), **f32)
-    alpha = torch.empty((max(E2, 1), sh.NH), **f32)
+    alpha = torch.empty((max(E2, 1), sh.NH), **f32) if want_alpha else None
     den = torch.empty((N, sh.NH), **f32)
     # argmax[0] (tie count) is reset by gatx_attention_max; M_ord is written by it
     argmax = torch.empty(ARGMAX_CAP + 2, dtype=torch.int64, device=dev)
@@ -378,8 +403,11 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
                  0, 0, 0, 1,
                  int(sh.const), None, float(p), ptr(seed), ptr(Z), sh.NH * Fin_p, None, 0, 0,
                  ptr(den), chunk, *hub, s)
-        with _span("attention_alpha", (E2, sh.NH)):
-            _attention_alpha(graph, S, M_ord, den, sh, alpha, argmax, s)
+        if want_alpha:
+            with _span("attention_alpha", (E2, sh.NH)):
+                _attention_alpha(graph, S, M_ord, den, sh, alpha, argmax, s)
+        else:
+            alpha = LazyAlpha(graph, S, M_ord, den, sh, argmax)
         Wp = padded_weight(W, Fin_p, sh.cache_weights)   # float4-readable rows
         saved["Wp"] = Wp   # the backward's batched GEMMs read the same padded copy
         with _span("gemm_out", (N, sh.F, sh.F_in, sh.NH)):
@@ -440,8 +468,11 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
                      ptr(seed), ptr(out), sh.out_cols, resid_p if last else None, sh.out_cols,
                      int(elu) if last else 0, ptr(den), chunk, *hub,
                      *(drop_args if last else (0.0, None)), s)
-    with _span("attention_alpha", (E2, sh.NH)):
-        _attention_alpha(graph, S, M_ord, den, sh, alpha, argmax, s)
+    if want_alpha:
+        with _span("attention_alpha", (E2, sh.NH)):
+            _attention_alpha(graph, S, M_ord, den, sh, alpha, argmax, s)
+    else:
+        alpha = LazyAlpha(graph, S, M_ord, den, sh, argmax)
     saved.update(Wh=Wh, S=S, reassoc=False)
     return out, alpha, saved
 
@@ -815,9 +846,11 @@ def prepare_layer(x, edge_index, W, a, bias, num_heads, out_features, concat, ad
 
 def gat_layer_lazy(x, edge_index, W, a, bias, num_heads, out_features, concat, add_self_loops,
                    const_attention=False, dropout_p=0.0, seed=0, graph: Graph | None = None,
-                   resid=None, elu=False, skip_weight=None, out_dropout=None):
+                   resid=None, elu=False, skip_weight=None, out_dropout=None,
+                   defer_alpha=False):
     """gat_layer without any host sync: returns (out, graph, alpha_bound) where alpha_bound is
     (graph.edge_bound, NH) and its first graph.num_edges rows are alpha in edge_index' order.
+    defer_alpha: with autograd off, alpha_bound is a LazyAlpha (its pass runs when it is read).
     resid / elu fuse GATModel's skip-add and ELU into the layer's epilogue:
     out = elu?(layer(x) + resid). skip_weight (GATModel's Linear skip, (NH*F, F_in)) folds the
     skip projection itself into the layer: resid = x W_skip^T (concat) or its head mean, computed
@@ -838,6 +871,10 @@ def gat_layer_lazy(x, edge_index, W, a, bias, num_heads, out_features, concat, a
         if not fuses_output_dropout(num_heads, out_features, x.size(1), concat, const_attention):
             raise RuntimeError("gatx: out_dropout needs a layer whose output comes from the edge "
                                "pass (fuses_output_dropout)")
+    if defer_alpha and not torch.is_grad_enabled():
+        out, alpha, _ = layer_forward(x, W, a, bias, graph, sh, p, seed_t, resid, bool(elu),
+                                      skip_weight, out_p, out_seed, want_alpha=False)
+        return out, graph, alpha
     out, alpha = GATLayerFunction.apply(x, W, a, bias, resid, skip_weight, graph, sh, p, seed_t,
                                         bool(elu), out_p, out_seed)
     return out, graph, alpha

@@ -18,7 +18,7 @@ import torch
 from torch import nn
 
 from . import ops  # noqa: F401  (registers torch.ops.gatx.*)
-from .functional import gat_layer_lazy
+from .functional import LazyAlpha, gat_layer_lazy
 
 
 class GATLayer(nn.Module):
@@ -64,11 +64,15 @@ class GATLayer(nn.Module):
     def normalised_attention_coeffs(self):
         """alpha of the last forward (`models/gat_layer.py:110`), (E', NH) in edge_index' order.
         Kept at its allocation bound until read: the exact E' lives on the device, so the slice
-        (one host read of E') happens here, not in forward."""
+        (one host read of E') happens here, not in forward. After an inference forward (autograd
+        off, no return_attention_weights) the alpha pass itself runs on this first read
+        (functional.LazyAlpha: same kernel, same inputs, same values)."""
         att = self.__dict__.get("_attention")
         if att is None or isinstance(att, torch.Tensor):
             return att
         graph, alpha = att
+        if isinstance(alpha, LazyAlpha):   # an inference forward's alpha, computed on first read
+            alpha = alpha.materialize()
         view = alpha[:graph.num_edges]
         self.__dict__["_attention"] = view
         return view
@@ -106,7 +110,8 @@ class GATLayer(nn.Module):
             x, edge_index, self.W.weight, None if self.const_attention else self.a.weight,
             self.bias_param if self.bias else None, self.num_heads, self.out_features,
             self.concat, self.add_self_loops, self.const_attention, p, seed, graph=graph,
-            resid=resid, elu=elu, skip_weight=skip_weight, out_dropout=out_dropout)
+            resid=resid, elu=elu, skip_weight=skip_weight, out_dropout=out_dropout,
+            defer_alpha=not return_attention_weights)
         self.normalised_attention_coeffs = (g, alpha)
         if return_attention_weights:
             return out, (g.edge_index, self.normalised_attention_coeffs)

@@ -75,3 +75,30 @@ def test_weight_update_through_data_is_seen(device):
         out = layer(x, ei)
     ref, _, _, _ = orc.gat_layer_forward(b.x, b.edge_index, W, -0.5 * a, NH, F, True)
     assert np.abs(out.cpu().numpy() - ref).max() <= OUT_TOL
+
+
+@pytest.mark.parametrize("shape", [(4, 8, 24, True), (4, 8, 24, False), (4, 16, 8, True)])
+def test_inference_alpha_on_read(shape, device):
+    """An inference forward without return_attention_weights defers the alpha pass until
+    `normalised_attention_coeffs` is read (`models/gat_layer.py:110` stores alpha in every
+    forward): the value read is bitwise the eager forward's alpha and matches the oracle, for
+    the plain and the reassociated (narrow input) dataflows; a later forward replaces it."""
+    NH, F, fin, concat = shape
+    b, W, a, _, _ = _small_case(seed=5, fin=fin, NH=NH, F=F)
+    layer = _layer(device, W, a, NH, F, concat).eval()
+    x = torch.from_numpy(b.x).to(device)
+    ei = torch.from_numpy(b.edge_index).to(device)
+    _, r_ei, r_alpha, _ = orc.gat_layer_forward(b.x, b.edge_index, W, a, NH, F, concat)
+    with torch.no_grad():
+        out_e, (ei2, alpha_e) = layer(x, ei, return_attention_weights=True)
+        alpha_e = alpha_e.clone()
+        out_l = layer(x, ei)
+        lazy = layer.normalised_attention_coeffs
+    assert torch.equal(out_e, out_l)
+    assert torch.equal(lazy, alpha_e)
+    assert np.array_equal(ei2.cpu().numpy(), r_ei)
+    assert np.abs(lazy.cpu().numpy() - r_alpha).max() <= OUT_TOL
+    assert layer.normalised_attention_coeffs is lazy   # materialised once
+    with torch.no_grad():
+        layer(x * 2, ei)
+    assert not torch.equal(layer.normalised_attention_coeffs, lazy)

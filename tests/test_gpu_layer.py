@@ -3,6 +3,8 @@ CPU oracle. Tolerances: outputs / alpha 1e-4 absolute (north_star); gradients
 max|d| <= 1e-4 * max(1, max|ref|) (from the reference's own fp32-vs-fp64 noise)."""
 import numpy as np
 import pytest
+
+DEFAULT_GEMM_MODE = 2   # f16x3 (csrc/gemm.hip gemm_mode)
 import torch
 
 from golden_io import LAYER_CASES, MODEL_CASES, grad_seeds, load_layer_case, load_model_case
@@ -143,19 +145,24 @@ def test_gemm_mfma_layout(device):
 
 
 @pytest.mark.gpu
-def test_gemm_x3_split_accuracy(device):
-    """The split-bf16 GEMM ("x3": 3 bf16 planes per operand, 6 MFMA products) against float64,
-    beside the f32-MFMA kernel on the same data: error relative to sum|a||b| must stay at the
-    fp32 GEMM's level (<= 1.25x f32's, and < 1e-6 absolute-relative) for every operand layout,
-    128- and 256-wide tiles (kind chosen by size), partial K-tiles, ragged edges, unaligned
-    leading dimensions and split-K; repeated launches are bitwise identical."""
+@pytest.mark.parametrize("split_mode", [1, 2])
+def test_gemm_x3_split_accuracy(split_mode, device):
+    """The split GEMMs — "x3" (mode 1: 3 bf16 planes per operand, 6 MFMA products) and "f16x3"
+    (mode 2, the default: 2 fp16 planes, 3 products, in-kernel x3 fallback for tiles outside
+    the fp16 range) — against float64, beside the f32-MFMA kernel on the same data: error
+    relative to sum|a||b| must stay at the fp32 GEMM's level (<= 1.25x f32's, and < 1e-6
+    absolute-relative) for every operand layout, 128- and 256-wide tiles (kind chosen by size),
+    partial K-tiles, ragged edges, unaligned leading dimensions and split-K; repeated launches
+    are bitwise identical. The f16x3 cases include operands far outside its range (|a| ~ 1e4:
+    those tiles take the fallback) and tiny ones (|a| ~ 1e-6: fp16 subnormal hi parts)."""
     from gatx._lib import call, lib, ptr, stream
     torch.manual_seed(11)
-    cases = [(600, 520, 1100), (300, 257, 33), (1000, 760, 70), (2000, 1024, 1100),
-             (513, 300, 4096), (129, 129, 17), (44, 1030, 70)]
+    cases = [(600, 520, 1100, 30), (300, 257, 33, 30), (1000, 760, 70, 30),
+             (2000, 1024, 1100, 30), (513, 300, 4096, 30), (129, 129, 17, 30),
+             (44, 1030, 70, 30), (700, 600, 300, 1e4), (700, 600, 300, 1e-6)]
     try:
-        for (M, N, K) in cases:
-            A = torch.randn(M, K, device=device) * torch.rand(M, 1, device=device) * 30
+        for (M, N, K, amp) in cases:
+            A = torch.randn(M, K, device=device) * torch.rand(M, 1, device=device) * amp
             B = torch.randn(K, N, device=device)
             ref = A.double() @ B.double()
             S = (A.double().abs() @ B.double().abs()).clamp_min(1e-30)
@@ -166,7 +173,7 @@ def test_gemm_x3_split_accuracy(device):
                     sam, sak = (1, M) if a_t else (K, 1)
                     sbk, sbn = (1, K) if b_t else (N, 1)
                     rel = {}
-                    for mode in (0, 1):
+                    for mode in (0, split_mode):
                         lib.gatx_set_gemm_mode(mode)
                         outs = []
                         for _ in range(2):
@@ -177,10 +184,10 @@ def test_gemm_x3_split_accuracy(device):
                         torch.cuda.synchronize()
                         assert torch.equal(outs[0], outs[1]), (M, N, K, a_t, b_t, mode)
                         rel[mode] = ((outs[0].double() - ref).abs() / S).max().item()
-                    assert rel[1] <= max(1.25 * rel[0], 2e-7) and rel[1] < 1e-6, \
-                        (M, N, K, a_t, b_t, rel)
-        # unaligned leading dimensions (scalar staging path) and split-K through x3
-        lib.gatx_set_gemm_mode(1)
+                    r = rel[split_mode]
+                    assert r <= max(1.25 * rel[0], 2e-7) and r < 1e-6, (M, N, K, a_t, b_t, rel)
+        # unaligned leading dimensions (scalar staging path) and split-K through the split kernel
+        lib.gatx_set_gemm_mode(split_mode)
         M, N, K = 301, 263, 1433
         A = torch.randn(M, K, device=device)
         B = torch.randn(N, K, device=device)
@@ -204,7 +211,7 @@ def test_gemm_x3_split_accuracy(device):
         torch.cuda.synchronize()
         assert ((C.double() - ref).abs() / S).max().item() < 1e-6
     finally:
-        lib.gatx_set_gemm_mode(1)
+        lib.gatx_set_gemm_mode(DEFAULT_GEMM_MODE)
 
 
 @pytest.mark.gpu
@@ -216,7 +223,7 @@ def test_layer_goldens_f32_gemm(name, device):
     try:
         test_layer_matches_reference_goldens(name, device)
     finally:
-        lib.gatx_set_gemm_mode(1)
+        lib.gatx_set_gemm_mode(DEFAULT_GEMM_MODE)
 
 
 @pytest.mark.gpu
@@ -259,7 +266,7 @@ def test_gemm_smallk(device):
                     assert rel <= max(1.5 * rel_f32, 3e-7) and rel < 1e-6, (M, NB, N, K, elu, rel,
                                                                            rel_f32)
     finally:
-        lib.gatx_set_gemm_mode(1)
+        lib.gatx_set_gemm_mode(DEFAULT_GEMM_MODE)
 
 
 @pytest.mark.gpu

@@ -8,6 +8,8 @@ Model level: a PATTERN-shaped GATModel (every layer a Linear skip) with the fold
 oracle's model forward/backward and the unfolded path (GATX_SKIP_FOLD=0)."""
 import numpy as np
 import pytest
+
+DEFAULT_GEMM_MODE = 2   # f16x3 (csrc/gemm.hip gemm_mode)
 import torch
 
 from oracle import gat_oracle as orc
@@ -175,7 +177,7 @@ def test_model_accepts_reference_data_object(device):
     assert len(atts) == data_config["PATTERN"]["num_layers"] and ei2.shape[0] == 2
 
 
-@pytest.mark.parametrize("mode", [1, 0])   # x3 (default) and f32-MFMA arithmetic
+@pytest.mark.parametrize("mode", [2, 1, 0])   # f16x3 (default), x3 and f32-MFMA arithmetic
 @pytest.mark.parametrize("M,N,K,s1,s2", [(96, 300, 64, 128, 200), (44900, 1036 + 48, 256, 1024, 1036),
                                           (3001, 450, 96, 48, 56)])
 def test_projection_gemm3_three_outputs(mode, M, N, K, s1, s2, device):
@@ -196,7 +198,7 @@ def test_projection_gemm3_three_outputs(mode, M, N, K, s1, s2, device):
              ptr(C1), s2 - s1, s2, ptr(C2), N - s2, *ws, stream())
         torch.cuda.synchronize()
     finally:
-        lib.gatx_set_gemm_mode(1)
+        lib.gatx_set_gemm_mode(DEFAULT_GEMM_MODE)
     ref = A.double() @ W.double().t()
     got = torch.cat([C0, C1, C2], 1).double()
     assert torch.isfinite(got).all()
