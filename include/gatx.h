@@ -123,10 +123,17 @@ int gatx_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t sam, 
  * copy of W_aug, so g_x = G_aug W_aug runs with both operands k-contiguous). */
 int gatx_transpose_f32(int64_t rows, int64_t cols, const float* src, int64_t ld_src, float* dst,
                        int64_t ld_dst, gatx_stream_t stream);
-/* Arithmetic of every gatx GEMM (process-wide; env GATX_GEMM=f32|x3 sets the initial value):
- * 1 = "x3" (default): each fp32 operand split exactly into three bf16 planes, the six partial
- *     products above fp32 resolution on v_mfma_f32_32x32x16_bf16 with f32 accumulation — fp32
- *     GEMM accuracy at 2.7x fewer MFMA cycles; 0 = "f32": v_mfma_f32_32x32x2_f32. */
+/* Arithmetic of every gatx GEMM (process-wide; env GATX_GEMM=f32|x3|f16x3 sets the initial
+ * value):
+ * 2 = "f16x3" (default): each fp32 operand split into an fp16 plane and a 2^11-scaled fp16
+ *     residual plane, three products on v_mfma_f32_32x32x16_f16 with f32 accumulation — fp32
+ *     GEMM accuracy at 2x fewer MFMA cycles than x3; k-contiguous operand pairs only, and a
+ *     workgroup whose operand rows leave the fp16 range (row max |a| > 1023 or |b| > 2047, or a
+ *     nonzero row max below 2^-13) recomputes its tile as x3; other layouts run x3;
+ * 1 = "x3": each fp32 operand split exactly into three bf16 planes, the six partial products
+ *     above fp32 resolution on v_mfma_f32_32x32x16_bf16 with f32 accumulation — fp32 GEMM
+ *     accuracy at 2.7x fewer MFMA cycles than f32;
+ * 0 = "f32": v_mfma_f32_32x32x2_f32. */
 void gatx_set_gemm_mode(int mode);
 int gatx_get_gemm_mode(void);
 /* Workspace that lets gatx_gemm_f32 / gatx_projection_gemm split the K range of the tiles in
