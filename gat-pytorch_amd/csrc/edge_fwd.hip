@@ -161,6 +161,8 @@ struct EdgeFwdArgs {
   float* hub_part;         // [slot][g_count][HS*Fp + HS]
   int64_t n_items_main;
   int64_t hub_blocks;      // blocks [0, hub_blocks) run hub pieces (hub_bound * g_count waves)
+  // destinations done by the graph-local pass (gatx_edge_forward_local): skip[n] != 0 -> no item
+  const uint8_t* skip;
 };
 
 int g_debug = 0;
@@ -298,6 +300,7 @@ __global__ void __launch_bounds__(256) edge_forward_kernel(EdgeFwdArgs g) {
     hgl = (int)(rem / g.chunk);
     n = ck * g.chunk + (rem - (int64_t)hgl * g.chunk);
     if (n >= g.N) return;
+    if (g.skip && g.skip[n]) return;
     beg = uni(g.rowptr[n]);
     end = uni(g.rowptr[n + 1]);
     if (g.hub_T > 0 && end - beg > g.hub_T) return;   // done in pieces below
@@ -504,6 +507,7 @@ __global__ void __launch_bounds__(256) edge_forward_shared_kernel(EdgeFwdArgs g)
     hgl = (int)(rem / g.chunk);
     n = ck * g.chunk + (rem - (int64_t)hgl * g.chunk);
     if (n >= g.N) return;
+    if (g.skip && g.skip[n]) return;
     beg = uni(g.rowptr[n]);
     end = uni(g.rowptr[n + 1]);
     if (g.hub_T > 0 && end - beg > g.hub_T) return;
@@ -1401,6 +1405,22 @@ extern "C" int gatx_edge_forward_drop(
     int elu, float* den, int64_t chunk, int hub_edges, const int32_t* hubs,
     const int32_t* hub_count, int64_t hub_bound, float* hub_part, float out_p,
     const uint64_t* out_seed, gatx_stream_t s) {
+  return gatx_edge_forward_skip(rows, row_stride, head_stride, S, M_ord, rowptr, col, perm, N, NH,
+                                F, heads_per_item, group_begin, group_count, mean_mode, concat,
+                                const_att, bias, p, seed, out, out_ld, resid, resid_ld, elu, den,
+                                chunk, hub_edges, hubs, hub_count, hub_bound, hub_part, out_p,
+                                out_seed, nullptr, s);
+}
+
+extern "C" int gatx_edge_forward_skip(
+    const float* rows, int64_t row_stride, int64_t head_stride, const float* S,
+    const uint32_t* M_ord, const int32_t* rowptr, const int32_t* col, const int32_t* perm,
+    int64_t N, int NH, int F, int heads_per_item, int group_begin, int group_count,
+    int mean_mode, int concat, int const_att, const float* bias,
+    float p, const uint64_t* seed, float* out, int64_t out_ld, const float* resid, int64_t resid_ld,
+    int elu, float* den, int64_t chunk, int hub_edges, const int32_t* hubs,
+    const int32_t* hub_count, int64_t hub_bound, float* hub_part, float out_p,
+    const uint64_t* out_seed, const uint8_t* skip, gatx_stream_t s) {
   hipStream_t st = (hipStream_t)s;
   GATX_REQUIRE(out_p >= 0.f && out_p < 1.f, "edge_forward: output dropout must be in [0, 1)");
   GATX_REQUIRE(out_p == 0.f || out_seed != nullptr,
@@ -1440,6 +1460,7 @@ extern "C" int gatx_edge_forward_drop(
   g.resid = resid; g.resid_ld = resid_ld; g.elu = elu;
   g.out_p = out_p; g.out_seed = out_seed; g.out_cols = concat ? (int64_t)NH * F : F;
   g.den = den;
+  g.skip = skip;
   g.vec_out = concat && (F & 3) == 0 && out_ld % 4 == 0 && ((uintptr_t)out % 16) == 0 &&
               (!resid || (resid_ld % 4 == 0 && ((uintptr_t)resid % 16) == 0)) &&
               (!bias || ((uintptr_t)bias % 16) == 0);

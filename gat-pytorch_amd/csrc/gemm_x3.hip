@@ -446,10 +446,20 @@ __device__ inline bool f16_mainloop(const GemmArgs& g, const float* __restrict__
       for (int ni = 0; ni < NB; ++ni)
         acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(sb8[ni], sa8[mi], acc[mi][ni], 0, 0, 0);
   };
+  auto rows_bad = [&]() {
+    bool bad = false;
+#pragma unroll
+    for (int c = 0; c < TA::NV; ++c) bad |= f16_row_bad(amax_a[c], kF16LimA);
+#pragma unroll
+    for (int c = 0; c < TB::NV; ++c) bad |= f16_row_bad(amax_b[c], kF16LimB);
+    return bad;
+  };
   int64_t kt = 0;
   load(kb);
   store(smem, kb);
-  __syncthreads();
+  // early exit: rows already out of range in the first K-tile (e.g. a gradient operand, whose
+  // rows are tiny throughout) go to the x3 fallback before any MFMA work is spent on them
+  if (__syncthreads_or(rows_bad())) return true;
   if constexpr (!MASK && CFG == 1) {
     // steady state as in x3_mainloop: tile kt + 1 staged into the other buffer right after this
     // tile's fragment reads, tile kt + 2's loads issued before the MFMAs
@@ -491,12 +501,7 @@ __device__ inline bool f16_mainloop(const GemmArgs& g, const float* __restrict__
   }
   // true: a row of this thread's operand slices out of range (see above)
   static_assert(BK / 4 == 4, "a k-contiguous row is staged by 4 adjacent lanes");
-  bool bad = false;
-#pragma unroll
-  for (int c = 0; c < TA::NV; ++c) bad |= f16_row_bad(amax_a[c], kF16LimA);
-#pragma unroll
-  for (int c = 0; c < TB::NV; ++c) bad |= f16_row_bad(amax_b[c], kF16LimB);
-  return bad;
+  return rows_bad();
 }
 
 // Epilogue of the transposed product. acc[mi][ni] is the C^T block of output rows

@@ -282,6 +282,63 @@ def bwd_hub_args(graph: Graph, NH: int, F: int, dev, source: bool):
     return (T, ptr(hubs), ptr(count), bound, ptr(part))
 
 
+def local_plan(graph: Graph, sh: LayerShape):
+    """(windows, win_count, in_window) of the graph-local edge pass (csrc/edge_local.hip: each
+    self-contained node window's source rows staged in LDS) or None: for graphs of at most
+    GATX_LOCAL_MAX_GRAPH (2^18) nodes below the hub-splitting threshold — batches of small graphs
+    (PPI, PATTERN) — unless GATX_LOCAL=0. Nodes outside windows (components of more than
+    gatx_local_max_nodes() nodes) stay on the generic pass."""
+    if _env_int("GATX_LOCAL", 1) == 0:
+        return None
+    if (graph.num_nodes == 0 or graph.num_nodes > _env_int("GATX_LOCAL_MAX_GRAPH", 1 << 18)
+            or graph.num_input_edges > _env_int("GATX_HUB_MIN_EDGES", 1 << 22)):
+        return None
+    return graph.window_plan()
+
+
+def _edge_pass(rows, row_stride, S, M_ord, graph, sh, bias, p, seed, out, resid_p, elu, den,
+               chunk, drop_args, dev, s):
+    """The edge pass of a non-reassociated layer (concat, or head mean over head groups):
+    graph-local windows first (LDS-staged rows), the generic pass for the remaining nodes."""
+    N = graph.num_nodes
+    plan = local_plan(graph, sh)
+    skip = None
+    if plan is not None:
+        windows, wcount, inw = plan
+        part = None
+        if not sh.concat:
+            nb = lib.gatx_edge_forward_local_part_bytes(N, sh.NH, sh.F, 0)
+            part = torch.empty(max(nb // 4, 1), dtype=torch.float32, device=dev)
+        call("gatx_edge_forward_local", ptr(rows), row_stride, ptr(S), ptr(M_ord),
+             ptr(graph.rowptr), ptr(graph.col), ptr(graph.perm), N, sh.NH, sh.F,
+             int(sh.concat), int(sh.const), ptr(bias), float(p), ptr(seed), ptr(out),
+             sh.out_cols, resid_p, sh.out_cols, int(elu), ptr(den), *drop_args,
+             ptr(windows), ptr(wcount), ptr(inw), N, ptr(part), s)
+        skip = ptr(inw)
+    hs = edge_heads_per_item(sh)
+    if skip is not None and not sh.concat and sh.NH <= 8 and sh.NH * sh.Fp <= 2048:
+        hs = sh.NH   # the few non-window nodes of a head-mean layer: one launch, all heads
+    ng = sh.NH // hs
+    if sh.concat or ng == 1:
+        hub = hub_args(graph, sh, hs, ng, dev)
+        call("gatx_edge_forward_skip", ptr(rows), row_stride, sh.Fp, ptr(S), ptr(M_ord),
+             ptr(graph.rowptr), ptr(graph.col), ptr(graph.perm), N, sh.NH, sh.F, hs,
+             0, 0, 0, int(sh.concat), int(sh.const), ptr(bias), float(p), ptr(seed),
+             ptr(out), sh.out_cols, resid_p, sh.out_cols, int(elu), ptr(den), chunk, *hub,
+             *drop_args, skip, s)
+    else:   # head mean over groups: one launch per group, accumulated in stream order
+        hub = hub_args(graph, sh, hs, 1, dev)
+        for gi in range(ng):
+            last = gi == ng - 1
+            mode = 1 if gi == 0 else (3 if last else 2)
+            call("gatx_edge_forward_skip", ptr(rows), row_stride, sh.Fp, ptr(S), ptr(M_ord),
+                 ptr(graph.rowptr), ptr(graph.col), ptr(graph.perm), N, sh.NH, sh.F, hs,
+                 gi, 1, mode, 0, int(sh.const), ptr(bias) if last else None, float(p),
+                 ptr(seed), ptr(out), sh.out_cols, resid_p if last else None, sh.out_cols,
+                 int(elu) if last else 0, ptr(den), chunk, *hub,
+                 *(drop_args if last else (0.0, None)), skip, s)
+
+
 def fold_scores_into_gemm(sh: LayerShape) -> bool:
     """Compute S as 2NH extra GEMM columns only when they fit the last column tile for free;
     otherwise (e.g. Dp = 1024: a whole extra 128-wide tile, +12% GEMM time) project Wh alone and
@@ -447,27 +504,9 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
         with _span("attention_max", (E2, sh.NH)):
             call("gatx_attention_max", ptr(graph.col), ptr(graph.rowidx), E2, graph.e2_ptr,
                  ptr(S), sh.NH, ptr(M_ord), ptr(argmax), ptr(_max_ws(dev)), s)
-    with _span("edge_forward", (N, E2, sh.NH, sh.F, sh.concat)):
-        hs = edge_heads_per_item(sh)
-        ng = sh.NH // hs
-        if sh.concat or ng == 1:
-            hub = hub_args(graph, sh, hs, ng, dev)
-            call("gatx_edge_forward_drop", ptr(Wh), sh.Dp, sh.Fp, ptr(S), ptr(M_ord),
-                 ptr(graph.rowptr), ptr(graph.col), ptr(graph.perm), N, sh.NH, sh.F, hs,
-                 0, 0, 0, int(sh.concat), int(sh.const), ptr(bias), float(p), ptr(seed),
-                 ptr(out), sh.out_cols, resid_p, sh.out_cols, int(elu), ptr(den), chunk, *hub,
-                 *drop_args, s)
-        else:   # head mean over groups: one launch per group, accumulated in stream order
-            hub = hub_args(graph, sh, hs, 1, dev)
-            for gi in range(ng):
-                last = gi == ng - 1
-                mode = 1 if gi == 0 else (3 if last else 2)
-                call("gatx_edge_forward_drop", ptr(Wh), sh.Dp, sh.Fp, ptr(S), ptr(M_ord),
-                     ptr(graph.rowptr), ptr(graph.col), ptr(graph.perm), N, sh.NH, sh.F, hs,
-                     gi, 1, mode, 0, int(sh.const), ptr(bias) if last else None, float(p),
-                     ptr(seed), ptr(out), sh.out_cols, resid_p if last else None, sh.out_cols,
-                     int(elu) if last else 0, ptr(den), chunk, *hub,
-                     *(drop_args if last else (0.0, None)), s)
+    with _span("edge_forward", (N, E2, sh.NH, sh.F, sh.concat)):   # local + generic: one record
+        _edge_pass(Wh, sh.Dp, S, M_ord, graph, sh, bias, p, seed, out, resid_p, elu, den, chunk,
+                   drop_args, dev, s)
     if want_alpha:
         with _span("attention_alpha", (E2, sh.NH)):
             _attention_alpha(graph, S, M_ord, den, sh, alpha, argmax, s)
