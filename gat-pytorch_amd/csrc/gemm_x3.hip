@@ -110,15 +110,32 @@ struct X3Tile {
       v[c].w = ok && lim > 3 ? v[c].w : 0.f;
     }
   }
+  // Power-of-two scale per staged row from its max |x| in this (the first) K-tile: the row is
+  // brought to max |x| in [2^(TGT-1), 2^TGT) (1 for an all-zero or non-finite max). KC only: a
+  // row's 4 staging lanes are adjacent.
+  template <int TGT>
+  static __device__ inline void row_scales(const float4 (&v)[NV], float (&sc)[NV]) {
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      float m = fmaxf(fmaxf(fabsf(v[c].x), fabsf(v[c].y)), fmaxf(fabsf(v[c].z), fabsf(v[c].w)));
+      m = fmaxf(m, __shfl_xor(m, 1));
+      m = fmaxf(m, __shfl_xor(m, 2));
+      int e = 0;
+      (void)frexpf(m, &e);   // m = f 2^e, f in [0.5, 1)
+      sc[c] = (m > 0.f && m <= 3.0e38f) ? ldexpf(1.f, TGT - e) : 1.f;
+    }
+  }
   // f16x3 staging (see f16_mainloop): plane 0 = h = fp16_rn(x), plane 1 = fp16_rn(2^11 (x - h));
   // amax tracks max |x| over the staged elements for the caller's range check.
-  template <bool MASK, bool KTAIL>
+  template <bool MASK, bool KTAIL, bool SCALED>
   static __device__ inline void store_f16(char* img, float4 (&v)[NV], int64_t r0, int64_t rmax,
-                                          int64_t k0, int64_t kmax, float (&amax)[NV]) {
+                                          int64_t k0, int64_t kmax, float (&amax)[NV],
+                                          const float (&sc)[NV]) {
     mask<MASK, KTAIL>(v, r0, rmax, k0, kmax);
 #pragma unroll
     for (int c = 0; c < NV; ++c) {
       const int idx = threadIdx.x + NT * c;
+      if (SCALED) v[c] = v[c] * sc[c];   // the row's power-of-two scale (exact)
       amax[c] = fmaxf(amax[c], fmaxf(fmaxf(fabsf(v[c].x), fabsf(v[c].y)),
                                      fmaxf(fabsf(v[c].z), fabsf(v[c].w))));
       uint32_t h0, l0, h1, l1;
@@ -334,6 +351,11 @@ __device__ inline void x3_mainloop(const GemmArgs& g, const float* __restrict__ 
 // (v_pk_mul_f16, exact); fp16 products are exact in the f32 accumulator, which is scaled by 2^-11
 // (exact) at the end: fp32-GEMM accuracy (tests/test_gpu_layer.py against fp64) at 3 MFMA
 // products per step instead of the bf16 split's 6, and two LDS planes per operand instead of 3.
+// Row scaling: every A row (an output row: activations, or a gradient's ~1e-7 rows) is multiplied
+// by a power of two chosen from its max |x| in the workgroup's first K-tile (to [2^7, 2^8)),
+// exactly undone in the epilogue, so it lands in the fp16 range with 4-8x headroom for the rest
+// of its K range. B (the weights in every caller) is not scaled (a per-column scale cost 14-19
+// spilled VGPRs in the epilogue).
 // Range: 64 a_h and 32 b_h must be finite fp16, i.e. |a| <= 1023 and |b| <= 2047; and below
 // 2^-13 an element's pieces reach fp16 subnormals (absolute error up to 2^-36), harmless next to
 // the row's larger elements but not for a row that is tiny throughout. Every thread tracks
@@ -351,7 +373,7 @@ __device__ inline bool f16_row_bad(float m, float lim) {
   return !(m <= lim) || (m > 0.f && m < kF16Tiny);
 }
 
-template <bool A_KC, bool B_KC, bool MASK, int CFG>
+template <bool A_KC, bool B_KC, bool MASK, int CFG, bool SCALE>
 __device__ inline bool f16_mainloop(const GemmArgs& g, const float* __restrict__ A,
                                     const float* __restrict__ B, int64_t m0, int64_t n0,
                                     int64_t kb, int64_t K, int64_t nk, char* smem, int wm, int wn,
@@ -370,6 +392,7 @@ __device__ inline bool f16_mainloop(const GemmArgs& g, const float* __restrict__
 #pragma unroll
   for (int c = 0; c < TB::NV; ++c) amax_b[c] = 0.f;
   float4 va[TA::NV], vb[TB::NV];
+  float sca[TA::NV], scb[TB::NV];   // per staged row: power-of-two scale (see above)
   const float* pa[TA::NV];
   const float* pb[TB::NV];
   int64_t sa = 0, sb = 0;
@@ -401,14 +424,14 @@ __device__ inline bool f16_mainloop(const GemmArgs& g, const float* __restrict__
   };
   auto store = [&](char* st, int64_t k0) {
     if (MASK) {
-      TA::template store_f16<true, true>(st, va, m0, M, k0, K, amax_a);
-      TB::template store_f16<true, true>(st + 2 * PA, vb, n0, N, k0, K, amax_b);
+      TA::template store_f16<true, true, SCALE>(st, va, m0, M, k0, K, amax_a, sca);
+      TB::template store_f16<true, true, false>(st + 2 * PA, vb, n0, N, k0, K, amax_b, scb);
     } else if (k0 + BK > K) {
-      TA::template store_f16<false, true>(st, va, m0, M, k0, K, amax_a);
-      TB::template store_f16<false, true>(st + 2 * PA, vb, n0, N, k0, K, amax_b);
+      TA::template store_f16<false, true, SCALE>(st, va, m0, M, k0, K, amax_a, sca);
+      TB::template store_f16<false, true, false>(st + 2 * PA, vb, n0, N, k0, K, amax_b, scb);
     } else {
-      TA::template store_f16<false, false>(st, va, m0, M, k0, K, amax_a);
-      TB::template store_f16<false, false>(st + 2 * PA, vb, n0, N, k0, K, amax_b);
+      TA::template store_f16<false, false, SCALE>(st, va, m0, M, k0, K, amax_a, sca);
+      TB::template store_f16<false, false, false>(st + 2 * PA, vb, n0, N, k0, K, amax_b, scb);
     }
   };
   f16x8 fa[MB][2], fb[NB][2];
@@ -456,6 +479,18 @@ __device__ inline bool f16_mainloop(const GemmArgs& g, const float* __restrict__
   };
   int64_t kt = 0;
   load(kb);
+#pragma unroll
+  for (int c = 0; c < TB::NV; ++c) scb[c] = 1.f;   // B (the weights) is not scaled
+#pragma unroll
+  for (int c = 0; c < TA::NV; ++c) sca[c] = 1.f;
+  if constexpr (SCALE) {
+    TA::template row_scales<8>(va, sca);
+    // the A rows' inverse scales, for the epilogue: [TBM] floats after the two stages
+    float* inv = (float*)(smem + 2 * STAGE);
+#pragma unroll
+    for (int c = 0; c < TA::NV; ++c)
+      if ((threadIdx.x & 3) == 0) inv[TA::row_of(threadIdx.x + NT * c)] = 1.f / sca[c];
+  }
   store(smem, kb);
   // early exit: rows already out of range in the first K-tile (e.g. a gradient operand, whose
   // rows are tiny throughout) go to the x3 fallback before any MFMA work is spent on them
@@ -470,8 +505,8 @@ __device__ inline bool f16_mainloop(const GemmArgs& g, const float* __restrict__
         char* cur = smem + (kt & 1) * STAGE;
         char* nxt = smem + ((kt & 1) ^ 1) * STAGE;
         frags(cur);
-        TA::template store_f16<false, false>(nxt, va, m0, M, 0, K, amax_a);
-        TB::template store_f16<false, false>(nxt + 2 * PA, vb, n0, N, 0, K, amax_b);
+        TA::template store_f16<false, false, SCALE>(nxt, va, m0, M, 0, K, amax_a, sca);
+        TB::template store_f16<false, false, false>(nxt + 2 * PA, vb, n0, N, 0, K, amax_b, scb);
 #pragma unroll
         for (int c = 0; c < TA::NV; ++c) { va[c] = *(const float4*)pa[c]; pa[c] += sa; }
 #pragma unroll
@@ -482,8 +517,8 @@ __device__ inline bool f16_mainloop(const GemmArgs& g, const float* __restrict__
       char* cur = smem + (kt & 1) * STAGE;
       char* nxt = smem + ((kt & 1) ^ 1) * STAGE;
       frags(cur);
-      TA::template store_f16<false, false>(nxt, va, m0, M, 0, K, amax_a);
-      TB::template store_f16<false, false>(nxt + 2 * PA, vb, n0, N, 0, K, amax_b);
+      TA::template store_f16<false, false, SCALE>(nxt, va, m0, M, 0, K, amax_a, sca);
+      TB::template store_f16<false, false, false>(nxt + 2 * PA, vb, n0, N, 0, K, amax_b, scb);
       mfmas();
       __syncthreads();
       ++kt;
@@ -727,16 +762,30 @@ __global__ void __launch_bounds__(X3Cfg<CFG>::NT, X3Cfg<CFG>::MINB) gemm_x3_kern
   if (nk > 0) {
     bool x3 = true;
     if constexpr (A_KC && B_KC && DBG == 0) if (arith == 2) {
+      // row scaling for the gradient GEMMs (TAG != 0: A = G_aug, rows ~1e-7); the forward
+      // projection's activations are in range as they come (a row that is not takes the fallback)
+      constexpr bool SCALE = TAG != 0;
       const bool bad =
-          VEC ? f16_mainloop<A_KC, B_KC, false, CFG>(g, A, B, m0, n0, kb, K, nk, smem, wm, wn, lane, acc)
-              : f16_mainloop<A_KC, B_KC, true, CFG>(g, A, B, m0, n0, kb, K, nk, smem, wm, wn, lane, acc);
+          VEC ? f16_mainloop<A_KC, B_KC, false, CFG, SCALE>(g, A, B, m0, n0, kb, K, nk, smem, wm,
+                                                             wn, lane, acc)
+              : f16_mainloop<A_KC, B_KC, true, CFG, SCALE>(g, A, B, m0, n0, kb, K, nk, smem, wm,
+                                                            wn, lane, acc);
       x3 = __syncthreads_or(bad);   // the workgroup's tiles out of fp16 range: redo as x3
+      // undo 2^11 and the row / column scales: lane -> row, register 4j + i -> column (the
+      // transposed product's layout, write_tile_t)
+      constexpr int STAGE16 = 2 * 2 * (C::TBM + C::TBN) * C::BK;
+      const float* inv = (const float*)(smem + 2 * STAGE16);
+      const int lr = lane & 31, lc = 4 * (lane >> 5);
+      (void)lc;
 #pragma unroll
-      for (int i = 0; i < C::MB; ++i)
+      for (int i = 0; i < C::MB; ++i) {
+        const float ra = SCALE ? inv[wm * (C::MB * 32) + i * 32 + lr] * 0x1p-11f : 0x1p-11f;
 #pragma unroll
         for (int j = 0; j < C::NB; ++j)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) acc[i][j][r] = x3 ? 0.f : acc[i][j][r] * 0x1p-11f;
+          for (int r = 0; r < 16; ++r) acc[i][j][r] = x3 ? 0.f : acc[i][j][r] * ra;
+      }
+      __syncthreads();   // the scales are read before a fallback or the epilogue reuses the LDS
     }
     if (x3) {
       if (VEC)

@@ -283,12 +283,14 @@ def bwd_hub_args(graph: Graph, NH: int, F: int, dev, source: bool):
 
 
 def local_plan(graph: Graph, sh: LayerShape):
-    """(windows, win_count, in_window) of the graph-local edge pass (csrc/edge_local.hip: each
-    self-contained node window's source rows staged in LDS) or None: for graphs of at most
-    GATX_LOCAL_MAX_GRAPH (2^18) nodes below the hub-splitting threshold — batches of small graphs
-    (PPI, PATTERN) — unless GATX_LOCAL=0. Nodes outside windows (components of more than
-    gatx_local_max_nodes() nodes) stay on the generic pass."""
-    if _env_int("GATX_LOCAL", 1) == 0:
+    """(starts, count, in_window) of the graph-local edge pass (csrc/edge_local.hip: each
+    self-contained node component's source rows staged in LDS) or None. Opt-in (GATX_LOCAL=1):
+    measured on MI355X it does not beat the generic L2-gather pass (PPI L1 311 vs 285 us, the
+    head-mean L2 255 vs 193-246 us: the per-edge broadcast / address / 4-float FMA work of a
+    16-float chunk costs more issue than the L2 gathers it saves). For graphs of
+    at most GATX_LOCAL_MAX_GRAPH (2^18) nodes below the hub-splitting threshold; nodes of
+    components larger than gatx_local_max_nodes() stay on the generic pass."""
+    if _env_int("GATX_LOCAL", 0) == 0:
         return None
     if (graph.num_nodes == 0 or graph.num_nodes > _env_int("GATX_LOCAL_MAX_GRAPH", 1 << 18)
             or graph.num_input_edges > _env_int("GATX_HUB_MIN_EDGES", 1 << 22)):

@@ -153,16 +153,22 @@ def test_gemm_x3_split_accuracy(split_mode, device):
     relative to sum|a||b| must stay at the fp32 GEMM's level (<= 1.25x f32's, and < 1e-6
     absolute-relative) for every operand layout, 128- and 256-wide tiles (kind chosen by size),
     partial K-tiles, ragged edges, unaligned leading dimensions and split-K; repeated launches
-    are bitwise identical. The f16x3 cases include operands far outside its range (|a| ~ 1e4:
-    those tiles take the fallback) and tiny ones (|a| ~ 1e-6: fp16 subnormal hi parts)."""
+    are bitwise identical. The f16x3 cases include operands of any scale (|a| ~ 1e4 and ~ 1e-6:
+    per-row power-of-two scaling from the first K-tile brings them into the fp16 range) and rows
+    whose magnitude grows 10^6-fold along K ("ramp": the later tiles overflow the first tile's
+    scale, so those workgroups take the x3 fallback)."""
     from gatx._lib import call, lib, ptr, stream
     torch.manual_seed(11)
     cases = [(600, 520, 1100, 30), (300, 257, 33, 30), (1000, 760, 70, 30),
              (2000, 1024, 1100, 30), (513, 300, 4096, 30), (129, 129, 17, 30),
-             (44, 1030, 70, 30), (700, 600, 300, 1e4), (700, 600, 300, 1e-6)]
+             (44, 1030, 70, 30), (700, 600, 300, 1e4), (700, 600, 300, 1e-6),
+             (700, 600, 300, "ramp")]
     try:
         for (M, N, K, amp) in cases:
-            A = torch.randn(M, K, device=device) * torch.rand(M, 1, device=device) * amp
+            if amp == "ramp":
+                A = torch.randn(M, K, device=device) * torch.logspace(-3, 3, K, device=device)
+            else:
+                A = torch.randn(M, K, device=device) * torch.rand(M, 1, device=device) * amp
             B = torch.randn(K, N, device=device)
             ref = A.double() @ B.double()
             S = (A.double().abs() @ B.double().abs()).clamp_min(1e-30)

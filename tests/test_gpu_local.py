@@ -17,10 +17,14 @@ pytestmark = pytest.mark.gpu
 OUT_TOL = 1e-4
 
 
-def _set_local(on: bool):
+def _set_local(on):
+    """on: True / False forces the graph-local pass on / off; None restores the default (off)."""
     import os
     from gatx.functional import reset_tuning
-    os.environ["GATX_LOCAL"] = "1" if on else "0"
+    if on is None:
+        os.environ.pop("GATX_LOCAL", None)
+    else:
+        os.environ["GATX_LOCAL"] = "1" if on else "0"
     reset_tuning()
 
 
@@ -104,7 +108,7 @@ def test_local_layer_vs_oracle(NH, F, concat, bias, device):
                                            layer.W.weight.grad.cpu().numpy()))
             assert np.array_equal(ei2.cpu().numpy(), r_ei)
     finally:
-        _set_local(True)
+        _set_local(None)
     loc, loc2, gen = res[True][0], res[True][1], res[False][0]
     for u, v in zip(loc, loc2):
         assert np.array_equal(u, v)
@@ -144,6 +148,6 @@ def test_local_dropout_and_epilogue_match_generic(concat, device):
                     out_dropout=(0.2, oseed) if concat else None)
             outs[on] = out.cpu().numpy()
     finally:
-        _set_local(True)
+        _set_local(None)
     assert np.abs(outs[True] - outs[False]).max() <= 1e-5 * max(1.0, np.abs(outs[False]).max())
     assert (outs[True] == 0).sum() == (outs[False] == 0).sum()
