@@ -306,19 +306,21 @@ int gatx_edge_forward_skip(const float* rows, int64_t row_stride, int64_t head_s
                            const int32_t* hub_count, int64_t hub_bound, float* hub_part,
                            float out_p, const uint64_t* out_seed, const uint8_t* skip,
                            gatx_stream_t stream);
-/* Self-contained node windows of a destination CSR (the graphs of a collated batch): the node
+/* Self-contained node components of a destination CSR (the graphs of a collated batch): the node
  * order is cut wherever no edge crosses (no destination before the cut has a source after it or
- * vice versa); every component of at most max_nodes (<= gatx_local_max_nodes()) nodes becomes a
- * window [start, end) in windows ([N][2] bound), *win_count of them; in_window[n] = 1 for their
- * nodes, 0 for nodes of larger components. Device-side (no host sync, capturable). */
+ * vice versa). windows (an [N][2] int32 buffer) receives the component starts P[0..C] (P[C] = N),
+ * *win_count = C; in_window[n] = 1 for the nodes of components of at most max_nodes
+ * (<= gatx_local_max_nodes()) nodes, 0 otherwise. Device-side (no host sync, capturable). Used
+ * by the opt-in graph-local edge pass below. */
 int gatx_local_max_nodes(void);
 size_t gatx_graph_windows_workspace_bytes(int64_t num_nodes);
 int gatx_graph_windows(const int32_t* rowptr, const int32_t* col, int64_t num_nodes,
                        int max_nodes, int32_t* windows, int32_t* win_count, uint8_t* in_window,
                        void* workspace, size_t workspace_bytes, gatx_stream_t stream);
 /* The edge pass of gatx_edge_forward_drop (models/gat_layer.py:66-135 for every head) for the
- * destinations of the windows above, with each window's source rows staged in LDS in 16-float
- * chunks (one workgroup per (window, head, chunk), persistent over a CU-sized grid): the same
+ * destinations of the in_window components above (windows / win_count: gatx_graph_windows'
+ * starts and count), with each component's source rows staged in LDS in 16-float chunks (one
+ * workgroup per (component, head, chunk), persistent over a CU-sized grid): the same
  * attention weights, softmax denominators (den), dropout masks and fused epilogue (bias, resid,
  * ELU, next layer's dropout); rows = Wh [N][row_stride] with head h at column h*round4(F).
  * concat = 0 (head mean): part (gatx_edge_forward_local_part_bytes) holds the normalised head
