@@ -2,7 +2,7 @@
 split x -> (h, l) = (fp16_rn(x), fp16_rn(2^11 (x - h))), the per-row power-of-two scale of A
 from its first 16-wide K-tile, and the three products (64 h_a)(32 h_b) + h_a l_b + l_a h_b
 scaled back by 2^-11. Checks the arithmetic's own error claims against float64 — the split is
-within 2^-23 relative of x inside the fp16 range, and the three-product GEMM with fp32
+within 2^-22 relative of x inside the fp16 range, and the three-product GEMM with fp32
 accumulation stays at the fp32 GEMM's error level — and the range rules that send a tile to
 the x3 fallback. (The GPU test test_gemm_x3_split_accuracy checks the kernel itself.)"""
 import numpy as np
