@@ -5,7 +5,8 @@ Inductive datasets (PPI, PATTERN) are disjoint unions of graphs, so a rank takes
 Training needs exactly one exchange per step: the gradient all-reduce. `GradientAllReducer`
 overlaps it with the backward the way DDP does: gradients are grouped into buckets in reverse
 registration order (the order backward produces them), and each bucket's all-reduce is launched
-asynchronously from a post-accumulate-grad hook the moment its last gradient is ready, while
+asynchronously from a post-accumulate-grad hook once its gradients are ready (buckets go out in
+index order on every rank, whatever order the hooks fire in), while
 autograd keeps computing earlier layers' gradients. PPI's 1.87 M parameters (7.47 MB) make a few
 buckets; PATTERN's 20 k parameters (81 KB) one latency-bound bucket.
 
@@ -174,12 +175,20 @@ class GradientAllReducer:
 
     Buckets hold consecutive parameters in reverse registration order (backward produces the
     last layer's gradients first), at most `bucket_bytes` each. A bucket's flat buffer is filled
-    from the post-accumulate-grad hooks of its parameters; when the last one arrives the bucket's
-    all-reduce (SUM; then x 1/world when `average`) is issued with async_op, so RCCL moves it over
-    xGMI while autograd continues. Parameters that got no gradient this step are reduced as zeros
-    in finish() (every rank must issue the same collectives, as in DDP with
-    find_unused_parameters); they leave finish() with the reduced .grad (zeros if no rank
-    produced one)."""
+    from the post-accumulate-grad hooks of its parameters; once the last one has arrived the
+    bucket's all-reduce (SUM; then x 1/world when `average`) is issued with async_op, so RCCL
+    moves it over xGMI while autograd continues.
+
+    Collective order: RCCL matches collectives by issue order, so every rank must issue the
+    buckets' all-reduces in the same order. Buckets are launched strictly in index order, as DDP
+    does: a bucket that fills before its predecessors waits in the queue and goes out right after
+    them. The order in which autograd fires the hooks may therefore differ between ranks without
+    mismatching collectives.
+
+    Parameters whose hook did not fire in the synced backward are filled in finish() from their
+    .grad (what no_sync() micro-steps accumulated on this rank) or with zeros when they have none
+    (every rank issues the same collectives, as DDP with find_unused_parameters); they leave
+    finish() with the reduced .grad (zeros if no rank produced one)."""
 
     def __init__(self, params: Iterable[torch.nn.Parameter], bucket_bytes: int = 4 << 20,
                  group=None, average: bool = True, always_reduce: bool = False):
@@ -220,6 +229,7 @@ class GradientAllReducer:
         return {"params": params, "offsets": offs, "numel": o, "flat": None}
 
     def _reset(self):
+        self._next = 0   # the next bucket to launch (buckets go out in index order)
         for b in self.buckets:
             b["ready"] = 0
             b["work"] = None
@@ -259,25 +269,43 @@ class GradientAllReducer:
         if not b["seen"][pi]:
             b["seen"][pi] = True
             b["ready"] += 1
-        if b["ready"] == len(b["params"]) and not b["launched"]:
-            b["launched"] = True
-            b["work"] = _all_reduce_flat(flat, self.group, async_op=True)
+        self._launch_ready()
+
+    def _launch(self, b):
+        b["launched"] = True
+        b["work"] = _all_reduce_flat(b["flat"], self.group, async_op=True)
+        self._next += 1
+
+    def _launch_ready(self):
+        """Issue the all-reduces of the complete buckets at the head of the queue, in index
+        order (never a later bucket ahead of an earlier one: the collective order is the same on
+        every rank whatever order the hooks fired in)."""
+        while self._next < len(self.buckets):
+            b = self.buckets[self._next]
+            if b["ready"] != len(b["params"]):
+                return
+            self._launch(b)
 
     def finish(self):
         """Wait for every bucket's all-reduce and write the results into .grad."""
         if not self.active:
             return
         dev = next((p.grad.device for p in self.params if p.grad is not None), None)
-        for b in self.buckets:
-            if not b["launched"]:   # some parameters produced no gradient on this rank
-                flat = self._flat(b, torch.empty(0, device=dev) if dev is not None
-                                  else b["params"][0])
-                for pi, p in enumerate(b["params"]):
-                    if not b["seen"][pi]:
-                        o = b["offsets"][pi]
+        for b in self.buckets:   # the rest of the queue, still in index order
+            if b["launched"]:
+                continue
+            flat = self._flat(b, torch.empty(0, device=dev) if dev is not None
+                              else b["params"][0])
+            for pi, p in enumerate(b["params"]):
+                if not b["seen"][pi]:
+                    # no hook in the synced backward: this rank's gradient is whatever .grad
+                    # holds (no_sync() micro-steps), or nothing
+                    o = b["offsets"][pi]
+                    if p.grad is not None:
+                        flat[o:o + p.numel()].copy_(p.grad.reshape(-1))
+                    else:
                         flat[o:o + p.numel()].zero_()
-                b["launched"] = True
-                b["work"] = _all_reduce_flat(flat, self.group, async_op=True)
+            self._launch(b)
         for b in self.buckets:
             if b["work"] is not None:
                 b["work"].wait()

@@ -244,3 +244,115 @@ def test_per_term_count_weights_world3():
     ref = torch.cat([p.grad.reshape(-1) for p in model.parameters()])
     for r in range(world):
         assert torch.allclose(out[r], ref, atol=1e-6), (r, (out[r] - ref).abs().max())
+
+
+class _TwoBranch(torch.nn.Module):
+    """out = branch_a(x) + branch_b(x). `b_first` evaluates branch_b first: autograd then runs
+    branch_a's backward first (reverse creation order), so the parameters' post-accumulate-grad
+    hooks fire in a different order with the same values (float addition commutes)."""
+
+    def __init__(self):
+        super().__init__()
+        self.a1, self.a2 = torch.nn.Linear(5, 6), torch.nn.Linear(6, 1)
+        self.b1, self.b2 = torch.nn.Linear(5, 4), torch.nn.Linear(4, 1)
+
+    def branch_a(self, x):
+        return self.a2(torch.nn.functional.elu(self.a1(x)))
+
+    def branch_b(self, x):
+        return self.b2(torch.nn.functional.elu(self.b1(x)))
+
+    def forward(self, x, b_first=False, use=("a", "b")):
+        if use == ("a",):
+            return self.branch_a(x)
+        if use == ("b",):
+            return self.branch_b(x)
+        if b_first:
+            yb = self.branch_b(x)
+            return self.branch_a(x) + yb
+        ya = self.branch_a(x)
+        return ya + self.branch_b(x)
+
+
+def _order_worker(rank, world, port, out):
+    """Rank 1 fires its hooks in another order than ranks 0 and 2 (one bucket per parameter):
+    the buckets must still go out in index order everywhere, giving the union-batch gradient."""
+    from gatx.distributed import GradientAllReducer, count_weight
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    model = _TwoBranch()
+    fired = []
+    for name, p in model.named_parameters():
+        p.register_post_accumulate_grad_hook(lambda p, n=name: fired.append(n))
+    reducer = GradientAllReducer(model.parameters(), bucket_bytes=64, average=False)
+    x, y = _union_data()
+    rows = [list(range(0, 3)), list(range(3, 8)), list(range(8, 13))][rank]
+    for _ in range(2):
+        fired.clear()
+        model.zero_grad(set_to_none=True)
+        w = count_weight(len(rows))
+        loss = torch.nn.functional.binary_cross_entropy_with_logits(
+            model(x[rows], b_first=rank == 1).squeeze(-1), y[rows])
+        (loss * w).backward()
+        reducer.finish()
+    out[rank] = torch.cat([p.grad.reshape(-1) for p in model.parameters()]).clone()
+    out[f"fired{rank}"] = list(fired)
+    out[f"nbuckets{rank}"] = len(reducer.buckets)
+    reducer.remove()
+    dist.destroy_process_group()
+
+
+def test_bucket_order_independent_of_hook_order_world3():
+    world = 3
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_order_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    # the permutation really happened: rank 1's hooks fired in another order
+    assert out["fired0"] == out["fired2"] and out["fired0"] != out["fired1"]
+    assert out["nbuckets0"] >= 4
+    torch.manual_seed(0)
+    model = _TwoBranch()
+    x, y = _union_data()
+    torch.nn.functional.binary_cross_entropy_with_logits(model(x).squeeze(-1), y).backward()
+    ref = torch.cat([p.grad.reshape(-1) for p in model.parameters()])
+    for r in range(world):
+        assert torch.allclose(out[r], ref, atol=1e-6), (r, (out[r] - ref).abs().max())
+
+
+def _nosync_only_worker(rank, world, port, out):
+    """branch_b gets its gradient only in the no_sync micro-step; the synced backward touches
+    branch_a alone. finish() must reduce branch_b's accumulated .grad, not zeros."""
+    from gatx.distributed import GradientAllReducer
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    model = _TwoBranch()
+    reducer = GradientAllReducer(model.parameters(), bucket_bytes=64, average=False)
+    x, _ = _union_data()
+    rows = list(range(rank, 13, world))
+    model.zero_grad(set_to_none=True)
+    with reducer.no_sync():
+        model(x[rows], use=("b",)).sum().backward()
+    model(x[rows], use=("a",)).sum().backward()
+    reducer.finish()
+    out[rank] = torch.cat([p.grad.reshape(-1) for p in model.parameters()]).clone()
+    reducer.remove()
+    dist.destroy_process_group()
+
+
+def test_no_sync_only_gradient_is_reduced_world2():
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_nosync_only_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    torch.manual_seed(0)
+    model = _TwoBranch()
+    x, _ = _union_data()
+    model(x, use=("b",)).sum().backward()
+    model(x, use=("a",)).sum().backward()
+    ref = torch.cat([p.grad.reshape(-1) for p in model.parameters()])
+    for r in range(world):
+        assert torch.allclose(out[r], ref, atol=1e-5), (r, (out[r] - ref).abs().max())
