@@ -86,6 +86,21 @@ def gemm_roof():
                 kernel="gemm_f32_kernel (v_mfma_f32_32x32x2_f32)")
 
 
+def gemm_dtype():
+    """The bench line's `dtype`: the arithmetic the path computes in. Data and accumulation are
+    fp32; the GEMMs run split arithmetics on the fp16 / bf16 matrix cores with fp32 accuracy."""
+    from gatx import _lib
+    mode = _lib.lib.gatx_get_gemm_mode()
+    if mode == 2:
+        gw = _lib.lib.gatx_gemm_layout_mode(0, 0)
+        return ("fp32 (GEMMs: f16x3 split = 2 fp16 planes x 3 MFMA products, x3 fallback per "
+                "out-of-range tile" + ("" if gw == 2 else "; weight gradient x3 = 3 bf16 planes x "
+                                       "6 products") + ")")
+    if mode == 1:
+        return "fp32 (GEMMs: x3 split = 3 bf16 planes x 6 MFMA products)"
+    return "fp32 (GEMMs: v_mfma_f32_32x32x2_f32)"
+
+
 def run_timed(step, steps, world, dev, instr_step=None):
     """The timed region: barrier + synchronize on both sides, max over ranks. Returns (elapsed,
     per-kernel HIP-event records, instrumented step count). Only the last steps // 10 (>= 1)
@@ -149,21 +164,23 @@ def survey_bytes(N, E2, F_in, NH, F, concat):
     return b_gemm, f_gemm, b_edge
 
 
-def layer_dataflow(N, E2, F_in, NH, F, concat, resid):
+def layer_dataflow(N, E2, F_in, NH, F, concat, resid, alpha=True):
     """Per-kernel COMPULSORY bytes and flops of one gatx layer forward, following the dataflow the
     library actually runs (gatx.functional.layer_forward): the reassociated first layer gathers
     4*round4(F_in)-byte x rows, the others 4*NH*Fp-byte Wh rows. Gathered rows count once per
     node when the gathered matrix fits in the on-chip caches (<= the 256 MB MALL: every PPI /
     PATTERN / Planetoid batch), and once per EDGE when it does not (RMAT: 20 GB of Wh gathered
     in random order, so every gather is an HBM read; hub sources aside). Every other array is
-    read or written once. Returns [(kernel, bytes, flops)]."""
-    from gatx.functional import LayerShape, fold_scores_into_gemm, use_reassociation
+    read or written once. alpha=False: the inference forward defers the alpha pass to the first
+    read of normalised_attention_coeffs (gatx.functional.LazyAlpha), so a step that never reads
+    it does not run it. Returns [(kernel, bytes, flops)]."""
+    from gatx.functional import LayerShape, _env_int, fold_scores_into_gemm, use_reassociation
     sh = LayerShape(NH, F, F_in, concat, False)
     H2, Fp, Dp = 2 * NH, sh.Fp, sh.Dp
     oc = sh.out_cols
     r = oc if resid else 0
     mx = ("attention_max", 4 * (2 * E2 + N * H2), 0)
-    alpha = ("attention_alpha", 16 * E2 + 4 * (N * H2 + N * NH + E2 * NH), 0)
+    alpha = [("attention_alpha", 16 * E2 + 4 * (N * H2 + N * NH + E2 * NH), 0)] if alpha else []
     if use_reassociation(sh):
         Fin_p = _r4(F_in)
         gath = N * Fin_p if N * Fin_p * 4 <= MALL_BYTES else E2 * Fin_p
@@ -171,7 +188,7 @@ def layer_dataflow(N, E2, F_in, NH, F, concat, resid):
             ("gemm_scores", 4 * (N * F_in + H2 * F_in + N * H2), 2 * N * F_in * H2),
             mx,
             ("edge_forward", 4 * ((N + 1) + E2 + N * H2 + gath + N * NH * Fin_p + N * NH), 0),
-            alpha,
+            *alpha,
             ("gemm_out", 4 * (N * NH * Fin_p + NH * F * Fin_p + N * oc + N * r),
              2 * N * Fin_p * NH * F),
         ]
@@ -180,13 +197,106 @@ def layer_dataflow(N, E2, F_in, NH, F, concat, resid):
     if fold_scores_into_gemm(sh):
         out.append(("gemm", 4 * (N * F_in + (Dp + H2) * F_in + N * Dp + N * H2),
                     2 * N * F_in * (NH * F + H2)))
+    elif _env_int("GATX_FUSED_SCORES", 1):
+        # S reduced from the accumulators in the GEMM epilogue (gatx_projection_gemm_scores): no
+        # second read of Wh; flops counted as the 2NH extra columns of x W_aug^T
+        out.append(("gemm", 4 * (N * F_in + (Dp + H2) * F_in + N * Dp + N * H2),
+                    2 * N * F_in * (NH * F + H2)))
     else:
         out.append(("gemm", 4 * (N * F_in + Dp * F_in + N * Dp), 2 * N * F_in * NH * F))
         out.append(("node_scores", 4 * (N * Dp + N * H2), 2 * N * Dp * H2))
     out += [mx,
             ("edge_forward", 4 * ((N + 1) + E2 + N * H2 + gath + N * NH + N * oc + N * r), 0),
-            alpha]
+            *alpha]
     return out
+
+
+def layer_backward_dataflow(N, E2, F_in, NH, F, concat, elu, need_x, fold_resid=False):
+    """Per-kernel COMPULSORY bytes and flops of one gatx layer backward, following the dataflow
+    gatx.functional.layer_backward runs (the closed-form autograd of models/gat_layer.py:64-135,
+    SURVEY.md §8a a14). Phase names are the KernelTimer records the backward makes, so each
+    record can be priced. Gathered rows (Wh, go) count once per node while the gathered matrix
+    fits the 256 MB MALL, else once per edge; every other array once. The reassociated first layer
+    whose input needs no gradient (the model input) takes _reassoc_backward's dataflow.
+    fold_resid: the identity skip's gradient accumulated by the g_x GEMM (reads g_x once more).
+    A folded Linear skip (PATTERN) is not modelled. Returns [(phase, bytes, flops)]."""
+    from gatx.functional import LayerShape, use_reassociation
+    sh = LayerShape(NH, F, F_in, concat, False)
+    H2, Fp, Dp = 2 * NH, sh.Fp, sh.Dp
+    oc = sh.out_cols
+    go_w = Dp if concat else Fp
+    g_out = 4 * N * oc * (2 if elu else 1)            # g_out (+ out for ELU's derivative)
+    csr = 4 * ((N + 1) + 2 * E2)                      # rowptr / col / perm (or the transpose's)
+    soft = 4 * (N * H2 + N * NH)                      # S and den
+    if use_reassociation(sh) and not need_x:
+        Fin_p = _r4(F_in)
+        xg = N * Fin_p if N * Fin_p * 4 <= MALL_BYTES else E2 * Fin_p
+        return [
+            ("bwd_prepare_go", g_out + 4 * N * Dp, 0),
+            ("bwd_gemm_gz", 4 * (N * Dp + NH * F * Fin_p + N * NH * Fin_p),
+             2 * N * Fin_p * F * NH),
+            ("bwd_edge_dst", csr + soft + 4 * (N * NH * Fin_p + xg + NH * E2 + 2 * N * NH), 0),
+            ("bwd_src_scores", 4 * ((N + 1) + E2 + NH * E2 + N * NH), 0),
+            ("bwd_max", 4 * N * NH, 0),
+            ("bwd_gemm_gw_z", 4 * (N * Dp + N * NH * Fin_p + NH * F * F_in),
+             2 * NH * F * F_in * N),
+            ("bwd_gemm_gs", 4 * (N * H2 + N * F_in + H2 * F_in), 2 * H2 * F_in * N),
+            ("bwd_weight_grads", 4 * ((sh.K_aug + NH * F) * F_in + 2 * NH * NH * 2 * F), 0),
+        ]
+    KC = sh.K_aug
+    ldg = _r4(KC)
+    wh = N * Dp if N * Dp * 4 <= MALL_BYTES else E2 * Dp
+    gog = N * go_w if N * go_w * 4 <= MALL_BYTES else E2 * go_w
+    out = [
+        # (an identity skip's gradient is go itself: no extra array)
+        ("bwd_prepare_go", g_out + 4 * N * go_w, 0),
+        # g_alpha' per edge from go[n] . Wh[src], softmax backward: g_raw (NH x E2), g_s_dst
+        ("bwd_edge_dst", csr + soft + 4 * (N * go_w + wh + NH * E2 + 2 * N * NH), 0),
+        # message gradient sum alpha~ go[dst] and g_s_src, one G_aug row per source
+        ("bwd_edge_src", csr + soft + 4 * (gog + NH * E2 + N * (Dp + NH)), 0),
+        ("bwd_max", 4 * N * NH, 0),
+    ]
+    if need_x:
+        out.append(("bwd_gemm_gx", 4 * (N * ldg + 2 * KC * F_in + N * F_in
+                                        + (N * F_in if fold_resid else 0)),
+                    2 * N * F_in * KC))
+    out += [("bwd_gemm_gw", 4 * (N * ldg + N * F_in + KC * F_in), 2 * KC * F_in * N),
+            ("bwd_weight_grads", 4 * ((KC + NH * F) * F_in + 2 * NH * NH * 2 * F), 0)]
+    return out
+
+
+def graph_transpose_bytes(E2, N):
+    """The backward's source-ordered CSR (graph_transpose): reads col / rowidx / perm, writes
+    srowptr, scol, seid."""
+    return 12 * E2 + 12 * E2 + 4 * (N + 1)
+
+
+def train_step_dataflow(cfg, N, E, E2, n_params, build_graph=True):
+    """Per-kernel compulsory bytes and flops of one PPI_GAT / PatternGAT-style training step as
+    bench.py runs it: graph build (+ the backward's transpose), the forward with alpha (training
+    forwards write it), the loss (fused BCE + its scaling backward), calc_attention_norm over the
+    layers' alphas, the backward of every layer (the first layer's input needs no gradient), and
+    the fused Adam update (param, grad, exp_avg, exp_avg_sq: 4 reads + 3 writes of 4 B per
+    parameter). Returns [(phase, bytes, flops)]."""
+    dims = layer_dims(cfg)
+    L = len(dims)
+    flows = []
+    if build_graph:
+        flows.append(("graph_build", graph_build_bytes(E, E2, N), 0))
+        flows.append(("graph_transpose", graph_transpose_bytes(E2, N), 0))
+    for i, (fin, nh, f, cc) in enumerate(dims):
+        flows += layer_dataflow(N, E2, fin, nh, f, cc, cfg["add_skip_connection"][i])
+    n_out = N * cfg["num_classes"]
+    flows += [("bce", 12 * n_out, 0), ("bce_bwd", 8 * n_out, 0)]
+    for (_, nh, _, _) in dims:   # alpha, the int64 destinations, rowptr
+        flows.append(("attn_norm", 4 * E2 * nh + 8 * E2 + 4 * (N + 1), 0))
+    for i, (fin, nh, f, cc) in enumerate(dims):
+        skip = cfg["add_skip_connection"][i]
+        ident = skip and fin == nh * f   # identity skip: folded into the g_x GEMM's accumulate
+        flows += layer_backward_dataflow(N, E2, fin, nh, f, cc, elu=(i != L - 1),
+                                         need_x=i > 0, fold_resid=ident)
+    flows.append(("adam", 28 * n_params, 0))
+    return flows
 
 
 def edge_pricer(dims, flows):
@@ -405,6 +515,96 @@ def roofline_objects(summ, edge_bytes, pm, n_instr, pm_path="", gather_E2=None):
     return ordered
 
 
+# what each training-step record is priced as: the KernelTimer phase -> its bound and the rocprof
+# kernel-name prefix(es) its launches carry (for `traffic`)
+TRAIN_PHASES = {
+    "gemm": ("mfma", None),
+    "bwd_gemm_gx": ("mfma", "gemm_x3_kernel<true, true, true, 1,"),
+    "bwd_gemm_gw": ("mfma", "gemm_x3_kernel<false, false, true, 2, 1,"),
+    "edge_forward": ("hbm", "edge_forward_kernel"),
+    "bwd_edge_dst": ("hbm", "edge_bwd_dst"),
+    "bwd_edge_src": ("hbm", "edge_bwd_src"),
+    "bwd_prepare_go": ("hbm", "prepare_go"),
+}
+
+
+def gemm_phase_roof(phase):
+    """(arithmetic, peak TF/s) of the GEMM a training record runs: the forward projection and g_x
+    (both operands k-contiguous) in the active mode; the weight gradient G_aug^T x (row-contiguous
+    operands) in the arithmetic the library reports for that layout."""
+    from gatx import _lib
+    gr = gemm_roof()
+    if phase == "bwd_gemm_gw":
+        mode = _lib.lib.gatx_gemm_layout_mode(0, 0)
+        return {2: "f16x3", 1: "x3", 0: "f32"}[mode], {
+            2: BF16_MFMA_PEAK_TFS / F16X3_PRODUCTS, 1: BF16_MFMA_PEAK_TFS / X3_PRODUCTS,
+            0: FP32_MFMA_PEAK_TFS}[mode]
+    return gr["mode"], gr["peak"]
+
+
+def record_pricer(dims, flows, cfg):
+    """price(phase, i, info) -> (bytes, flops) of the i-th record of `phase` in a training step:
+    forward records from layer_dataflow (the projection GEMM by its flops; edge records by layer
+    index), backward records from layer_backward_dataflow at the record's own shape (the info
+    tuple functional.layer_backward records: N, E2, F_in, NH, F, concat, C, elu, reassoc[, fold])."""
+    edge = edge_pricer(dims, flows)
+
+    def price(phase, i, info):
+        if phase == "gemm":
+            n, _, fin, nh, f = info
+            return 0, 2.0 * n * fin * (nh * f + 2 * nh)
+        if phase == "edge_forward":
+            return edge(i, info), 0
+        N, E2, fin, nh, f, cc, _, elu, reassoc = info[:9]
+        fold = bool(info[9]) if len(info) > 9 else False
+        for k, b, fl in layer_backward_dataflow(N, E2, fin, nh, f, cc, elu, need_x=not reassoc,
+                                                fold_resid=fold):
+            if k == phase:
+                return b, fl
+        raise KeyError(f"{phase} record {info} not in the backward dataflow")
+    return price
+
+
+def train_roofline_objects(summ, price, pm, n_instr, pm_path=""):
+    """Roofline objects of a training step: every TRAIN_PHASES phase with records, priced per
+    record (price(phase, i, info)) and timed by its HIP events; the two with the most time per
+    step come first. GEMM phases are MFMA-bound (flops / the peak of the arithmetic they run),
+    the others HBM-bound (compulsory bytes / 8 TB/s). `traffic` = PMC fabric bytes per record of
+    the phase's kernels (tools/pmc_summary.py window of a train run), when a summary is given."""
+    objs = []
+    for phase, (bound, prefix) in TRAIN_PHASES.items():
+        recs = summ.get(phase, [])
+        if not recs:
+            continue
+        ms_ = sum(t for _, t in recs)
+        priced = [price(phase, i, info) for i, (info, _) in enumerate(recs)]
+        per_step = len(recs) / n_instr
+        if bound == "mfma":
+            fl = sum(f for _, f in priced)
+            tfs = fl / (ms_ * 1e-3) / 1e12
+            mode, peak = gemm_phase_roof(phase)
+            o = {"bound": "mfma", "kernel": f"{phase} ({mode} arithmetic)", "achieved": round(tfs, 2),
+                 "peak": round(peak, 1), "unit": "TFLOP/s", "frac": round(tfs / peak, 4),
+                 "traffic": None, "gemm_mode": mode, "flops_per_launch": fl / len(recs)}
+        else:
+            by = sum(b for b, _ in priced)
+            gbs = by / (ms_ * 1e-3) / 1e9
+            o = {"bound": "hbm", "kernel": phase, "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                 "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                 "bytes_per_launch": by / len(recs)}
+        o.update({"avg_launch_ms": ms_ / len(recs), "records_per_step": per_step,
+                  "ms_per_step": ms_ / n_instr})
+        if pm is not None and prefix:
+            from pmc_summary import prefix_bytes_per_step
+            b = prefix_bytes_per_step(pm, prefix)
+            if b > 0:
+                o["traffic"] = b / per_step
+                o["traffic_source"] = (f"{os.path.relpath(pm_path, ROOT) if pm_path else ''} "
+                                       f"({pm.get('source', '')}), kernels {prefix}*")
+        objs.append(o)
+    return sorted(objs, key=lambda o: -o["ms_per_step"])
+
+
 def run_rmat(args, world, rank, dev):
     """BASELINE config 5: one GATLayer (F_in 512 -> 8 heads x 64, concat, self-loops) forward on
     a synthetic R-MAT graph (1e7 nodes, exactly 1.6e8 edges), eval mode, CSR built per step. One
@@ -461,7 +661,7 @@ def run_rmat(args, world, rank, dev):
         "value": round(E2 * world / step_s, 1), "unit": "layer-edges/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(step_s * 1e3, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": gemm_dtype(),
         "data": "synthetic R-MAT (a,b,c,d)=(0.57,0.19,0.19,0.05), rejected ids redrawn, ids "
                 "permuted, x ~ N(0,1), xavier weights",
         "config": {"workload": f"RMAT {N} nodes / {E} edges, GATLayer 512 -> 8x64 concat, "
@@ -640,6 +840,9 @@ def main():
         w_main, w_norm = count_weights([n_local, e_local],
                                        device=dev if backend == "nccl" else "cpu")
 
+    from gatx.functional import _span
+    n_params = sum(p.numel() for p in model.parameters())
+
     def _w(t, w):   # no extra launch for the single-rank weight 1
         return t if w == 1.0 else t * w
 
@@ -669,12 +872,13 @@ def main():
         loss.backward()
         if reducer is not None:
             reducer.finish()
-        opt.step()
+        with _span("adam", (n_params,)):
+            opt.step()
         return out
 
     eager_step = step
+    from gatx.capture import CapturedStep
     if use_graph:
-        from gatx.capture import CapturedStep
         step = CapturedStep(eager_step)
     for _ in range(args.warmup):
         step()
@@ -683,39 +887,76 @@ def main():
     N = b.num_nodes
     dims = layer_dims(cfg)
 
+    from gatx import _lib
+    fb = torch.zeros(1, dtype=torch.int64, device=dev)
+    _lib.call("gatx_gemm_fallback_read", _lib.ptr(fb), 1, _lib.stream())   # reset the counter
     elapsed, summ, n_instr = run_timed(step, args.steps, world, dev,
                                        eager_step if use_graph else None)
-    clear_graph_cache()
-    E2 = graph_cache.get(ei, N, True).num_edges
+    _lib.call("gatx_gemm_fallback_read", _lib.ptr(fb), 1, _lib.stream())
+    fallback_tiles = int(fb.item())
     step_s = elapsed / args.steps
     ms = step_s * 1e3
+
+    # the inference forward defers alpha to its first read (gatx.functional.LazyAlpha); the
+    # reference writes it in every forward (models/gat_layer.py:106-110), as every training
+    # forward_and_return_attention does: time the forward that way too
+    alpha_eager_ms = None
+    deferred = args.mode == "fwd" and os.environ.get("GATX_DEFER_ALPHA", "1") != "0"
+    if deferred and world == 1:
+        from gatx import functional as gf
+        os.environ["GATX_DEFER_ALPHA"] = "0"
+        gf.reset_tuning()
+        st = CapturedStep(eager_step) if use_graph else eager_step
+        for _ in range(args.warmup):
+            st()
+        el, _, _ = run_timed(st, args.steps, world, dev, eager_step if use_graph else None)
+        alpha_eager_ms = el / args.steps * 1e3
+        os.environ["GATX_DEFER_ALPHA"] = "1"
+        gf.reset_tuning()
+        del st
+
+    clear_graph_cache()
+    E2 = graph_cache.get(ei, N, True).num_edges
     layer_edges = len(dims) * E2
     value = layer_edges * world / step_s
 
     # honest accounting: unique bytes of the dataflow actually run, priced against HBM
     peak = gemm_roof()["peak"] * 1e12
-    flows = [layer_dataflow(N, E2, fin, nh, f, cc, cfg["add_skip_connection"][i])
+    flows = [layer_dataflow(N, E2, fin, nh, f, cc, cfg["add_skip_connection"][i],
+                            alpha=not deferred)
              for i, (fin, nh, f, cc) in enumerate(dims)]
     gb = graph_build_bytes(b.num_edges, E2, N) if not args.cached_graph else 0
-    uniq = sum(bb for fl in flows for _, bb, _ in fl) + gb
-    t_roof = sum(max(bb / (HBM_PEAK_GBS * 1e9), ff / peak) for fl in flows for _, bb, ff in fl) \
-        + gb / (HBM_PEAK_GBS * 1e9)
+    if args.mode == "train":
+        # the whole training step: forward (alpha eager), loss, attention norm, backward, Adam
+        tflow = train_step_dataflow(cfg, N, b.num_edges, E2, n_params,
+                                    build_graph=not args.cached_graph)
+        uniq = sum(bb for _, bb, _ in tflow)
+        t_roof = sum(max(bb / (HBM_PEAK_GBS * 1e9), ff / peak) for _, bb, ff in tflow)
+    else:
+        uniq = sum(bb for fl in flows for _, bb, _ in fl) + gb
+        t_roof = sum(max(bb / (HBM_PEAK_GBS * 1e9), ff / peak) for fl in flows
+                     for _, bb, ff in fl) + gb / (HBM_PEAK_GBS * 1e9)
     surv = [survey_bytes(N, E2, fin, nh, f, cc) for (fin, nh, f, cc) in dims]
     l2_gather = sum(bg + be for bg, _, be in surv)
 
     edge_unique = edge_pricer(dims, flows)
-    pmc_path = os.path.join(ROOT, "profiles",
-                            "pmc_latest.json" if (ds == "PPI" and args.mode == "fwd"
-                                                  and args.graphs == 20) else "_none_")
+    pm_name = "_none_"
+    if ds == "PPI" and args.graphs == 20:
+        pm_name = "pmc_latest.json" if args.mode == "fwd" else "pmc_train.json"
+    pmc_path = os.path.join(ROOT, "profiles", pm_name)
     pm = load_pmc(pmc_path)
-    ordered = roofline_objects(summ, edge_unique, pm, n_instr, pmc_path, gather_E2=E2)
+    if args.mode == "train" and ds == "PPI":
+        ordered = train_roofline_objects(summ, record_pricer(dims, flows, cfg), pm, n_instr,
+                                         pmc_path)
+    else:
+        ordered = roofline_objects(summ, edge_unique, pm, n_instr, pmc_path, gather_E2=E2)
 
     result = {
         "metric": f"GAT-layer edges/sec + achieved HBM GB/s, {ds} {len(dims)}-layer fwd"
                   + ("" if args.mode == "fwd" else " (+bwd, train step)"),
         "value": round(value, 1), "unit": "layer-edges/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "scaling": "weak", "vs_baseline": None, "dtype": gemm_dtype(),
         "data": f"synthetic {ds}-shaped graphs (uniform random edges, N(0,1) features), xavier "
                 "weights",
         "config": {"workload": f"{ds} {len(dims)}-layer GAT {args.mode} ("
@@ -730,16 +971,27 @@ def main():
                              if use_graph else "eager",
                    "wiring": ("gatx (skip / ELU / dropout fused into the layers)"
                               if args.wiring == "gatx" else
-                              "reference GATModel.forward around gatx GATLayers (drop-in)")},
+                              "reference GATModel.forward around gatx GATLayers (drop-in)"),
+                   "alpha": ("deferred: the inference forward computes alpha on the first read "
+                             "of normalised_attention_coeffs (not read in this step; see "
+                             "ms_per_step_alpha_eager)" if deferred else
+                             "eager: every layer writes alpha in the forward")},
+        "ms_per_step_alpha_eager": (round(alpha_eager_ms, 4) if alpha_eager_ms is not None
+                                    else None),
+        "gemm_f16x3_fallback_tiles_per_step": fallback_tiles / args.steps,
         "unique_GBps": round(uniq / step_s / 1e9, 1),
-        # forward dataflow only: not defined for a train step (its backward is not priced)
-        "roofline_time_frac": round(t_roof / step_s, 4) if args.mode == "fwd" else None,
+        "roofline_time_frac": (round(t_roof / step_s, 4) if ds == "PPI" or args.mode == "fwd"
+                               else None),
         "roofline_time_basis": ("sum over the forward's kernels of max(unique bytes / 8 TB/s, "
                                 "flops / GEMM peak) + graph build bytes / 8 TB/s, over step time"
-                                if args.mode == "fwd" else "omitted: only the forward dataflow "
-                                "is priced"),
+                                if args.mode == "fwd" else
+                                "sum over the training step's kernels (bench.train_step_dataflow:"
+                                " graph build + transpose, forward with alpha, BCE, attention "
+                                "norm, every layer's backward, Adam) of max(unique bytes / 8 TB/s,"
+                                " flops / GEMM peak), over step time"
+                                if ds == "PPI" else "omitted: only the PPI step is priced"),
         "l2_gather_GBps": round(l2_gather / step_s / 1e9, 1),
-        "hbm_measured": pmc_step_bytes(pm, ms, pmc_path) if args.mode == "fwd" else None,
+        "hbm_measured": pmc_step_bytes(pm, ms, pmc_path),
         "roofline": ordered[0] if ordered else None,
         "roofline_other": ordered[1] if len(ordered) > 1 else None,
         "kernels": kernel_summary(summ, n_instr),

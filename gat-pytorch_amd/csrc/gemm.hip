@@ -621,6 +621,17 @@ extern "C" void gatx_set_gemm_mode(int mode) { g_gemm_mode = mode <= 0 ? 0 : mod
 
 extern "C" int gatx_get_gemm_mode(void) { return gemm_mode(); }
 
+extern "C" int gatx_gemm_layout_mode(int a_kc, int b_kc) {
+  // f16x3 needs k-contiguous operand pairs (gemm_x3.hip f16_mainloop); other layouts run x3
+  const int m = gemm_mode();
+  return m == 2 && !(a_kc && b_kc) ? 1 : m;
+}
+
+extern "C" int gatx_gemm_fallback_read(uint64_t* dst, int reset, gatx_stream_t stream) {
+  GATX_REQUIRE(dst != nullptr, "gatx_gemm_fallback_read: dst is NULL");
+  return read_f16_fallbacks((unsigned long long*)dst, reset, (hipStream_t)stream);
+}
+
 extern "C" size_t gatx_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K) {
   int64_t rem = 0;
   const Kind kd = choose_kind(M, N);

@@ -283,6 +283,8 @@ int launch_gemm_x3(const gk::GemmArgs& g, bool a_kc, bool b_kc, int batch, int t
 bool gemm_smallk_fits(int64_t M, int64_t N, int64_t K, bool a_kc, bool b_kc, int accumulate,
                       bool resid);
 int launch_gemm_smallk(const gk::GemmArgs& g, int batch, hipStream_t stream);
+// gemm_x3.hip: copy (and optionally zero) the f16x3 -> x3 fallback tile counter
+int read_f16_fallbacks(unsigned long long* dst, int reset, hipStream_t stream);
 // the x3 kernel instance whose occupancy sizes tail / split-K decisions
 const void* gemm_x3_occupancy_fn(int cfg);   // cfg 0: 128 x 128 tiles, 1: 256 x 256
 

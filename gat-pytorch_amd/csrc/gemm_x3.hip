@@ -343,13 +343,17 @@ __device__ inline void x3_mainloop(const GemmArgs& g, const float* __restrict__ 
 
 // ---------------------------------------------------------------------------------------------
 // fp32 GEMM as a two-way fp16 split ("f16x3"): x = h + l 2^-11 with h = fp16_rn(x) and
-// l = fp16_rn(2^11 (x - h)) (11 + 11 significand bits; |x - h - l 2^-11| <= 2^-23 |x|, and the
-// 2^11 keeps l a normal fp16 wherever x is), and the product as three fp16 MFMA products, all
-// carrying the same factor 2^11:
-//     2^11 a b ~= (64 a_h)(32 b_h) + a_h b_l + a_l b_h        (dropped: a_l b_l 2^-22 <= 2^-24 |ab|)
+// l = fp16_rn(2^11 (x - h)) (11 + 11 significand bits: |x - h| <= 2^-11 |x|, and rounding l to
+// fp16 leaves |x - h - l 2^-11| <= 2^-22 |x|; the 2^11 keeps l a normal fp16 wherever x is), and
+// the product as three fp16 MFMA products, all carrying the same factor 2^11:
+//     2^11 a b ~= (64 a_h)(32 b_h) + a_h b_l + a_l b_h        (dropped: a_l b_l 2^-22 <= 2^-22 |ab|)
+// So each product carries a relative error of a few 2^-22 — not one fp32 rounding (2^-24). What
+// makes the result as accurate as an fp32 GEMM is the accumulation: the fp16 products are exact
+// in the f32 accumulator, whose K-long summation error dominates the per-product terms;
+// tests/test_gpu_layer.py::test_gemm_x3_split_accuracy holds the kernel to <= 1.25x the exact
+// fp32-MFMA kernel's error against fp64 (tests/test_f16x3_numerics.py: the 2^-22 split bound).
 // The 64 / 32 factors of the first product are applied to the hi fragments in registers
-// (v_pk_mul_f16, exact); fp16 products are exact in the f32 accumulator, which is scaled by 2^-11
-// (exact) at the end: fp32-GEMM accuracy (tests/test_gpu_layer.py against fp64) at 3 MFMA
+// (v_pk_mul_f16, exact) and the accumulator is scaled by 2^-11 (exact) at the end: 3 MFMA
 // products per step instead of the bf16 split's 6, and two LDS planes per operand instead of 3.
 // Row scaling: every A row (an output row: activations, or a gradient's ~1e-7 rows) is multiplied
 // by a power of two chosen from its max |x| in the workgroup's first K-tile (to [2^7, 2^8)),
@@ -366,6 +370,18 @@ __device__ inline void x3_mainloop(const GemmArgs& g, const float* __restrict__ 
 // so accuracy never depends on the operands' magnitudes. Used for k-contiguous A and B (the
 // forward projection's layout); the other layouts run x3.
 constexpr float kF16LimA = 1023.f, kF16LimB = 2047.f, kF16Tiny = 0x1p-13f;
+
+// Workgroups that tripped the range check and recomputed their tile as x3 (~1.5x the tile's
+// cost), counted since the last gatx_gemm_fallback_read with reset: a perf cliff on operands out
+// of the fp16 range (e.g. a trained weight row below 2^-13) shows up here, not only in timings.
+__device__ unsigned long long g_f16_fallback_tiles = 0;
+
+__global__ void fallback_read_kernel(unsigned long long* dst, int reset) {
+  if (threadIdx.x == 0) {
+    dst[0] = __hip_atomic_load(&g_f16_fallback_tiles, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (reset) __hip_atomic_store(&g_f16_fallback_tiles, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
 
 __device__ inline bool f16_row_bad(float m, float lim) {
   m = fmaxf(m, __shfl_xor(m, 1));
@@ -771,6 +787,8 @@ __global__ void __launch_bounds__(X3Cfg<CFG>::NT, X3Cfg<CFG>::MINB) gemm_x3_kern
               : f16_mainloop<A_KC, B_KC, true, CFG, SCALE>(g, A, B, m0, n0, kb, K, nk, smem, wm,
                                                             wn, lane, acc);
       x3 = __syncthreads_or(bad);   // the workgroup's tiles out of fp16 range: redo as x3
+      if (x3 && threadIdx.x == 0)
+        __hip_atomic_fetch_add(&g_f16_fallback_tiles, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       // undo 2^11 and the row / column scales: lane -> row, register 4j + i -> column (the
       // transposed product's layout, write_tile_t)
       constexpr int STAGE16 = 2 * 2 * (C::TBM + C::TBN) * C::BK;
@@ -854,6 +872,12 @@ int launch_gemm_x3(const gk::GemmArgs& g, bool a_kc, bool b_kc, int batch, int t
 #undef GATX_X3_T
 #undef GATX_X3_V
   GATX_LAUNCH_CHECK("gemm_x3");
+  return 0;
+}
+
+int read_f16_fallbacks(unsigned long long* dst, int reset, hipStream_t stream) {
+  fallback_read_kernel<<<1, 64, 0, stream>>>(dst, reset);
+  GATX_LAUNCH_CHECK("gatx_gemm_fallback_read");
   return 0;
 }
 

@@ -84,6 +84,8 @@ SIGNATURES = {
     "gatx_set_debug": (None, [c_i]),
     "gatx_set_gemm_mode": (None, [c_i]),
     "gatx_get_gemm_mode": (c_i, []),
+    "gatx_gemm_fallback_read": (c_i, [P, c_i, P]),
+    "gatx_gemm_layout_mode": (c_i, [c_i, c_i]),
     "gatx_gemm_splitk_workspace_bytes": (c_sz, [c_i64, c_i64, c_i64]),
     "gatx_gemm_f32_splitk": (c_i, [c_i64, c_i64, c_i64, P, c_i64, c_i64, P, c_i64, c_i64, P, c_i64,
                                    c_i, P, c_sz, P]),

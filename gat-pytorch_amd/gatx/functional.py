@@ -383,15 +383,30 @@ class LazyAlpha:
     when `normalised_attention_coeffs` is first read, from the softmax state the forward left (the
     node scores S, the global max and the denominators, all kept alive by this object) — the
     same kernel on the same inputs, so the same values as an eager forward. Training forwards
-    stay eager: the backward's max() gradient needs the argmax entries that pass records."""
+    stay eager: the backward's max() gradient needs the argmax entries that pass records.
 
-    __slots__ = ("graph", "S", "M_ord", "den", "sh", "argmax")
+    Streams: the forward's stream is remembered; a read from another stream first makes that
+    stream wait for the forward's (and marks the saved buffers as used there, so the caching
+    allocator cannot hand them out before the pass has read them). The pass reads edge_index'
+    — with add_self_loops=False that is the caller's own edge_index — so edge_index must not be
+    modified in place before alpha has been read (the reference has no such window: it writes
+    alpha inside the forward)."""
+
+    __slots__ = ("graph", "S", "M_ord", "den", "sh", "argmax", "fwd_stream")
 
     def __init__(self, graph, S, M_ord, den, sh, argmax):
         self.graph, self.S, self.M_ord, self.den, self.sh, self.argmax = \
             graph, S, M_ord, den, sh, argmax
+        self.fwd_stream = torch.cuda.current_stream(S.device)
 
     def materialize(self) -> torch.Tensor:
+        cur = torch.cuda.current_stream(self.S.device)
+        if cur != self.fwd_stream:
+            cur.wait_stream(self.fwd_stream)
+            ei = self.graph._ei_flat if self.graph._ei_flat is not None else self.graph.source
+            for t in (self.S, self.M_ord, self.den, self.argmax, ei, self.graph.rowptr,
+                      self.graph.perm, self.graph.meta):
+                t.record_stream(cur)
         alpha = torch.empty((max(self.graph.edge_bound, 1), self.sh.NH), dtype=torch.float32,
                             device=self.S.device)
         with _span("attention_alpha", (self.graph.edge_bound, self.sh.NH)):
@@ -557,60 +572,72 @@ def layer_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShape, 
         g_pre = go if (sh.concat and sh.F % 4 == 0) else torch.empty((N, sh.out_cols), **f32)
         pre_p = ptr(g_pre)
     out_p = saved.get("out_p", 0.0)
-    call("gatx_prepare_go_ex", ptr(g_out), ptr(out) if elu else None, N, sh.NH, sh.F,
-         int(sh.concat), int(elu), ptr(go), pre_p, pre_ld, out_p,
-         ptr(saved["out_seed"]) if out_p > 0 else None, s)
+    # KernelTimer record info (bench.py prices each backward record from it)
+    binfo = (N, E2, sh.F_in, sh.NH, sh.F, sh.concat, C, bool(elu), False)
+    with _span("bwd_prepare_go", binfo):
+        call("gatx_prepare_go_ex", ptr(g_out), ptr(out) if elu else None, N, sh.NH, sh.F,
+             int(sh.concat), int(elu), ptr(go), pre_p, pre_ld, out_p,
+             ptr(saved["out_seed"]) if out_p > 0 else None, s)
     g_raw = g_corr = None
     if not sh.const:
         g_raw = torch.empty((sh.NH, max(E2, 1)), **f32)
         gsd = torch.empty((N, sh.NH), **f32)
-        call("gatx_edge_backward_dst_hubs", ptr(saved["Wh"]), sh.Dp, sh.Fp, ptr(saved["S"]),
+        with _span("bwd_edge_dst", binfo):
+            call("gatx_edge_backward_dst_hubs", ptr(saved["Wh"]), sh.Dp, sh.Fp, ptr(saved["S"]),
              ptr(saved["M_ord"]), ptr(saved["den"]), ptr(graph.rowptr), ptr(graph.col),
-             ptr(graph.perm), N, E2, sh.NH, sh.F, ptr(go), sh.Dp if sh.concat else sh.Fp,
-             sh.Fp if sh.concat else 0, float(p), ptr(seed),
-             ptr(g_alpha.contiguous()) if g_alpha is not None else None, ptr(g_raw), ptr(gsd),
-             ptr(G_aug), ldg, sh.Dp, *bwd_hub_args(graph, sh.NH, sh.F, dev, False), s)
-    call("gatx_edge_backward_src_hubs", ptr(saved["S"]), ptr(saved["M_ord"]), ptr(saved["den"]),
-         ptr(graph.srowptr), ptr(graph.scol), ptr(graph.seid), ptr(graph.perm), N, E2, sh.NH,
-         sh.F, int(sh.concat), int(sh.const), float(p), ptr(seed), ptr(go), ptr(g_raw), None,
-         ptr(G_aug), ldg, *bwd_hub_args(graph, sh.NH, sh.F, dev, True), s)
+                 ptr(graph.perm), N, E2, sh.NH, sh.F, ptr(go), sh.Dp if sh.concat else sh.Fp,
+                 sh.Fp if sh.concat else 0, float(p), ptr(seed),
+                 ptr(g_alpha.contiguous()) if g_alpha is not None else None, ptr(g_raw),
+                 ptr(gsd), ptr(G_aug), ldg, sh.Dp, *bwd_hub_args(graph, sh.NH, sh.F, dev, False),
+                 s)
+    with _span("bwd_edge_src", binfo):
+        call("gatx_edge_backward_src_hubs", ptr(saved["S"]), ptr(saved["M_ord"]),
+             ptr(saved["den"]), ptr(graph.srowptr), ptr(graph.scol), ptr(graph.seid),
+             ptr(graph.perm), N, E2, sh.NH, sh.F, int(sh.concat), int(sh.const), float(p),
+             ptr(seed), ptr(go), ptr(g_raw), None, ptr(G_aug), ldg,
+             *bwd_hub_args(graph, sh.NH, sh.F, dev, True), s)
     if not sh.const:   # max()'s share, added into both logit-gradient columns of G_aug
         mws = torch.empty(lib.gatx_max_backward_workspace_bytes(), dtype=torch.uint8, device=dev)
-        call("gatx_max_backward", ptr(saved["argmax"]), ptr(gsd), ptr(saved["S"]),
-             ptr(saved["M_ord"]), ptr(graph.col), ptr(graph.rowidx), N, E2, graph.e2_ptr, sh.NH,
-             None, ptr(G_aug), ldg, sh.Dp, ptr(mws), s)
+        with _span("bwd_max", binfo):
+            call("gatx_max_backward", ptr(saved["argmax"]), ptr(gsd), ptr(saved["S"]),
+                 ptr(saved["M_ord"]), ptr(graph.col), ptr(graph.rowidx), N, E2, graph.e2_ptr,
+                 sh.NH, None, ptr(G_aug), ldg, sh.Dp, ptr(mws), s)
     g_x = g_W = g_a = g_bias = None
     W_aug = saved["W_aug"]
     KC = sh.K_aug + C   # GEMM depth / rows over [g_Wh | g_s | g_skip]
     if need_bias and bias is not None:   # before g_pre may become g_x's accumulator
         g_bias = torch.empty_like(bias)
         src_p, src_ld = (pre_p, pre_ld) if elu else (ptr(g_out), sh.out_cols)
-        call("gatx_colsum", src_p, N, sh.out_cols, src_ld, ptr(g_bias), s)
+        with _span("bwd_colsum", binfo):
+            call("gatx_colsum", src_p, N, sh.out_cols, src_ld, ptr(g_bias), s)
     fold = resid_is_x and need_x and g_pre is not None
     if need_x:
         g_x = g_pre if fold else torch.empty((N, sh.F_in), **f32)
-        if N * sh.F_in * KC >= (1 << 27):
-            # W_aug^T (F_in x K_aug, 4 MB at PPI): both GEMM operands k-contiguous (the
-            # n-contiguous B staging of W_aug as stored ran this product ~25% slower)
-            W_augT = torch.empty((sh.F_in, ldg), **f32)
-            call("gatx_transpose_f32", KC, sh.F_in, ptr(W_aug), sh.F_in, ptr(W_augT), ldg, s)
-            call("gatx_gemm_f32", N, sh.F_in, KC, ptr(G_aug), ldg, 1, ptr(W_augT), 1,
-                 ldg, ptr(g_x), sh.F_in, sh.F_in, None, 0, int(fold),
-                 *gemm_workspace(N, sh.F_in, KC, dev), s)
-        else:   # small layers are launch-bound: read W_aug as stored (no transpose launch)
-            call("gatx_gemm_f32", N, sh.F_in, KC, ptr(G_aug), ldg, 1, ptr(W_aug), sh.F_in,
-                 1, ptr(g_x), sh.F_in, sh.F_in, None, 0, int(fold),
-                 *gemm_workspace(N, sh.F_in, KC, dev), s)
+        with _span("bwd_gemm_gx", binfo + (bool(fold),)):
+            if N * sh.F_in * KC >= (1 << 27):
+                # W_aug^T (F_in x K_aug, 4 MB at PPI): both GEMM operands k-contiguous (the
+                # n-contiguous B staging of W_aug as stored ran this product ~25% slower)
+                W_augT = torch.empty((sh.F_in, ldg), **f32)
+                call("gatx_transpose_f32", KC, sh.F_in, ptr(W_aug), sh.F_in, ptr(W_augT), ldg, s)
+                call("gatx_gemm_f32", N, sh.F_in, KC, ptr(G_aug), ldg, 1, ptr(W_augT), 1,
+                     ldg, ptr(g_x), sh.F_in, sh.F_in, None, 0, int(fold),
+                     *gemm_workspace(N, sh.F_in, KC, dev), s)
+            else:   # small layers are launch-bound: read W_aug as stored (no transpose launch)
+                call("gatx_gemm_f32", N, sh.F_in, KC, ptr(G_aug), ldg, 1, ptr(W_aug), sh.F_in,
+                     1, ptr(g_x), sh.F_in, sh.F_in, None, 0, int(fold),
+                     *gemm_workspace(N, sh.F_in, KC, dev), s)
     if need_W or need_a or need_skip:
         gW_aug = torch.empty((KC, sh.F_in), **f32)
         ws_bytes = lib.gatx_gemm_splitk_workspace_bytes(KC, sh.F_in, N)
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-        call("gatx_gemm_f32_splitk", KC, sh.F_in, N, ptr(G_aug), 1, ldg, ptr(x),
-             sh.F_in, 1, ptr(gW_aug), sh.F_in, 0, ptr(ws), ws_bytes, s)
+        with _span("bwd_gemm_gw", binfo):
+            call("gatx_gemm_f32_splitk", KC, sh.F_in, N, ptr(G_aug), 1, ldg, ptr(x),
+                 sh.F_in, 1, ptr(gW_aug), sh.F_in, 0, ptr(ws), ws_bytes, s)
         g_W = torch.empty_like(W)
         g_a = torch.empty_like(a) if a is not None else None
-        call("gatx_weight_grads", ptr(gW_aug), ptr(W), ptr(a), sh.NH, sh.F, sh.F_in, ptr(g_W),
-             ptr(g_a), s)
+        with _span("bwd_weight_grads", binfo):
+            call("gatx_weight_grads", ptr(gW_aug), ptr(W), ptr(a), sh.NH, sh.F, sh.F_in,
+                 ptr(g_W), ptr(g_a), s)
         if need_skip:
             saved["g_skip_eff"] = gW_aug[sh.K_aug:]
     g_resid = None
@@ -649,49 +676,60 @@ def _reassoc_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShap
     elif need_resid or (need_bias and elu):
         g_pre = torch.empty((N, sh.out_cols), **f32)
         pre_p = ptr(g_pre)
-    call("gatx_prepare_go_ex", ptr(g_out), ptr(out) if elu else None, N, NH, F, 1, int(elu),
-         ptr(go), pre_p, pre_ld, 0.0, None, s)
+    binfo = (N, E2, F_in, NH, F, True, C, bool(elu), True)
+    with _span("bwd_prepare_go", binfo):
+        call("gatx_prepare_go_ex", ptr(g_out), ptr(out) if elu else None, N, NH, F, 1,
+             int(elu), ptr(go), pre_p, pre_ld, 0.0, None, s)
     Wp = saved.get("Wp")    # [NH*F][Fin_p], zero tail: the forward's copy
     if Wp is None:
         Wp = padded_weight(W, Fin_p, sh.cache_weights)
     g_Z = torch.empty((N, NH * Fin_p), **f32)
-    call("gatx_gemm_f32_batched", NH, N, Fin_p, F, ptr(go), sh.Dp, 1, Fp, ptr(Wp), Fin_p, 1,
-         F * Fin_p, ptr(g_Z), NH * Fin_p, Fin_p, 0, None, 0, None, 0, 0, 0, s)
+    with _span("bwd_gemm_gz", binfo):
+        call("gatx_gemm_f32_batched", NH, N, Fin_p, F, ptr(go), sh.Dp, 1, Fp, ptr(Wp), Fin_p, 1,
+             F * Fin_p, ptr(g_Z), NH * Fin_p, Fin_p, 0, None, 0, None, 0, 0, 0, s)
     g_raw = torch.empty((NH, max(E2, 1)), **f32)
     gsd = torch.empty((N, NH), **f32)
-    call("gatx_edge_backward_dst_hubs", ptr(x_rows), Fin_p, 0, ptr(saved["S"]),
-         ptr(saved["M_ord"]), ptr(saved["den"]), ptr(graph.rowptr), ptr(graph.col),
-         ptr(graph.perm), N, E2, NH, Fin_p, ptr(g_Z), NH * Fin_p, Fin_p, float(p), ptr(seed),
-         ptr(g_alpha.contiguous()) if g_alpha is not None else None, ptr(g_raw), ptr(gsd),
-         ptr(G_s), lds, 0, *bwd_hub_args(graph, NH, Fin_p, dev, False), s)
-    call("gatx_edge_backward_src_scores", ptr(graph.srowptr), ptr(graph.seid), N, E2, NH,
-         ptr(g_raw), None, ptr(G_s), lds, 0, s)
+    with _span("bwd_edge_dst", binfo):
+        call("gatx_edge_backward_dst_hubs", ptr(x_rows), Fin_p, 0, ptr(saved["S"]),
+             ptr(saved["M_ord"]), ptr(saved["den"]), ptr(graph.rowptr), ptr(graph.col),
+             ptr(graph.perm), N, E2, NH, Fin_p, ptr(g_Z), NH * Fin_p, Fin_p, float(p), ptr(seed),
+             ptr(g_alpha.contiguous()) if g_alpha is not None else None, ptr(g_raw), ptr(gsd),
+             ptr(G_s), lds, 0, *bwd_hub_args(graph, NH, Fin_p, dev, False), s)
+    with _span("bwd_src_scores", binfo):
+        call("gatx_edge_backward_src_scores", ptr(graph.srowptr), ptr(graph.seid), N, E2, NH,
+             ptr(g_raw), None, ptr(G_s), lds, 0, s)
     mws = torch.empty(lib.gatx_max_backward_workspace_bytes(), dtype=torch.uint8, device=dev)
-    call("gatx_max_backward", ptr(saved["argmax"]), ptr(gsd), ptr(saved["S"]),
-         ptr(saved["M_ord"]), ptr(graph.col), ptr(graph.rowidx), N, E2, graph.e2_ptr, NH, None,
-         ptr(G_s), lds, 0, ptr(mws), s)
+    with _span("bwd_max", binfo):
+        call("gatx_max_backward", ptr(saved["argmax"]), ptr(gsd), ptr(saved["S"]),
+             ptr(saved["M_ord"]), ptr(graph.col), ptr(graph.rowidx), N, E2, graph.e2_ptr, NH,
+             None, ptr(G_s), lds, 0, ptr(mws), s)
     g_W = g_a = g_bias = None
     if need_W or need_a or need_skip:
         gW_aug = torch.empty((sh.K_aug + C, F_in), **f32)
         # main rows, head h at rows h*Fp.. : go_h^T (F x N) . Z_h (N x F_in)
         wb = lib.gatx_gemm_splitk_batched_workspace_bytes(NH, F, F_in, N)
         ws = torch.empty(max(wb, 1), dtype=torch.uint8, device=dev)
-        call("gatx_gemm_f32_splitk_batched", NH, F, F_in, N, ptr(go), 1, sh.Dp, Fp, ptr(Z),
-             NH * Fin_p, 1, Fin_p, ptr(gW_aug), F_in, Fp * F_in, 0, ptr(ws), wb, s)
+        with _span("bwd_gemm_gw_z", binfo):
+            call("gatx_gemm_f32_splitk_batched", NH, F, F_in, N, ptr(go), 1, sh.Dp, Fp, ptr(Z),
+                 NH * Fin_p, 1, Fin_p, ptr(gW_aug), F_in, Fp * F_in, 0, ptr(ws), wb, s)
         # score rows (+ folded skip rows): G_s^T (2NH + C x N) . x (N x F_in)
         wb2 = lib.gatx_gemm_splitk_workspace_bytes(2 * NH + C, F_in, N)
         ws2 = torch.empty(max(wb2, 1), dtype=torch.uint8, device=dev)
-        call("gatx_gemm_f32_splitk", 2 * NH + C, F_in, N, ptr(G_s), 1, lds, ptr(x), F_in, 1,
-             ptr(gW_aug) + 4 * sh.Dp * F_in, F_in, 0, ptr(ws2), wb2, s)
+        with _span("bwd_gemm_gs", binfo):
+            call("gatx_gemm_f32_splitk", 2 * NH + C, F_in, N, ptr(G_s), 1, lds, ptr(x), F_in, 1,
+                 ptr(gW_aug) + 4 * sh.Dp * F_in, F_in, 0, ptr(ws2), wb2, s)
         g_W = torch.empty_like(W)
         g_a = torch.empty_like(a)
-        call("gatx_weight_grads", ptr(gW_aug), ptr(W), ptr(a), NH, F, F_in, ptr(g_W), ptr(g_a), s)
+        with _span("bwd_weight_grads", binfo):
+            call("gatx_weight_grads", ptr(gW_aug), ptr(W), ptr(a), NH, F, F_in, ptr(g_W),
+                 ptr(g_a), s)
         if need_skip:
             saved["g_skip_eff"] = gW_aug[sh.K_aug:]
     if need_bias and bias is not None:
         g_bias = torch.empty_like(bias)
         src_p, src_ld = (pre_p, pre_ld) if elu else (ptr(g_out), sh.out_cols)
-        call("gatx_colsum", src_p, N, sh.out_cols, src_ld, ptr(g_bias), s)
+        with _span("bwd_colsum", binfo):
+            call("gatx_colsum", src_p, N, sh.out_cols, src_ld, ptr(g_bias), s)
     return (None, (g_W if need_W else None), (g_a if need_a else None), g_bias,
             g_pre if need_resid else None)
 
@@ -949,8 +987,9 @@ class AttentionNormFunction(torch.autograd.Function):
             if a.dim() != 2 or a.size(0) != E2:
                 raise RuntimeError(f"attention {i} has shape {tuple(a.shape)}, edge_index has "
                                    f"{E2} edges")
-            call("gatx_attention_norm", ptr(a), E2, a.size(1), *_dst_row(graph), ptr(graph.rowptr),
-                 scale, int(i > 0), ptr(out), ptr(ws), s)
+            with _span("attn_norm", (graph.num_nodes, E2, a.size(1))):
+                call("gatx_attention_norm", ptr(a), E2, a.size(1), *_dst_row(graph),
+                     ptr(graph.rowptr), scale, int(i > 0), ptr(out), ptr(ws), s)
         ctx.graph, ctx.scale = graph, scale
         ctx.save_for_backward(*alphas)
         return out.view(())
@@ -963,8 +1002,9 @@ class AttentionNormFunction(torch.autograd.Function):
         grads = []
         for a in ctx.saved_tensors:
             ga = torch.empty_like(a)
-            call("gatx_attention_norm_backward", ptr(a), E2, a.size(1), *_dst_row(graph),
-                 ptr(graph.rowptr), ptr(g), ctx.scale, ptr(ga), stream())
+            with _span("attn_norm_bwd", (graph.num_nodes, E2, a.size(1))):
+                call("gatx_attention_norm_backward", ptr(a), E2, a.size(1), *_dst_row(graph),
+                     ptr(graph.rowptr), ptr(g), ctx.scale, ptr(ga), stream())
             grads.append(ga)
         return (None, *grads)
 

@@ -18,7 +18,7 @@ import torch
 from torch import nn
 
 from . import ops  # noqa: F401  (registers torch.ops.gatx.*)
-from .functional import LazyAlpha, gat_layer_lazy
+from .functional import LazyAlpha, _env_int, gat_layer_lazy
 
 
 class GATLayer(nn.Module):
@@ -106,12 +106,15 @@ class GATLayer(nn.Module):
             self.__dict__["_attention"] = alpha
             return (out, (ei2, alpha)) if return_attention_weights else out
         seed = self._dropout_seed(x.device) if p > 0 else 0
+        # GATX_DEFER_ALPHA=0: every forward writes alpha, as the reference does (bench.py times
+        # the forward both ways)
+        defer = not return_attention_weights and _env_int("GATX_DEFER_ALPHA", 1) != 0
         out, g, alpha = gat_layer_lazy(
             x, edge_index, self.W.weight, None if self.const_attention else self.a.weight,
             self.bias_param if self.bias else None, self.num_heads, self.out_features,
             self.concat, self.add_self_loops, self.const_attention, p, seed, graph=graph,
             resid=resid, elu=elu, skip_weight=skip_weight, out_dropout=out_dropout,
-            defer_alpha=not return_attention_weights)
+            defer_alpha=defer)
         self.normalised_attention_coeffs = (g, alpha)
         if return_attention_weights:
             return out, (g.edge_index, self.normalised_attention_coeffs)

@@ -8,6 +8,7 @@ from __future__ import annotations
 import torch
 
 from ._lib import call, lib, ptr, stream
+from .functional import _span
 
 
 class BCEWithLogitsFunction(torch.autograd.Function):
@@ -17,6 +18,11 @@ class BCEWithLogitsFunction(torch.autograd.Function):
             raise RuntimeError("gatx: bce_with_logits needs HIP tensors (no CPU path)")
         if x.dtype != torch.float32 or y.dtype != torch.float32:
             raise RuntimeError("gatx: bce_with_logits needs float32 input and target")
+        if y.requires_grad:
+            # the fused kernel writes d loss / d input only; torch would also differentiate the
+            # target (-x / n + (pos_weight - 1) softplus(-x) / n): refuse rather than drop it
+            raise RuntimeError("gatx: bce_with_logits does not differentiate the target; pass "
+                               "target.detach() (the task modules' targets are labels)")
         if x.shape != y.shape:
             raise ValueError(f"Target size ({tuple(y.shape)}) must be the same as input size "
                              f"({tuple(x.shape)})")
@@ -29,18 +35,19 @@ class BCEWithLogitsFunction(torch.autograd.Function):
         if n > (1 << 16):
             ws = torch.empty(lib.gatx_bce_logits_workspace_bytes(), dtype=torch.uint8,
                              device=x.device)
-        call("gatx_bce_logits", ptr(x), ptr(y), n, float(pos_weight), ptr(loss), ptr(grad),
-             ptr(ws), stream())
+        with _span("bce", (n,)):
+            call("gatx_bce_logits", ptr(x), ptr(y), n, float(pos_weight), ptr(loss), ptr(grad),
+                 ptr(ws), stream())
         ctx.save_for_backward(grad)
-        ctx.mark_non_differentiable(y)
         return loss
 
     @staticmethod
     def backward(ctx, g):
         (grad,) = ctx.saved_tensors
         out = torch.empty_like(grad)
-        call("gatx_scale_by_scalar", ptr(g.to(torch.float32).contiguous()), ptr(grad),
-             grad.numel(), ptr(out), stream())
+        with _span("bce_bwd", (grad.numel(),)):
+            call("gatx_scale_by_scalar", ptr(g.to(torch.float32).contiguous()), ptr(grad),
+                 grad.numel(), ptr(out), stream())
         return out, None, None
 
 

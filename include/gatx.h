@@ -136,6 +136,13 @@ int gatx_transpose_f32(int64_t rows, int64_t cols, const float* src, int64_t ld_
  * 0 = "f32": v_mfma_f32_32x32x2_f32. */
 void gatx_set_gemm_mode(int mode);
 int gatx_get_gemm_mode(void);
+/* The arithmetic (2 f16x3, 1 x3, 0 f32) the tiled GEMMs run for an operand layout: a_kc / b_kc
+ * = whether A's rows / B's columns are k-contiguous (the weight gradient G_aug^T x has neither). */
+int gatx_gemm_layout_mode(int a_kc, int b_kc);
+/* Diagnostic (not on the reference path): enqueue a copy of the count of f16x3 GEMM workgroups
+ * that tripped the range check and recomputed their tile as x3 (each costs ~1.5x its tile) into
+ * dst (device uint64[1]); reset != 0 also zeroes the counter. Stream-ordered, capturable. */
+int gatx_gemm_fallback_read(uint64_t* dst, int reset, gatx_stream_t stream);
 /* Workspace that lets gatx_gemm_f32 / gatx_projection_gemm split the K range of the tiles in
  * their last, partially filled wave (0 = no split for this shape; NULL workspace = never split).
  * The slices are summed in a fixed order by a fix-up kernel, so results stay deterministic. */

@@ -102,3 +102,26 @@ def test_inference_alpha_on_read(shape, device):
     with torch.no_grad():
         layer(x * 2, ei)
     assert not torch.equal(layer.normalised_attention_coeffs, lazy)
+
+
+def test_inference_alpha_read_on_another_stream(device):
+    """The deferred alpha read from a side stream waits for the forward's stream: bitwise the
+    eager alpha, also when the forward was just enqueued behind a long kernel."""
+    NH, F, fin = 4, 8, 24
+    b, W, a, _, _ = _small_case(seed=6, fin=fin, NH=NH, F=F)
+    layer = _layer(device, W, a, NH, F, True).eval()
+    x = torch.from_numpy(b.x).to(device)
+    ei = torch.from_numpy(b.edge_index).to(device)
+    with torch.no_grad():
+        _, (_, alpha_e) = layer(x, ei, return_attention_weights=True)
+        alpha_e = alpha_e.clone()
+        big = torch.randn(4096, 4096, device=device)
+        torch.cuda.synchronize()
+        for _ in range(4):   # keep the forward's stream busy ahead of the forward
+            big = big @ big * 1e-3
+        layer(x, ei)
+    side = torch.cuda.Stream(device)
+    with torch.cuda.stream(side):
+        lazy = layer.normalised_attention_coeffs.clone()
+    side.synchronize()
+    assert torch.equal(lazy, alpha_e)

@@ -37,7 +37,7 @@ def _hub_graph(n=3000, e=20000, hubs=(30000, 9000, 1001, 1000, 999), fin=16, see
     return x, ei
 
 
-def _run(device, x, ei, W, a, NH, F, concat, dropout=0.0, grads=True):
+def _run(device, x, ei, W, a, NH, F, concat, dropout=0.0, grads=True, x_grad=True):
     import gatx
     layer = gatx.GATLayer(x.shape[1], F, NH, concat, dropout=dropout,
                           add_self_loops=True).to(device)
@@ -47,7 +47,9 @@ def _run(device, x, ei, W, a, NH, F, concat, dropout=0.0, grads=True):
     if dropout > 0:
         layer._dropout_seed = lambda *_: 77
         layer.train()
-    xt = torch.from_numpy(x).to(device).requires_grad_(grads)
+    # x_grad=False: the model input (no gradient wanted), which sends a reassociated first
+    # layer down _reassoc_backward (gathers over x rows, G_s score rows) instead of layer_backward
+    xt = torch.from_numpy(x).to(device).requires_grad_(grads and x_grad)
     et = torch.from_numpy(ei).to(device)
     gatx.clear_graph_cache()
     out, (ei2, alpha) = layer(xt, et, return_attention_weights=True)
@@ -57,7 +59,8 @@ def _run(device, x, ei, W, a, NH, F, concat, dropout=0.0, grads=True):
         g_out, g_alpha = grad_seeds(tuple(out.shape), tuple(alpha.shape))
         ((out * torch.from_numpy(g_out).to(device)).sum()
          + (alpha * torch.from_numpy(g_alpha).to(device)).sum()).backward()
-        r["grad_x"] = xt.grad.cpu().numpy()
+        if x_grad:
+            r["grad_x"] = xt.grad.cpu().numpy()
         r["grad_W"] = layer.W.weight.grad.cpu().numpy()
         r["grad_a"] = layer.a.weight.grad.cpu().numpy()
     return r
@@ -69,6 +72,7 @@ CASES = {   # name: (fin, NH, F, concat, env)
     "mean_one_pass": (16, 6, 12, False, {}),
     "mean_multi_pass": (16, 6, 12, False, {"GATX_MEAN_HEADS": "2"}),
     "reassociated": (8, 4, 64, True, {}),
+    "reassociated_input": (8, 4, 64, True, {}),   # x needs no gradient: _reassoc_backward
     "dropout": (16, 4, 16, True, {}),
 }
 
@@ -87,7 +91,9 @@ def test_hub_split_vs_oracle(name, T, device, monkeypatch):
     x, ei = _hub_graph(fin=fin)
     W = gd.xavier_uniform(6, NH * F, fin)
     a = gd.xavier_uniform(7, NH, NH * 2 * F)
-    r = _run(device, x, ei, W, a, NH, F, concat, dropout)
+    x_grad = name != "reassociated_input"
+    keys = ("x", "W", "a") if x_grad else ("W", "a")
+    r = _run(device, x, ei, W, a, NH, F, concat, dropout, x_grad=x_grad)
     keep = orc.dropout_keep(77, r["alpha"].shape[0], NH, dropout) if dropout > 0 else None
     out, ei2, alpha, cache = orc.gat_layer_forward(x, ei, W, a, NH, F, concat, dropout_p=dropout,
                                                    keep=keep)
@@ -96,22 +102,22 @@ def test_hub_split_vs_oracle(name, T, device, monkeypatch):
     assert np.abs(r["alpha"] - alpha).max() <= OUT_TOL
     g_out, g_alpha = grad_seeds(out.shape, alpha.shape)
     gr = orc.gat_layer_backward(cache, g_out, g_alpha)
-    for k in ("x", "W", "a"):
+    for k in keys:
         err = np.abs(r[f"grad_{k}"] - gr[k]).max()
         assert err <= GRAD_TOL * max(1.0, np.abs(gr[k]).max()), (k, err)
     # split backward is deterministic: a second run is bitwise identical
-    r1 = _run(device, x, ei, W, a, NH, F, concat, dropout)
-    for k in ("out", "alpha", "grad_x", "grad_W", "grad_a"):
+    r1 = _run(device, x, ei, W, a, NH, F, concat, dropout, x_grad=x_grad)
+    for k in ("out", "alpha") + tuple(f"grad_{k}" for k in keys):
         np.testing.assert_array_equal(r[k], r1[k], err_msg=k)
     # the same layer without splitting: same result to fp32 summation-order noise
     monkeypatch.setenv("GATX_HUB_EDGES", "0")
     monkeypatch.setenv("GATX_BWD_HUB_EDGES", "0")
     from gatx import functional
     functional.reset_tuning()
-    r0 = _run(device, x, ei, W, a, NH, F, concat, dropout)
+    r0 = _run(device, x, ei, W, a, NH, F, concat, dropout, x_grad=x_grad)
     assert np.abs(r["out"] - r0["out"]).max() <= 1e-5
     assert np.abs(r["alpha"] - r0["alpha"]).max() <= 1e-5
-    for k in ("x", "W", "a"):
+    for k in keys:
         err = np.abs(r[f"grad_{k}"] - r0[f"grad_{k}"]).max()
         assert err <= 1e-5 * max(1.0, np.abs(r0[f"grad_{k}"]).max()), (k, err)
 

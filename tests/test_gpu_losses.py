@@ -38,3 +38,7 @@ def test_bce_module_and_shape_check(device):
     assert abs(loss(x, torch.ones(3, 4, device=device)).item() - 2.0 * 0.6931471805599453) < 1e-6
     with pytest.raises(ValueError):
         loss(x, torch.ones(4, 3, device=device))
+    # a target that wants a gradient is refused (torch would differentiate it; the fused kernel
+    # only writes the input's gradient)
+    with pytest.raises(RuntimeError, match="target"):
+        loss(x, torch.ones(3, 4, device=device, requires_grad=True))
