@@ -245,11 +245,14 @@ def calc_attention_norm_grad(edge_index, attention_list, g=1.0):
 
 
 def gat_model_forward_backward(x, edge_index, layers, skips, num_heads, out_features, concat,
-                               add_skip, g_out, dtype=np.float64):
+                               add_skip, g_out, dtype=np.float64, g_alphas=None):
     """gat_model_forward plus its backward for an upstream gradient g_out: the layer backward
     (gat_layer_backward) chained through ELU (d elu = 1 for x > 0 else exp(x)), the skip add
     (concat: add; head-mean: add of the skip's per-head mean, models/GATModel.py:135-145) and
-    the skip projection. Returns (out, {"W": [...], "a": [...], "skip": [...], "x": g_x})."""
+    the skip projection. g_alphas: optional per-layer upstream gradients of the returned alphas
+    (a loss on the attention, e.g. calc_attention_norm). g_out may be a callable out -> g_out
+    (a loss of the forward's output). Returns (out, {"W": [...], "a": [...], "skip": [...],
+    "x": g_x})."""
     x = np.asarray(x, dtype=dtype)
     L = len(layers)
     saved, skip_i = [], 0
@@ -266,12 +269,12 @@ def gat_model_forward_backward(x, edge_index, layers, skips, num_heads, out_feat
             o = o + (so if concat[i] else so.reshape(-1, num_heads[i], out_features[i]).mean(axis=1))
         saved.append((inp, cache, o, Ws))
         x = elu(o) if i != L - 1 else o
-    g = np.asarray(g_out, dtype=dtype)
+    g = np.asarray(g_out(x) if callable(g_out) else g_out, dtype=dtype)
     gW, ga, gs = [None] * L, [None] * L, []
     for i in reversed(range(L)):
         inp, cache, pre, Ws = saved[i]
         g_pre = g * np.where(pre > 0, 1.0, np.exp(np.minimum(pre, 0))) if i != L - 1 else g
-        gr = gat_layer_backward(cache, g_pre)
+        gr = gat_layer_backward(cache, g_pre, None if g_alphas is None else g_alphas[i])
         gW[i], ga[i] = gr["W"], gr["a"]
         g_inp = gr["x"]
         if add_skip[i]:
@@ -289,3 +292,38 @@ def gat_model_forward_backward(x, edge_index, layers, skips, num_heads, out_feat
                 g_inp = g_inp + g_so @ Wsd
         g = g_inp
     return x, {"W": gW, "a": ga, "skip": gs[::-1], "x": g}
+
+
+# --------------------------------------------------------------------------- task module step
+def cross_entropy_grad(logits, labels, rows):
+    """d/d logits of torch.nn.CrossEntropyLoss(reduction='mean')(logits[rows], labels[rows])
+    (models/planetoid_gat.py:11,28): (softmax - onehot) / |rows| on the masked rows, 0 elsewhere.
+    Returns (loss, grad)."""
+    z = logits[rows].astype(np.float64)
+    z = z - z.max(axis=1, keepdims=True)
+    p = np.exp(z)
+    p /= p.sum(axis=1, keepdims=True)
+    n = len(rows)
+    y = labels[rows]
+    loss = -np.log(p[np.arange(n), y]).mean()
+    g = np.zeros(logits.shape, dtype=np.float64)
+    p[np.arange(n), y] -= 1.0
+    g[rows] = p / n
+    return loss, g
+
+
+def planetoid_step_grads(x, edge_index, layers, num_heads, out_features, concat, labels, rows,
+                         attention_reward):
+    """PlanetoidGAT.training_step's gradients (`models/planetoid_gat.py:15-30`) in eval-mode
+    arithmetic (no dropout): loss = CE(out[train], y[train]) + attention_reward *
+    calc_attention_norm(edge_index', alphas). Returns (loss, grads) with grads as
+    gat_model_forward_backward's."""
+    L = len(layers)
+    out, ei2, alphas = gat_model_forward(x, edge_index, layers, [], num_heads, out_features,
+                                         concat, [False] * L, dtype=np.float64)
+    ce, g_out = cross_entropy_grad(out, labels, rows)
+    norm = calc_attention_norm(ei2, alphas)
+    g_al = [attention_reward * g for g in calc_attention_norm_grad(ei2, alphas)]
+    _, grads = gat_model_forward_backward(x, edge_index, layers, [], num_heads, out_features,
+                                          concat, [False] * L, g_out, g_alphas=g_al)
+    return ce + attention_reward * norm, grads

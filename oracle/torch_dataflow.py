@@ -1,6 +1,7 @@
 """ORACLE-SIDE CPU BASELINE — test/bench infrastructure only (never imported by the product).
 
-The reference GATLayer's forward restated in torch eager on CPU, op for op, so `bench.py`'s
+The reference GATLayer's forward restated in torch eager, op for op (on CPU for the baseline;
+the full-size headline parity test also runs it at fp64 on the device as its checker), so `bench.py`'s
 `cpu_baseline` leg times the same ATen dataflow the reference runs on its CPU path
 (`cpu_baseline.kind` = "restatement"): materialised per-edge gathers with `index_select`, the
 (E', NH, 2F) concatenation times `a`, one global `max`, LeakyReLU, `exp`, `scatter_add_` for the
@@ -24,7 +25,8 @@ def self_loop_rewrite(edge_index: torch.Tensor) -> torch.Tensor:
     """models/utils.py:47-72: drop src == dst, append (i, i) for i <= max id."""
     n = int(edge_index.max()) + 1
     keep = edge_index[0] != edge_index[1]
-    loops = torch.arange(n, dtype=edge_index.dtype).unsqueeze(0).expand(2, n)
+    loops = torch.arange(n, dtype=edge_index.dtype,
+                         device=edge_index.device).unsqueeze(0).expand(2, n)
     return torch.cat([edge_index[:, keep], loops], dim=1)
 
 

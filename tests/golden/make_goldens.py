@@ -293,6 +293,22 @@ def model_cases(sd_pat):
                [None], "PPI", wgen=[[90 + i, 95 + i] for i in range(3)])
 
 
+def planetoid_model_cases():
+    """Round-4 additions (BASELINE configs 1-2 at model level): the 2-layer Cora / Citeseer /
+    Pubmed GATModels with their TRAINED checkpoints (`checkpoints/*-100epochs.ckpt`) in eval
+    mode — output logits, both layers' alphas, calc_attention_norm and its gradient — on
+    synthetic graphs of the datasets' sizes (the layer cases' graphs)."""
+    for ds, gen in (("Cora", dict(G=1, n=2708, e=10556, in_features=1433, features="bernoulli")),
+                    ("Citeseer", dict(G=1, n=3327, e=9104, in_features=3703,
+                                      features="bernoulli", feature_seed=19)),
+                    ("Pubmed", dict(G=1, n=19717, e=88648, in_features=500, feature_seed=20))):
+        sd = read_state_dict(f"{CKPT}/{ds}-100epochs.ckpt")
+        x, ei = gen_batch(gen)
+        model_case(f"{ds.lower()}_model_trained", x, ei, gen,
+                   [(sd[f"gat_layer_list.{i}.W.weight"], sd[f"gat_layer_list.{i}.a.weight"])
+                    for i in range(2)], [], ds)
+
+
 def model_case(name, x, ei, gen, layers, skips, dataset, wgen=None):
     sys.path.insert(0, REPO)
     from gatx.config import data_config
@@ -359,7 +375,10 @@ def ppi_full_cases():
                        gdata.xavier_uniform(23, NH, NH * 2 * F), gen=g, wgen=[22, 23])
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and "--planetoid" in sys.argv:
+    torch.set_num_threads(8)
+    planetoid_model_cases()
+elif __name__ == "__main__":
     if "--ppi-full-only" in sys.argv:
         torch.set_num_threads(8)
         ppi_full_cases()

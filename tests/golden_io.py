@@ -12,8 +12,9 @@ from gatx import data as gdata
 
 GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 LAYER_CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz"))
-                     if not os.path.basename(p).startswith(("pattern_model", "ppi_model")))
-MODEL_CASES = ["pattern_model_trained", "ppi_model_small"]
+                     if "_model_" not in os.path.basename(p))
+MODEL_CASES = ["pattern_model_trained", "ppi_model_small", "cora_model_trained",
+               "citeseer_model_trained", "pubmed_model_trained"]
 
 
 def _gen_batch(gen):

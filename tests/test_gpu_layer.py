@@ -613,17 +613,18 @@ def test_attention_norm_matches_reference(name, device):
     c = load_model_case(name)
     e = c["expected"]
     L = len(c["layers"])
-    ei = torch.from_numpy(c["edge_index_out"]).to(device)
-    alphas = [torch.from_numpy(e[f"alpha{i}"].full).to(device).requires_grad_(True)
-              for i in range(L)]
-    v = attention_norm(ei, alphas)
     ref = e["attention_norm"]
-    assert abs(v.item() - ref) <= 1e-5 * max(1.0, abs(ref)), (v.item(), ref)
-    v.backward()
-    for i, a in enumerate(alphas):
-        e[f"attention_norm_grad{i}"].check(a.grad.cpu().numpy(), 1e-7)
-    # bitwise reproducible
-    assert attention_norm(ei, alphas).item() == v.item()
+    if all(e[f"alpha{i}"].full is not None for i in range(L)):   # Pubmed's alpha is sampled
+        ei = torch.from_numpy(c["edge_index_out"]).to(device)
+        alphas = [torch.from_numpy(e[f"alpha{i}"].full).to(device).requires_grad_(True)
+                  for i in range(L)]
+        v = attention_norm(ei, alphas)
+        assert abs(v.item() - ref) <= 1e-5 * max(1.0, abs(ref)), (v.item(), ref)
+        v.backward()
+        for i, a in enumerate(alphas):
+            e[f"attention_norm_grad{i}"].check(a.grad.cpu().numpy(), 1e-7)
+        # bitwise reproducible
+        assert attention_norm(ei, alphas).item() == v.item()
     # the model path: alphas of the HIP layers, edge_index' returned by the HIP layers
     cfg = c["cfg"]
     model = gatx.GATModel(**cfg).to(device).eval()
@@ -739,7 +740,7 @@ def test_model_backward_vs_oracle(name, device):
     gatx = _gatx()
     from gatx import data as gd
     c = load_model_case(name)
-    cfg = c["cfg"]
+    cfg = dict(c["cfg"], dropout=0.0)   # the Planetoid configs train with dropout 0.6
     model = gatx.GATModel(**cfg).to(device).train()
     with torch.no_grad():
         for i, (W, a) in enumerate(c["layers"]):
