@@ -256,6 +256,8 @@ def layer_backward_dataflow(N, E2, F_in, NH, F, concat, elu, need_x, fold_resid=
         ("bwd_edge_src", csr + soft + 4 * (gog + NH * E2 + N * (Dp + NH)), 0),
         ("bwd_max", 4 * N * NH, 0),
     ]
+    # G_aug's exact row / column maxima for the f16x3 gradient GEMMs' scales (one read)
+    out.append(("bwd_gaug_stats", 4 * (N * ldg + N + KC), 0))
     if need_x:
         out.append(("bwd_gemm_gx", 4 * (N * ldg + 2 * KC * F_in + N * F_in
                                         + (N * F_in if fold_resid else 0)),
@@ -891,7 +893,7 @@ def main():
     fb = torch.zeros(1, dtype=torch.int64, device=dev)
     _lib.call("gatx_gemm_fallback_read", _lib.ptr(fb), 1, _lib.stream())   # reset the counter
     elapsed, summ, n_instr = run_timed(step, args.steps, world, dev,
-                                       eager_step if use_graph else None)
+                                       step.eager if use_graph else None)
     _lib.call("gatx_gemm_fallback_read", _lib.ptr(fb), 1, _lib.stream())
     fallback_tiles = int(fb.item())
     step_s = elapsed / args.steps
@@ -909,7 +911,7 @@ def main():
         st = CapturedStep(eager_step) if use_graph else eager_step
         for _ in range(args.warmup):
             st()
-        el, _, _ = run_timed(st, args.steps, world, dev, eager_step if use_graph else None)
+        el, _, _ = run_timed(st, args.steps, world, dev, st.eager if use_graph else None)
         alpha_eager_ms = el / args.steps * 1e3
         os.environ["GATX_DEFER_ALPHA"] = "1"
         gf.reset_tuning()

@@ -307,6 +307,41 @@ int gemm_variant() {
   return v;
 }
 
+// GATX_F16P=0 (A/B tests): the in-loop split kernel even when pre-split weight planes are given
+bool f16p_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("GATX_F16P");
+    return !(e && strcmp(e, "0") == 0);
+  }();
+  return on;
+}
+
+// The pre-split kernel, then the tail fix-up of its partial last wave (as launch_gemm).
+int launch_f16p_and_fixups(const GemmArgs& g, int tag, hipStream_t stream) {
+  GATX_CALL(launch_gemm_f16p(g, tag, stream));
+  if (g.tail_s > 1 && g.s_part) {
+    tail_fixup_scores_kernel<<<(unsigned)(g.tail_rem * (g.bm / 64)), 256, 0, stream>>>(g);
+    GATX_LAUNCH_CHECK("tail_fixup_scores");
+  } else if (g.tail_s > 1) {
+    const int64_t total = g.tail_rem * g.bm * g.bn;
+    tail_fixup_kernel<<<(unsigned)std::min<int64_t>(ceil_div(total, 256), 8192), 256, 0, stream>>>(g);
+    GATX_LAUNCH_CHECK("tail_fixup");
+  }
+  return 0;
+}
+
+// The row-contiguous f16x3 weight-gradient kernel, then the split-K reduction of its slabs.
+int launch_f16rc_and_reduce(const GemmArgs& g, hipStream_t stream) {
+  GATX_CALL(launch_gemm_f16rc(g, stream));
+  if (g.splits > 1) {
+    const int64_t total = g.M * g.N;
+    const unsigned rg = (unsigned)std::min<int64_t>(ceil_div(total, 256), 8192);
+    splitk_reduce_kernel<<<rg, 256, 0, stream>>>(g, 1);
+    GATX_LAUNCH_CHECK("splitk_reduce");
+  }
+  return 0;
+}
+
 template <int TAG>
 int launch_gemm(const GemmArgs& g0, bool a_kc, bool b_kc, int batch, hipStream_t stream) {
   GemmArgs g = g0;
@@ -500,7 +535,8 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
                      int64_t bias_bs, const float* resid, int64_t resid_ld, int64_t resid_bs,
                      int elu, void* workspace, size_t workspace_bytes, int tag,
                      hipStream_t stream, int64_t n_split2 = -1, float* C2 = nullptr,
-                     int64_t ldc2 = 0, const ScoreReq* sc = nullptr, bool* fused = nullptr) {
+                     int64_t ldc2 = 0, const ScoreReq* sc = nullptr, bool* fused = nullptr,
+                     const void* b_planes = nullptr, const float* a_rowmax = nullptr) {
   if (fused) *fused = false;
   GATX_REQUIRE(M >= 0 && N >= 0 && K >= 0 && batch >= 1, "gemm: negative size");
   if (M == 0 || N == 0) return 0;
@@ -527,6 +563,8 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
   g.elu = elu;
   g.splits = 1; g.k_per_split = K; g.partial = nullptr;
   g.s_a = nullptr; g.s_nh = g.s_f = g.s_fp = g.s_h2 = 0; g.s_part = nullptr;
+  g.b_planes = nullptr; g.b_prow = 0; g.fb_counter = f16_fallback_counter();
+  g.a_rowmax = a_rowmax;
   auto aligned = [](const void* p, int64_t ld, int64_t bs) {
     return ((uintptr_t)p % 16 == 0) && (ld % 4 == 0) && (bs % 4 == 0);
   };
@@ -602,7 +640,18 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
     g.s_a = sc->a; g.s_nh = sc->nh; g.s_f = sc->f; g.s_fp = (int)round_up(sc->f, 4);
     g.s_h2 = 2 * sc->nh; g.s_part = s_part;
   }
-  if (tag == 0) GATX_CALL(launch_gemm<0>(g, a_kc, b_kc, batch, stream));
+  if (b_planes && gemm_mode() == 2 && f16p_enabled() && kd.id == 2 && batch == 1 && a_kc &&
+      b_kc && g.a_vec && g.b_vec && g.splits == 1 && tag != 2 && g.lda < (1 << 20)) {
+    g.b_planes = (const char*)b_planes + 256;   // past the planes' header (gemm_f16p.hip)
+    g.b_prow = round_up(K, (int64_t)32) * 4;
+  }
+  // the weight gradient G_aug^T x with G_aug's exact column maxima: the row-contiguous f16x3
+  // kernel (gemm_f16p.hip)
+  const bool wgrad_f16 = a_rowmax && tag == 2 && gemm_mode() == 2 && f16p_enabled() &&
+                         kd.id == 2 && batch == 1 && !a_kc && !b_kc && !accumulate;
+  if (g.b_planes) GATX_CALL(launch_f16p_and_fixups(g, tag, stream));
+  else if (wgrad_f16) GATX_CALL(launch_f16rc_and_reduce(g, stream));
+  else if (tag == 0) GATX_CALL(launch_gemm<0>(g, a_kc, b_kc, batch, stream));
   else if (tag == 2) GATX_CALL(launch_gemm<2>(g, a_kc, b_kc, batch, stream));
   else GATX_CALL(launch_gemm<1>(g, a_kc, b_kc, batch, stream));
   if (s_part) {
@@ -700,6 +749,67 @@ extern "C" int gatx_projection_gemm_scores(int64_t M, int64_t N, int64_t K, cons
   // score pass over the stored Wh
   if (!fused) return gatx_node_scores(C0, M, NH, F, a, S, s);
   return 0;
+}
+
+extern "C" size_t gatx_weight_planes_bytes(int64_t rows, int64_t K) {
+  return weight_planes_bytes(rows, K);
+}
+
+extern "C" int gatx_weight_planes(const float* W, int64_t rows, int64_t K, int64_t ld,
+                                  void* planes, gatx_stream_t s) {
+  GATX_REQUIRE(rows >= 1 && K >= 1 && ld >= K, "weight_planes: bad shape");
+  GATX_REQUIRE((uintptr_t)planes % 256 == 0, "weight_planes: buffer must be 256-byte aligned");
+  return build_weight_planes(W, rows, K, ld, planes, (hipStream_t)s);
+}
+
+extern "C" int gatx_gemm_planes(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                                const float* B, int64_t ldb, const void* b_planes, float* C0,
+                                int64_t ldc0, int64_t n_split, float* C1, int64_t ldc1,
+                                int64_t n_split2, float* C2, int64_t ldc2, int accumulate,
+                                const float* a, int NH, int F, float* S, int gradient,
+                                const float* a_rowmax, void* workspace, size_t workspace_bytes,
+                                gatx_stream_t s) {
+  GATX_REQUIRE(b_planes == nullptr || (uintptr_t)b_planes % 256 == 0,
+               "gemm_planes: planes must be 256-byte aligned");
+  const int tag = gradient ? 1 : 0;
+  if (a != nullptr) {   // the forward projection with the node scores fused (see _scores)
+    GATX_REQUIRE(!gradient && !accumulate && n_split >= N && NH >= 1 && F >= 1 &&
+                     N == (int64_t)NH * round_up(F, 4) && ldc0 == N,
+                 "gemm_planes: scores need the packed [M][NH * round4(F)] Wh as the only output");
+    const ScoreReq sc{a, NH, F, S};
+    bool fused = false;
+    if (2 * NH <= 16 && M > 0) {
+      GATX_CALL(gemm_impl(M, N, K, 1, A, lda, 1, 0, B, 1, ldb, 0, C0, ldc0, 0, N, nullptr, 0, 0,
+                          0, nullptr, 0, nullptr, 0, 0, 0, workspace, workspace_bytes, 0,
+                          (hipStream_t)s, -1, nullptr, 0, &sc, &fused, b_planes));
+    } else {
+      GATX_CALL(gemm_impl(M, N, K, 1, A, lda, 1, 0, B, 1, ldb, 0, C0, ldc0, 0, N, nullptr, 0, 0,
+                          0, nullptr, 0, nullptr, 0, 0, 0, workspace, workspace_bytes, 0,
+                          (hipStream_t)s, -1, nullptr, 0, nullptr, nullptr, b_planes));
+    }
+    if (!fused) return gatx_node_scores(C0, M, NH, F, a, S, s);
+    return 0;
+  }
+  return gemm_impl(M, N, K, 1, A, lda, 1, 0, B, 1, ldb, 0, C0, ldc0, 0, n_split, C1, ldc1, 0,
+                   accumulate, nullptr, 0, nullptr, 0, 0, 0, workspace, workspace_bytes, tag,
+                   (hipStream_t)s, n_split2, C2, ldc2, nullptr, nullptr, b_planes,
+                   gradient ? a_rowmax : nullptr);
+}
+
+extern "C" int gatx_gemm_wgrad(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                               const float* B, int64_t ldb, const float* a_rowmax, float* C,
+                               int64_t ldc, void* workspace, size_t workspace_bytes,
+                               gatx_stream_t s) {
+  return gemm_impl(M, N, K, 1, A, 1, lda, 0, B, ldb, 1, 0, C, ldc, 0, N, nullptr, 0, 0, 0,
+                   nullptr, 0, nullptr, 0, 0, 0, workspace, workspace_bytes, 2, (hipStream_t)s,
+                   -1, nullptr, 0, nullptr, nullptr, nullptr, a_rowmax);
+}
+
+extern "C" int gatx_absmax_rows_cols(const float* X, int64_t rows, int64_t cols, int64_t ld,
+                                     float* rowmax, float* colmax, gatx_stream_t s) {
+  GATX_REQUIRE(rows >= 0 && cols >= 1 && ld >= cols && rowmax != nullptr,
+               "absmax_rows_cols: bad arguments");
+  return absmax_rows_cols(X, rows, cols, ld, rowmax, colmax, (hipStream_t)s);
 }
 
 extern "C" int gatx_gemm_f32_batched(int64_t batch, int64_t M, int64_t N, int64_t K,

@@ -121,6 +121,13 @@ struct GemmArgs {
   // tile tn adds its columns' share of S = Wh . A2^T as s_part[tn][row][s_h2], A2 read from the
   // reference's attention vector s_a (heads s_nh, features s_f, padded s_fp per head of Wh)
   const float* s_a; int s_nh, s_f, s_fp, s_h2; float* s_part;
+  // f16p (gemm_f16p.hip): B's pre-split fp16 planes (after their header; nullptr = none) with
+  // b_prow bytes per row, and the f16x3 -> x3 fallback tile counter
+  const void* b_planes; int64_t b_prow;
+  unsigned long long* fb_counter;
+  // exact max |A row| per row (gatx_absmax_rows_cols; nullptr = none): the split kernels scale
+  // each A row by it instead of by its first K-tile's max
+  const float* a_rowmax;
 };
 
 // A2[h2][col] of the attention vector a (models/gat_layer.py:76-82 split per half): the weight of
@@ -283,6 +290,16 @@ int launch_gemm_x3(const gk::GemmArgs& g, bool a_kc, bool b_kc, int batch, int t
 bool gemm_smallk_fits(int64_t M, int64_t N, int64_t K, bool a_kc, bool b_kc, int accumulate,
                       bool resid);
 int launch_gemm_smallk(const gk::GemmArgs& g, int batch, hipStream_t stream);
+// gemm_f16p.hip: the f16x3 kernel with B given as pre-split fp16 planes (tags 0 and 1)
+int launch_gemm_f16p(const gk::GemmArgs& g, int tag, hipStream_t stream);
+int launch_gemm_f16rc(const gk::GemmArgs& g, hipStream_t stream);
+size_t weight_planes_bytes(int64_t rows, int64_t K);
+int absmax_rows_cols(const float* X, int64_t rows, int64_t cols, int64_t ld, float* rowmax,
+                     float* colmax, hipStream_t stream);
+int build_weight_planes(const float* W, int64_t rows, int64_t K, int64_t ld, void* buf,
+                        hipStream_t stream);
+// gemm_x3.hip: the device address of the f16x3 -> x3 fallback tile counter
+unsigned long long* f16_fallback_counter();
 // gemm_x3.hip: copy (and optionally zero) the f16x3 -> x3 fallback tile counter
 int read_f16_fallbacks(unsigned long long* dst, int reset, hipStream_t stream);
 // the x3 kernel instance whose occupancy sizes tail / split-K decisions

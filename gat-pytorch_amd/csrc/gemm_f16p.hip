@@ -1,0 +1,742 @@
+// f16x3 GEMM with the weight operand pre-split ("f16p"): C = A . B^T for a k-contiguous fp32 A
+// (activations, or a gradient G_aug) and a weight B (W_aug, W_aug^T) given as fp16 planes built
+// once per weight version by gatx_weight_planes.
+//
+// Arithmetic: the f16x3 split of gemm_x3_impl.h (x = h + l 2^-11, three fp16 MFMA products), with
+// the 2^11 of the main product carried by the planes themselves instead of register multiplies:
+//     A planes  Ah = fp16(64 s_r a),       Al = fp16(64 s_r a - Ah)       (s_r: row scale, A)
+//     B planes  Bh = fp16(32 s_B b),       Bl = fp16(32 s_B b - Bh)       (s_B: one scale, B)
+//     Ah Bh + Ah Bl + Al Bh = 2^11 s_r s_B a b  (dropped: Al Bl, <= 2^-22 |2^11 s_r s_B a b|)
+// so the MFMA phase is three plain v_mfma_f32_32x32x16_f16 per block (no v_pk_mul), and the split
+// of A is four v_fma_mix per element pair (fp16 rounding of the exact product, then of the exact
+// residual) instead of eight conversions and subtractions. B's planes come from memory (two
+// 16-byte loads per thread per K-tile, no VALU). Per K-tile and wave the VALU work drops from ~113
+// instructions (gemm_x3_impl.h f16_mainloop) to ~30, which is what kept the matrix pipe waiting
+// there: with two waves per SIMD the split, the planes' LDS stores and the hi-fragment scaling
+// filled most of the issue slots between MFMAs.
+//
+// Range: s_B puts max |B| at [2^9, 2^10) (32 s_B |b| < 2^15), so B never overflows; a B row whose
+// max is below 2^-8 / s_B (its residual plane would lose precision) flags its 256-row tile, and
+// workgroups reading a flagged tile recompute as x3 (the fp32 weight is still passed). A rows are
+// scaled by their max over the first K-tile to [2^7, 2^8) (SCALE) or taken as they are; a row
+// whose max leaves [2^-9, 1023] after scaling sends its workgroup to the x3 recomputation too, so
+// accuracy never depends on the operands' magnitudes (tests/test_gpu_layer.py::
+// test_gemm_f16p_accuracy). Loads go through buffer resources bounded to the tile's rows: rows
+// past M or N read as zero.
+#include "gemm_x3_impl.h"
+
+namespace gatx {
+namespace {
+using namespace gk;
+
+// h = fp16_rn(x c), l = fp16_rn(x c - h) for an element pair (x in the low halves): v_fma_mix
+// rounds the exact product and then the exact residual (hipcc never selects fma_mix here).
+__device__ inline void split_mix(float x, float y, float c, uint32_t& h, uint32_t& l) {
+  asm volatile(
+      "v_fma_mixlo_f16 %0, %2, %4, 0 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixhi_f16 %0, %3, %4, 0 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixlo_f16 %1, %2, %4, -%0 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %1, %3, %4, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(h), "=&v"(l)
+      : "v"(x), "v"(y), "v"(c));
+}
+
+__device__ inline __amdgpu_buffer_rsrc_t buffer_rsrc(const void* base, int64_t bytes) {
+  const int nr = (int)(bytes > 0x7ffffff0 ? 0x7ffffff0 : bytes);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, nr, 0x00020000);
+}
+
+// One fp16 plane image of 256 rows x BK k (gemm_x3_impl.h PlaneImg extended to BK 32): 16-byte
+// 8-k slots, slot-major; odd slots' rows XOR'd by 12 for conflict-free fragment reads.
+template <int BK>
+struct PImg {
+  static constexpr int BYTES = 256 * BK * 2;
+  static __device__ inline int off(int r, int k) {
+    const int s = k >> 3;
+    return s * (256 * 16) + ((r ^ ((s & 1) * 12)) << 4) + ((k & 4) << 1);
+  }
+};
+
+constexpr int kPlanesHeader = 256;   // bytes before the planes: [0] 2^-11 / s_B, [1] s_B, [16..] tile flags
+
+template <int BK>
+struct F16pCfg {
+  static constexpr int PB = PImg<BK>::BYTES;
+  static constexpr int STAGE = 4 * PB;   // A_h A_l B_h B_l
+  static constexpr int X3_STAGE = 3 * 2 * (256 + 256) * 16;
+  static constexpr int SMEM = (2 * STAGE > 2 * X3_STAGE ? 2 * STAGE : 2 * X3_STAGE) + 256 * 4;
+};
+
+// Main loop over the K-tiles [kb, K) of one 256 x 256 tile. Returns true when a row of A left the
+// fp16 range (the caller recomputes the tile as x3). inv[256] (LDS, after the stages) receives
+// 1 / s_r per tile row.
+template <int BK, int SCALE>
+__device__ inline bool f16p_mainloop(const GemmArgs& g, const float* __restrict__ A, int64_t m0,
+                                     int64_t n0, int64_t kb, int64_t K, char* smem, int wm,
+                                     int wn, int lane, floatx16 (&acc)[4][2]) {
+  using I = PImg<BK>;
+  using Cf = F16pCfg<BK>;
+  constexpr int PB = Cf::PB, STAGE = Cf::STAGE, MB = 4, NB = 2, NT = 512;
+  constexpr int NV = BK / 8;   // float4 (A) and 16-byte plane pieces (B) per thread per K-tile
+  constexpr int TPR = BK / 4;  // staging threads per row
+  float* inv = (float*)(smem + 2 * STAGE);
+  const int tid = threadIdx.x;
+  const int64_t arows = g.M - m0 < 256 ? g.M - m0 : 256;
+  const int64_t brows = g.N - n0 < 256 ? g.N - n0 : 256;
+  const auto ra = buffer_rsrc(A + m0 * g.lda, arows * g.lda * 4);
+  const auto rb = buffer_rsrc((const char*)g.b_planes + n0 * g.b_prow, brows * g.b_prow);
+  int voa[NV], vob[NV], oa[NV], ob[NV], ka[NV];
+#pragma unroll
+  for (int c = 0; c < NV; ++c) {
+    const int idx = tid + NT * c;
+    const int r = idx / TPR, k = 4 * (idx % TPR), j = idx % TPR;
+    voa[c] = (r * (int)g.lda + k) * 4;
+    oa[c] = I::off(r, k);
+    ka[c] = k;
+    vob[c] = r * (int)g.b_prow + (j >> 1) * 32 + (j & 1) * 16;   // slot j >> 1, plane j & 1
+    ob[c] = (2 + (j & 1)) * PB + I::off(r, 8 * (j >> 1));
+  }
+  float4 va[NV];
+  uint4 vb[NV];
+  const int64_t nk = ceil_div(K - kb, BK);
+  auto load = [&](int64_t kt) {
+    const int so = (int)((kb + kt * BK) * 4);   // bytes: 4 per k in A and in the planes
+#pragma unroll
+    for (int c = 0; c < NV; ++c)
+      va[c] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ra, voa[c], so, 0));
+#pragma unroll
+    for (int c = 0; c < NV; ++c)
+      vb[c] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rb, vob[c], so, 0));
+  };
+  float cs[NV], amax[NV];
+#pragma unroll
+  for (int c = 0; c < NV; ++c) { cs[c] = 64.f; amax[c] = 0.f; }
+  // the last K-tile may run past K: A's k >= K would read the next row (B's planes are zero
+  // there, but an inf / nan in A would still poison the sums) -> zeroed
+  auto mask_tail = [&](int64_t kt) {
+    const int64_t k0 = kb + kt * BK;
+    if (k0 + BK <= K) return;
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      const int64_t lim = K - (k0 + ka[c]);
+      va[c].x = lim > 0 ? va[c].x : 0.f;
+      va[c].y = lim > 1 ? va[c].y : 0.f;
+      va[c].z = lim > 2 ? va[c].z : 0.f;
+      va[c].w = lim > 3 ? va[c].w : 0.f;
+    }
+  };
+  auto store = [&](char* st) {
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      const float4 v = va[c];
+      amax[c] = fmaxf(amax[c], fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+      uint32_t h0, l0, h1, l1;
+      split_mix(v.x, v.y, cs[c], h0, l0);
+      split_mix(v.z, v.w, cs[c], h1, l1);
+      *(uint2*)(st + oa[c]) = make_uint2(h0, h1);
+      *(uint2*)(st + PB + oa[c]) = make_uint2(l0, l1);
+    }
+#pragma unroll
+    for (int c = 0; c < NV; ++c) *(uint4*)(st + ob[c]) = vb[c];
+  };
+  load(0);
+  mask_tail(0);
+  if constexpr (SCALE > 0) {
+    // power-of-two row scale bringing the row's max |a| to [2^7, 2^8): the exact max over the
+    // whole row (SCALE 2: g.a_rowmax) or the first K-tile's (SCALE 1; a row's TPR staging lanes
+    // are adjacent)
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      float m;
+      if constexpr (SCALE == 2) {
+        const int64_t row = m0 + (tid + NT * c) / TPR;
+        m = row < g.M ? g.a_rowmax[row] : 0.f;
+      } else {
+        const float4 v = va[c];
+        m = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+#pragma unroll
+        for (int o = 1; o < TPR; o <<= 1) m = fmaxf(m, __shfl_xor(m, o));
+      }
+      int e = 0;
+      (void)frexpf(m, &e);
+      const float sc = (m > 0.f && m <= 3.0e38f) ? ldexpf(1.f, 8 - e) : 1.f;
+      cs[c] = 64.f * sc;
+      if ((tid % TPR) == 0) inv[(tid + NT * c) / TPR] = 1.f / sc;
+    }
+  } else if (tid < 256) {
+    inv[tid] = 1.f;
+  }
+  store(smem);
+  if (nk > 1) {
+    load(1);
+    mask_tail(1);
+  }
+  __syncthreads();
+  for (int64_t kt = 0; kt < nk; ++kt) {
+    const char* cur = smem + (kt & 1) * STAGE;
+    char* nxt = smem + ((kt & 1) ^ 1) * STAGE;
+#pragma unroll
+    for (int q = 0; q < BK / 16; ++q) {
+      f16x8 fa[MB][2], fb[NB][2];
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+#pragma unroll
+        for (int x = 0; x < MB; ++x)
+          fa[x][p] = *(const f16x8*)(cur + p * PB +
+                                     I::off(wm * (MB * 32) + x * 32 + (lane & 31), 16 * q + 8 * (lane >> 5)));
+#pragma unroll
+        for (int x = 0; x < NB; ++x)
+          fb[x][p] = *(const f16x8*)(cur + (2 + p) * PB +
+                                     I::off(wn * (NB * 32) + x * 32 + (lane & 31), 16 * q + 8 * (lane >> 5)));
+      }
+      if (q == 0) {
+        // tile kt + 1 (loaded during iteration kt - 1) into the other stage, then tile kt + 2's
+        // loads, then this tile's MFMAs
+        if (kt + 1 < nk) store(nxt);
+        if (kt + 2 < nk) {
+          load(kt + 2);
+          mask_tail(kt + 2);
+        }
+      }
+      // C^T = B^T A^T (lane = output row, see write_tile_t); small terms first
+#pragma unroll
+      for (int mi = 0; mi < MB; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NB; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][1], fa[mi][0], acc[mi][ni], 0, 0, 0);
+#pragma unroll
+      for (int mi = 0; mi < MB; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NB; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][0], fa[mi][1], acc[mi][ni], 0, 0, 0);
+#pragma unroll
+      for (int mi = 0; mi < MB; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NB; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][0], fa[mi][0], acc[mi][ni], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  bool bad = false;
+#pragma unroll
+  for (int c = 0; c < NV; ++c) {
+    float m = amax[c];
+#pragma unroll
+    for (int o = 1; o < TPR; o <<= 1) m = fmaxf(m, __shfl_xor(m, o));
+    const float s = cs[c] * (1.f / 64.f);
+    bad |= !(m * s <= 1023.f) || (m > 0.f && m * s < 0x1p-9f);
+  }
+  return bad;
+}
+
+template <int BK, int TAG>
+__global__ void __launch_bounds__(512, 1) gemm_f16p_kernel(GemmArgs g) {
+  using Cf = F16pCfg<BK>;
+  using C = X3Cfg<1>;
+  __shared__ __attribute__((aligned(16))) char smem[Cf::SMEM];
+  const int64_t T = g.tiles_m * g.tiles_n;
+  int64_t tm, tn, kb, K;
+  int tail_z = -1;
+  int64_t tail_ti = 0;
+  if (g.tail_s > 1 && (int64_t)blockIdx.x >= g.dp_blocks) {
+    const int64_t j = blockIdx.x - g.dp_blocks;
+    tail_ti = j % g.tail_rem;
+    tail_z = (int)(j / g.tail_rem);
+    const int64_t lin = g.dp_blocks + tail_ti;
+    tm = lin / g.tiles_n;
+    tn = lin - tm * g.tiles_n;
+    kb = tail_z * g.k_per_split;
+    K = min(g.K, kb + g.k_per_split);
+  } else if (g.tail_s > 1) {
+    tile_of(blockIdx.x, g.dp_blocks, g.tiles_n, tm, tn);
+    kb = 0;
+    K = g.K;
+  } else {
+    tile_of(blockIdx.x, T, g.tiles_n, tm, tn);
+    kb = blockIdx.z * g.k_per_split;
+    K = min(g.K, kb + g.k_per_split);
+  }
+  const int64_t m0 = tm * 256, n0 = tn * 256;
+  const float* __restrict__ A = g.A;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave / C::WGN, wn = wave % C::WGN;
+  floatx16 acc[C::MB][C::NB];
+#pragma unroll
+  for (int i = 0; i < C::MB; ++i)
+#pragma unroll
+    for (int j = 0; j < C::NB; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const char* hdr = (const char*)g.b_planes - kPlanesHeader;
+  if (K > kb) {
+    // a flagged weight tile (a B row whose residual plane would lose precision) goes to x3
+    const bool btile_bad = ((const uint32_t*)(hdr + 16))[tn] != 0;
+    bool x3 = btile_bad;
+    if (!btile_bad) {
+      // gradients (TAG 1, rows ~1e-7): scaled by their exact row max when given, else by the
+      // first K-tile's; activations (TAG 0) as they come
+      const bool bad =
+          TAG == 0 ? f16p_mainloop<BK, 0>(g, A, m0, n0, kb, K, smem, wm, wn, lane, acc)
+          : g.a_rowmax ? f16p_mainloop<BK, 2>(g, A, m0, n0, kb, K, smem, wm, wn, lane, acc)
+                       : f16p_mainloop<BK, 1>(g, A, m0, n0, kb, K, smem, wm, wn, lane, acc);
+      x3 = __syncthreads_or(bad);
+      const float* inv = (const float*)(smem + 2 * Cf::STAGE);
+      const float binv = ((const float*)hdr)[0];
+      const int lr = lane & 31;
+#pragma unroll
+      for (int i = 0; i < C::MB; ++i) {
+        const float ra = inv[wm * (C::MB * 32) + i * 32 + lr] * binv;
+#pragma unroll
+        for (int j = 0; j < C::NB; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] = x3 ? 0.f : acc[i][j][r] * ra;
+      }
+      __syncthreads();   // inv read before the fallback or the epilogue reuses the LDS
+    }
+    if (x3) {
+      if (threadIdx.x == 0 && g.fb_counter)
+        __hip_atomic_fetch_add(g.fb_counter, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      x3_mainloop<true, true, false, 1, 0>(g, A, g.B, m0, n0, kb, K, ceil_div(K - kb, C::BK),
+                                           smem, wm, wn, lane, acc);
+    }
+  }
+  write_tile_t<C::MB, C::NB, C::TBM, C::TBN>(g, acc, tail_z, tail_ti, m0, n0, wm, wn, lane);
+  if constexpr (TAG == 0)
+    if (g.s_part && tail_z < 0)
+      scores_tile<C::MB, C::NB, C::TBM, C::TBN, C::WGN>(g, acc, m0, n0, tn, wm, wn, lane, smem);
+}
+
+// ---- the weight gradient: g_W_aug = G_aug^T x (both operands row-contiguous, K = nodes) --------
+// f16x3 with G_aug's columns (the A rows) scaled by their exact max (gatx_absmax_rows_cols) to
+// [2^3, 2^4), which allows a third A plane carrying the main product's 2^11:
+//     A planes  Ah = fp16(s_m a),  Ah' = 2^11 Ah (exact, <= 2^15),  Al = fp16(2^11 (s_m a - Ah))
+//     B planes  Bh = fp16(b),      Bl = fp16(2^11 (b - Bh))          (x as it comes, any |x|)
+//     Ah' Bh + Ah Bl + Al Bh = 2^11 s_m a b            (dropped: Al Bl 2^-11, <= 2^-22 of it)
+// so B = x needs no scale (a column of x far below its peers keeps full precision down to
+// 2^-13, as the in-loop kernel's unscaled operands), and no register multiply precedes the MFMAs.
+// Staging as x3_mainloop's row-contiguous operands ([k][rows] plane images, fragments read
+// transposed by ds_read_b64_tr_b16). Range: every B row (a column of x over this K-slice) must have
+// max |b| <= 65504 and, unless zero, >= 2^-13; A rows (exactly scaled) only need to be finite. A
+// workgroup with any row outside recomputes its tile as x3.
+
+// (x, y) -> fp16_rn(x c) pair (one scale per element)
+__device__ inline uint32_t mix_pair(float x, float y, float cx, float cy) {
+  uint32_t h;
+  asm volatile(
+      "v_fma_mixlo_f16 %0, %1, %3, 0 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixhi_f16 %0, %2, %4, 0 op_sel_hi:[0,0,0]"
+      : "=&v"(h)
+      : "v"(x), "v"(y), "v"(cx), "v"(cy));
+  return h;
+}
+// fp16_rn(x c - 2^11 h) pair, h the fp16 pair already in hp (2^11 h taken exactly inside the mix)
+__device__ inline uint32_t mix_resid(float x, float y, float cx, float cy, uint32_t hp) {
+  uint32_t l;
+  float tx, ty;
+  const float m2048 = -2048.f;   // not an inline constant: a register operand
+  asm volatile(
+      "v_fma_mix_f32 %1, %5, %8, 0 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %2, %5, %8, 0 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixlo_f16 %0, %3, %6, %1 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixhi_f16 %0, %4, %7, %2 op_sel_hi:[0,0,0]"
+      : "=&v"(l), "=&v"(tx), "=&v"(ty)
+      : "v"(x), "v"(y), "v"(hp), "v"(cx), "v"(cy), "v"(m2048));
+  return l;
+}
+
+template <bool MASK>
+__device__ inline bool f16rc_mainloop(const GemmArgs& g, const float* __restrict__ A,
+                                      const float* __restrict__ B, int64_t m0, int64_t n0,
+                                      int64_t kb, int64_t K, int64_t nk, char* smem, int wm,
+                                      int wn, int lane, floatx16 (&acc)[4][2]) {
+  using C = X3Cfg<1>;
+  constexpr int NT = C::NT, BK = C::BK, MB = C::MB, NB = C::NB;
+  using TA = X3Tile<false, C::TBM, BK, NT>;
+  using TB = X3Tile<false, C::TBN, BK, NT>;
+  constexpr int PL = TA::Img::BYTES;   // bytes per plane (A and B images have the same size)
+  constexpr int STAGE = 5 * PL;        // A: Ah, Ah', Al; B: Bh, Bl
+  static_assert(TA::NV == 2 && TB::NV == 2, "256 x 16 row-contiguous tiles: 2 float4 per thread");
+  const int64_t M = g.M, N = g.N;
+  const int tid = threadIdx.x;
+  // this thread's 4 A rows (fixed over K: NT is a multiple of ROWS / 4) and their scales
+  const int ra = TA::row_of(tid);
+  float4 sc;
+  {
+    float s4[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t r = m0 + ra + j;
+      const float m = r < M ? g.a_rowmax[r] : 0.f;
+      int e = 0;
+      (void)frexpf(m, &e);
+      s4[j] = (m > 0.f && m <= 3.0e38f) ? ldexpf(1.f, 4 - e) : 1.f;   // max -> [2^3, 2^4)
+    }
+    sc = make_float4(s4[0], s4[1], s4[2], s4[3]);
+  }
+  float4 amax_a = make_float4(0.f, 0.f, 0.f, 0.f), amax_b = amax_a;
+  float4 va[2], vb[2];
+  const float* pa[2];
+  const float* pb[2];
+  int64_t sa = 0, sbs = 0;
+  if (!MASK) {
+    TA::setup(A, g.lda, m0, M, kb, pa, sa);
+    TB::setup(B, g.ldb, n0, N, kb, pb, sbs);
+  }
+  auto load = [&](int64_t k0) {
+    if (MASK) {
+      TA::T::template load<false>(A, g.lda, m0, M, k0, K, va);
+      TB::T::template load<false>(B, g.ldb, n0, N, k0, K, vb);
+    } else {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int64_t k = k0 + TA::k_of(tid + NT * c);
+        va[c] = *(const float4*)(k < K ? pa[c] : pa[c] - (k - kb) * g.lda);
+        pa[c] += sa;
+      }
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int64_t k = k0 + TB::k_of(tid + NT * c);
+        vb[c] = *(const float4*)(k < K ? pb[c] : pb[c] - (k - kb) * g.ldb);
+        pb[c] += sbs;
+      }
+    }
+  };
+  auto absmax4 = [](float4 m, float4 v) {
+    return make_float4(fmaxf(m.x, fabsf(v.x)), fmaxf(m.y, fabsf(v.y)), fmaxf(m.z, fabsf(v.z)),
+                       fmaxf(m.w, fabsf(v.w)));
+  };
+  // zero what lies outside the matrices (rows past M / N, k past K): only edge tiles
+  const bool edge_rows = MASK || m0 + C::TBM > M || n0 + C::TBN > N;
+  auto store = [&](char* st, int64_t k0) {
+    if (edge_rows || k0 + BK > K) {
+      TA::template mask<true, true>(va, m0, M, k0, K);
+      TB::template mask<true, true>(vb, n0, N, k0, K);
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int idx = tid + NT * c;
+      const int o = TA::Img::off(TA::row_of(idx), TA::k_of(idx));
+      const float4 v = va[c], w = vb[c];
+      amax_a = absmax4(amax_a, v);
+      amax_b = absmax4(amax_b, w);
+      // A: h = fp16(s a), h' = 2^11 h, l = fp16(2^11 (s a) - 2^11 h)
+      const uint32_t h0 = mix_pair(v.x, v.y, sc.x, sc.y), h1 = mix_pair(v.z, v.w, sc.z, sc.w);
+      const uint32_t l0 = mix_resid(v.x, v.y, 2048.f * sc.x, 2048.f * sc.y, h0);
+      const uint32_t l1 = mix_resid(v.z, v.w, 2048.f * sc.z, 2048.f * sc.w, h1);
+      const f16x2 k2048 = {(_Float16)2048.f, (_Float16)2048.f};
+      const uint32_t g0 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(f16x2, h0) * k2048);
+      const uint32_t g1 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(f16x2, h1) * k2048);
+      *(uint2*)(st + o) = make_uint2(h0, h1);
+      *(uint2*)(st + PL + o) = make_uint2(g0, g1);
+      *(uint2*)(st + 2 * PL + o) = make_uint2(l0, l1);
+      // B: h = fp16(b), l = fp16(2^11 b - 2^11 h)
+      const uint32_t b0 = mix_pair(w.x, w.y, 1.f, 1.f), b1 = mix_pair(w.z, w.w, 1.f, 1.f);
+      const uint32_t e0 = mix_resid(w.x, w.y, 2048.f, 2048.f, b0);
+      const uint32_t e1 = mix_resid(w.z, w.w, 2048.f, 2048.f, b1);
+      *(uint2*)(st + 3 * PL + o) = make_uint2(b0, b1);
+      *(uint2*)(st + 4 * PL + o) = make_uint2(e0, e1);
+    }
+  };
+  load(kb);
+  store(smem, kb);
+  __syncthreads();
+  for (int64_t kt = 0; kt < nk; ++kt) {
+    const char* cur = smem + (kt & 1) * STAGE;
+    char* nxt = smem + ((kt & 1) ^ 1) * STAGE;
+    const bool more = kt + 1 < nk;
+    if (more) load(kb + (kt + 1) * BK);
+    f16x8 fa[MB][3], fb[NB][2];
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int x = 0; x < MB; ++x)
+        fa[x][p] = __builtin_bit_cast(f16x8, TA::frag(cur + p * PL, wm * (MB * 32) + x * 32, 0, lane));
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int x = 0; x < NB; ++x)
+        fb[x][p] = __builtin_bit_cast(f16x8, TB::frag(cur + (3 + p) * PL, wn * (NB * 32) + x * 32, 0, lane));
+    // C^T = B^T A^T; small terms first: Ah Bl, Al Bh, then Ah' Bh
+#pragma unroll
+    for (int mi = 0; mi < MB; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NB; ++ni)
+        acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][1], fa[mi][0], acc[mi][ni], 0, 0, 0);
+#pragma unroll
+    for (int mi = 0; mi < MB; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NB; ++ni)
+        acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][0], fa[mi][2], acc[mi][ni], 0, 0, 0);
+#pragma unroll
+    for (int mi = 0; mi < MB; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NB; ++ni)
+        acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][0], fa[mi][1], acc[mi][ni], 0, 0, 0);
+    if (more) store(nxt, kb + (kt + 1) * BK);
+    __syncthreads();
+  }
+  // per-row range over this K-slice: a thread holds 4 rows at its k's; the 8 waves' lanes with the
+  // same lane index share rows -> LDS reduction
+  float* red = (float*)smem;   // [2][8][256]
+  const int w8 = tid >> 6;
+  *(float4*)&red[(0 * 8 + w8) * 256 + ra] = amax_a;
+  *(float4*)&red[(1 * 8 + w8) * 256 + ra] = amax_b;
+  __syncthreads();
+  bool bad = false;
+  if (tid < 256) {
+    float ma = 0.f, mb = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      ma = fmaxf(ma, red[w * 256 + tid]);
+      mb = fmaxf(mb, red[(8 + w) * 256 + tid]);
+    }
+    const float s = (m0 + tid < M) ? [&] {
+      const float m = g.a_rowmax[m0 + tid];
+      int e = 0;
+      (void)frexpf(m, &e);
+      return (m > 0.f && m <= 3.0e38f) ? ldexpf(1.f, 4 - e) : 1.f;
+    }() : 1.f;
+    bad = !(ma * s <= 31.f) || !(mb <= 65504.f) || (mb > 0.f && mb < 0x1p-13f);
+  }
+  bad = __syncthreads_or(bad);
+  return bad;
+}
+
+template <bool VEC>
+__global__ void __launch_bounds__(512, 1) gemm_f16rc_kernel(GemmArgs g) {
+  using C = X3Cfg<1>;
+  constexpr int SMEM = 2 * 5 * (256 * 16 * 2) > 2 * 3 * 2 * (256 + 256) * 16
+                           ? 2 * 5 * (256 * 16 * 2) : 2 * 3 * 2 * (256 + 256) * 16;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  int64_t tm, tn;
+  tile_of(blockIdx.x, g.tiles_m * g.tiles_n, g.tiles_n, tm, tn);
+  const int64_t kb = blockIdx.z * g.k_per_split;
+  const int64_t K = min(g.K, kb + g.k_per_split);
+  const int64_t m0 = tm * C::TBM, n0 = tn * C::TBN;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave / C::WGN, wn = wave % C::WGN;
+  floatx16 acc[C::MB][C::NB];
+#pragma unroll
+  for (int i = 0; i < C::MB; ++i)
+#pragma unroll
+    for (int j = 0; j < C::NB; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int64_t nk = K > kb ? ceil_div(K - kb, C::BK) : 0;
+  if (nk > 0) {
+    const bool x3 = f16rc_mainloop<!VEC>(g, g.A, g.B, m0, n0, kb, K, nk, smem, wm, wn, lane, acc);
+    // undo 2^11 and the A rows' scales (lane -> output row = A row, write_tile_t's layout)
+    const int lr = lane & 31;
+#pragma unroll
+    for (int i = 0; i < C::MB; ++i) {
+      const int64_t row = m0 + wm * (C::MB * 32) + i * 32 + lr;
+      float f = 0x1p-11f;
+      if (row < g.M) {
+        const float m = g.a_rowmax[row];
+        int e = 0;
+        (void)frexpf(m, &e);
+        f = (m > 0.f && m <= 3.0e38f) ? ldexpf(1.f, e - 4 - 11) : 0x1p-11f;
+      }
+#pragma unroll
+      for (int j = 0; j < C::NB; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = x3 ? 0.f : acc[i][j][r] * f;
+    }
+    if (x3) {
+      if (threadIdx.x == 0 && g.fb_counter)
+        __hip_atomic_fetch_add(g.fb_counter, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      x3_mainloop<false, false, !VEC, 1, 0>(g, g.A, g.B, m0, n0, kb, K, nk, smem, wm, wn, lane,
+                                            acc);
+    }
+  }
+  write_tile_t<C::MB, C::NB, C::TBM, C::TBN>(g, acc, -1, 0, m0, n0, wm, wn, lane);
+}
+
+// ---- weight planes (gatx_weight_planes) ---------------------------------------------------------
+// Header (kPlanesHeader bytes) then rows x prow bytes: row n = K_pad / 8 slots of 32 bytes, each
+// h[8] then l[8] (fp16), K_pad = round_up(K, 32), zero past K.
+
+__global__ void __launch_bounds__(256) planes_max_kernel(const float* __restrict__ W, int64_t rows,
+                                                         int64_t K, int64_t ld, uint32_t* gmax) {
+  float m = 0.f;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < rows * K; i += gridDim.x * 256ll) {
+    const int64_t r = i / K, k = i - r * K;
+    const float v = fabsf(W[r * ld + k]);
+    m = (v > m || v != v) ? (v != v ? __int_as_float(0x7f800000) : v) : m;   // nan -> inf
+  }
+  __shared__ float red[4];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    atomicMax(gmax, __float_as_uint(m));   // non-negative floats order as their bit patterns
+  }
+}
+
+// One wave per row: scale s_B from the global max, the row's max for its tile flag, the planes.
+__global__ void __launch_bounds__(256) planes_split_kernel(const float* __restrict__ W,
+                                                           int64_t rows, int64_t K, int64_t ld,
+                                                           char* __restrict__ planes) {
+  char* hdr = planes - kPlanesHeader;
+  const float gm = __uint_as_float(*(const uint32_t*)(hdr + 8));
+  int e = 0;
+  (void)frexpf(gm, &e);
+  const bool finite = gm <= 3.0e38f;
+  const float sB = (gm > 0.f && finite) ? ldexpf(1.f, 10 - e) : 1.f;
+  const float c = 32.f * sB;
+  const int64_t row = blockIdx.x * 4ll + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    ((float*)hdr)[0] = 0x1p-11f / sB;
+    ((float*)hdr)[1] = sB;
+  }
+  if (row >= rows) return;
+  const int64_t kpad = round_up(K, (int64_t)32);
+  const int64_t prow = kpad * 4;
+  const float* w = W + row * ld;
+  float m = 0.f;
+  for (int64_t k = lane; k < K; k += 64) m = fmaxf(m, fabsf(w[k]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  // a nonzero row whose residual plane would go subnormal (max s_B < 2^-8), or any non-finite
+  // value anywhere (the global max then is inf): the row's 256-row tile recomputes as x3
+  if (lane == 0 && (!finite || (m > 0.f && m * sB < 0x1p-8f)))
+    atomicOr((uint32_t*)(hdr + 16) + row / 256, 1u);
+  char* dst = planes + row * prow;
+  for (int64_t s = lane; s < kpad / 8; s += 64) {   // one 8-k slot per lane
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t k = 8 * s + j;
+      v[j] = k < K ? w[k] : 0.f;
+    }
+    uint32_t h[4], l[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) split_mix(v[2 * j], v[2 * j + 1], finite ? c : 0.f, h[j], l[j]);
+    uint4* d = (uint4*)(dst + s * 32);
+    d[0] = make_uint4(h[0], h[1], h[2], h[3]);
+    d[1] = make_uint4(l[0], l[1], l[2], l[3]);
+  }
+}
+
+// Exact max |x| per row and per column of X (rows x cols, row stride ld): one wave per row at a
+// time (the row's max by a wave reduction), every lane keeping its columns' running max over the
+// block's rows; the block's 4 waves combine in LDS, then one atomicMax per column (non-negative
+// floats order as their bit patterns; nan counts as inf). colmax must be zero on entry.
+constexpr int kStatRows = 128;   // rows per block
+__global__ void __launch_bounds__(256) absmax_rows_cols_kernel(const float* __restrict__ X,
+                                                               int64_t rows, int64_t cols,
+                                                               int64_t ld, float* rowmax,
+                                                               uint32_t* colmax) {
+  constexpr int CH = 8;                       // 256-column chunks held per lane (cols <= 2048)
+  __shared__ float red[4][CH * 256];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nch = (int)((cols + 255) / 256);
+  const bool vec = (ld % 4 == 0) && ((uintptr_t)X % 16 == 0);
+  float4 cm[CH];
+#pragma unroll
+  for (int j = 0; j < CH; ++j) cm[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto absn = [](float v) { return v != v ? __int_as_float(0x7f800000) : fabsf(v); };
+  const int64_t r0 = blockIdx.x * (int64_t)kStatRows;
+  for (int64_t r = r0 + wave; r < rows && r < r0 + kStatRows; r += 4) {
+    const float* x = X + r * ld;
+    float m = 0.f;
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      if (j >= nch) break;
+      const int64_t c = 256 * j + 4 * lane;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (vec && c + 3 < cols) {
+        v = *(const float4*)(x + c);
+      } else {
+        if (c < cols) v.x = x[c];
+        if (c + 1 < cols) v.y = x[c + 1];
+        if (c + 2 < cols) v.z = x[c + 2];
+        if (c + 3 < cols) v.w = x[c + 3];
+      }
+      v = make_float4(absn(v.x), absn(v.y), absn(v.z), absn(v.w));
+      cm[j] = make_float4(fmaxf(cm[j].x, v.x), fmaxf(cm[j].y, v.y), fmaxf(cm[j].z, v.z),
+                          fmaxf(cm[j].w, v.w));
+      m = fmaxf(m, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if (lane == 0) rowmax[r] = m;
+  }
+#pragma unroll
+  for (int j = 0; j < CH; ++j)
+    if (j < nch) *(float4*)&red[wave][256 * j + 4 * lane] = cm[j];
+  __syncthreads();
+  for (int c = threadIdx.x; c < cols; c += 256) {
+    const float v = fmaxf(fmaxf(red[0][c], red[1][c]), fmaxf(red[2][c], red[3][c]));
+    atomicMax(colmax + c, __float_as_uint(v));
+  }
+}
+
+}  // namespace
+
+int absmax_rows_cols(const float* X, int64_t rows, int64_t cols, int64_t ld, float* rowmax,
+                     float* colmax, hipStream_t stream) {
+  GATX_REQUIRE(cols <= 2048, "absmax_rows_cols: at most 2048 columns");
+  if (colmax) GATX_CALL(hipMemsetAsync(colmax, 0, cols * sizeof(float), stream));
+  if (rows == 0) return 0;
+  absmax_rows_cols_kernel<<<(unsigned)ceil_div(rows, (int64_t)kStatRows), 256, 0, stream>>>(
+      X, rows, cols, ld, rowmax, (uint32_t*)colmax);
+  GATX_LAUNCH_CHECK("absmax_rows_cols");
+  return 0;
+}
+
+size_t weight_planes_bytes(int64_t rows, int64_t K) {
+  return (size_t)kPlanesHeader + (size_t)rows * round_up(K, (int64_t)32) * 4;
+}
+
+int build_weight_planes(const float* W, int64_t rows, int64_t K, int64_t ld, void* buf,
+                        hipStream_t stream) {
+  GATX_REQUIRE(rows <= 60 * 256, "weight planes: at most 15360 rows (tile flags in the header)");
+  GATX_CALL(hipMemsetAsync(buf, 0, kPlanesHeader, stream));
+  char* planes = (char*)buf + kPlanesHeader;
+  const int64_t n = rows * K;
+  const unsigned gb = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, 256 * 8), 1024));
+  planes_max_kernel<<<gb, 256, 0, stream>>>(W, rows, K, ld, (uint32_t*)((char*)buf + 8));
+  GATX_LAUNCH_CHECK("weight_planes max");
+  planes_split_kernel<<<(unsigned)ceil_div(rows, (int64_t)4), 256, 0, stream>>>(W, rows, K, ld,
+                                                                               planes);
+  GATX_LAUNCH_CHECK("weight_planes split");
+  return 0;
+}
+
+// The weight-gradient kernel (row-contiguous A and B, split-K slabs; g.a_rowmax = the exact
+// max of every A row, i.e. of every G_aug column).
+int launch_gemm_f16rc(const gk::GemmArgs& g, hipStream_t stream) {
+  dim3 grid((unsigned)(g.tiles_m * g.tiles_n), 1u, (unsigned)g.splits);
+  if (g.a_vec && g.b_vec) gemm_f16rc_kernel<true><<<grid, 512, 0, stream>>>(g);
+  else gemm_f16rc_kernel<false><<<grid, 512, 0, stream>>>(g);
+  GATX_LAUNCH_CHECK("gemm_f16rc");
+  return 0;
+}
+
+// The pre-split kernel for GemmArgs prepared by gemm_impl; g.b_planes points at the planes (after
+// the header), g.B at the fp32 weight (the x3 recomputation of flagged tiles).
+int launch_gemm_f16p(const gk::GemmArgs& g, int tag, hipStream_t stream) {
+  const int64_t tiles = g.tiles_m * g.tiles_n;
+  const int64_t gx = g.tail_s > 1 ? g.dp_blocks + g.tail_rem * g.tail_s : tiles;
+  dim3 grid((unsigned)gx, 1u, (unsigned)g.splits);
+  static const int bk = [] {   // tuning only: GATX_F16P_BK=32
+    const char* e = getenv("GATX_F16P_BK");
+    return e && atoi(e) == 32 ? 32 : 16;
+  }();
+  if (bk == 32) {
+    if (tag == 0) gemm_f16p_kernel<32, 0><<<grid, 512, 0, stream>>>(g);
+    else gemm_f16p_kernel<32, 1><<<grid, 512, 0, stream>>>(g);
+  } else {
+    if (tag == 0) gemm_f16p_kernel<16, 0><<<grid, 512, 0, stream>>>(g);
+    else gemm_f16p_kernel<16, 1><<<grid, 512, 0, stream>>>(g);
+  }
+  GATX_LAUNCH_CHECK("gemm_f16p");
+  return 0;
+}
+
+}  // namespace gatx

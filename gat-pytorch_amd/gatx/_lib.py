@@ -86,6 +86,12 @@ SIGNATURES = {
     "gatx_get_gemm_mode": (c_i, []),
     "gatx_gemm_fallback_read": (c_i, [P, c_i, P]),
     "gatx_gemm_layout_mode": (c_i, [c_i, c_i]),
+    "gatx_weight_planes_bytes": (c_sz, [c_i64, c_i64]),
+    "gatx_weight_planes": (c_i, [P, c_i64, c_i64, c_i64, P, P]),
+    "gatx_gemm_planes": (c_i, [c_i64, c_i64, c_i64, P, c_i64, P, c_i64, P, P, c_i64, c_i64, P,
+                               c_i64, c_i64, P, c_i64, c_i, P, c_i, c_i, P, c_i, P, P, c_sz, P]),
+    "gatx_absmax_rows_cols": (c_i, [P, c_i64, c_i64, c_i64, P, P, P]),
+    "gatx_gemm_wgrad": (c_i, [c_i64, c_i64, c_i64, P, c_i64, P, c_i64, P, P, c_i64, P, c_sz, P]),
     "gatx_gemm_splitk_workspace_bytes": (c_sz, [c_i64, c_i64, c_i64]),
     "gatx_gemm_f32_splitk": (c_i, [c_i64, c_i64, c_i64, P, c_i64, c_i64, P, c_i64, c_i64, P, c_i64,
                                    c_i, P, c_sz, P]),

@@ -25,11 +25,19 @@ import torch
 
 class CapturedStep:
     """Capture `fn()` into a hipGraph after `warmup` eager runs on a side stream (which settle the
-    caching allocator and every lazy init); each call replays it and returns the static output."""
+    caching allocator and every lazy init); each call replays it and returns the static output.
+
+    The warm-ups and the capture run on the SAME side stream (`self.stream`): a training step's
+    autograd graph can outlive the step (GATLayer keeps its last alpha, as the reference's
+    `normalised_attention_coeffs` does, and that tensor holds the graph), and with it the
+    parameters' AccumulateGrad nodes, which remember the stream they were created on. Capturing
+    on another stream than the warm-ups would make the captured backward accumulate across
+    streams (torch warns: extra synchronisation, and it can break capture). `eager()` runs the
+    step outside the graph on that same stream (e.g. HIP-event-instrumented steps)."""
 
     def __init__(self, fn, warmup: int = 2, pool=None):
         self.fn = fn
-        s = torch.cuda.Stream()
+        self.stream = s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(warmup):
@@ -37,12 +45,22 @@ class CapturedStep:
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph, pool=pool):
+        with torch.cuda.graph(self.graph, pool=pool, stream=s):
             self.out = fn()
 
     def __call__(self):
         self.graph.replay()
         return self.out
+
+    def eager(self):
+        """One un-captured run of the step on the capture stream, ordered after everything
+        already enqueued on the current stream (and the current stream after it)."""
+        cur = torch.cuda.current_stream()
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            out = self.fn()
+        cur.wait_stream(self.stream)
+        return out
 
     def reset(self):
         self.graph.reset()

@@ -201,6 +201,55 @@ def augmented_weight(W, a, sh: "LayerShape", skip_W=None):
     return W_aug
 
 
+def use_weight_planes(rows: int, k: int, m: int) -> bool:
+    """Whether a GEMM with this weight operand takes the pre-split f16x3 kernel (gemm_f16p.hip):
+    the f16x3 arithmetic, float4-aligned rows, and outputs big enough for its 256 x 256 tiles (the
+    library makes the final choice; planes it does not use cost one small build per weight
+    version). GATX_F16P=0: never build them."""
+    if _env_int("GATX_F16P", 1) == 0 or lib.gatx_get_gemm_mode() != 2:
+        return False
+    return k % 4 == 0 and rows >= 256 and m >= 256
+
+
+def use_wgrad_f16(M: int, N: int, K: int) -> bool:
+    """Whether the weight gradient G_aug^T x (M = K_aug rows, N = F_in, K = nodes) takes the
+    row-contiguous f16x3 kernel (gemm_f16p.hip, scales from G_aug's exact column maxima): the
+    f16x3 arithmetic and an output its 256 x 256 tiles cover (the library decides finally; the
+    statistics pass is then only wasted work). GATX_F16P=0: never."""
+    if _env_int("GATX_F16P", 1) == 0 or lib.gatx_get_gemm_mode() != 2:
+        return False
+    return M >= 256 and N >= 256 and M <= 2048 and N % 4 == 0
+
+
+def build_weight_planes(W, rows: int, k: int, ld: int):
+    """fp16 planes of the weight W (rows x k, row stride ld) for gatx_gemm_planes: one 256-byte
+    aligned buffer (header + planes), built on the current stream."""
+    nb = lib.gatx_weight_planes_bytes(rows, k)
+    buf = torch.empty(nb + 256, dtype=torch.uint8, device=W.device)
+    off = (-ptr(buf)) % 256
+    planes = buf[off:off + nb]
+    call("gatx_weight_planes", ptr(W), rows, k, ld, ptr(planes), stream())
+    return planes
+
+
+def projection_planes(W_aug, sh: "LayerShape", N: int):
+    """The planes of the projection weight W_aug ([K_aug + C] x F_in), cached beside W_aug (same
+    key, same lifetime) in no-grad use, rebuilt with it in training; None when the pre-split
+    kernel would not take the GEMM."""
+    rows = sh.K_aug + sh.skip_cols
+    if not use_weight_planes(rows, sh.F_in, N):
+        return None
+    if sh.cache_weights and _WAUG_CACHE is not None:
+        for key, val in _WAUG_CACHE.items():
+            if val[2] is W_aug:
+                if len(val) > 4:
+                    return val[4]
+                planes = build_weight_planes(W_aug, rows, sh.F_in, sh.F_in)
+                _WAUG_CACHE[key] = val[:4] + (planes,)
+                return planes
+    return build_weight_planes(W_aug, rows, sh.F_in, sh.F_in)
+
+
 def _attention_alpha(graph: Graph, S, M_ord, den, sh: "LayerShape", alpha, argmax, s):
     """alpha in edge_index' order (models/gat_layer.py:106-110): iterates edge_index' itself, so
     both its reads and the alpha writes are coalesced; |edge_index'| is read on the device."""
@@ -492,24 +541,28 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
         return out, alpha, saved
     Wh = torch.empty((N, sh.Dp), **f32)
     S = torch.empty((N, max(sh.H2, 1)), **f32)
+    # the weight operand pre-split into fp16 planes (gemm_f16p.hip; None: in-loop split)
+    planes = projection_planes(W_aug, sh, N)
+    pp = ptr(planes) if planes is not None else None
+    saved["planes"] = planes
     if C:   # one launch: [Wh | S | R] = x [W_aug; W_skip_eff]^T into three outputs
         with _span("gemm", (N, sh.K_aug + C, sh.F_in, sh.NH, sh.F)):
-            call("gatx_projection_gemm3", N, sh.K_aug + C, sh.F_in, ptr(x), sh.F_in, 1,
-                 ptr(W_aug), 1, sh.F_in, ptr(Wh), sh.Dp, sh.Dp, ptr(S), max(sh.H2, 1), sh.K_aug,
-                 ptr(R), C, *gemm_workspace(N, sh.K_aug + C, sh.F_in, dev), s)
+            call("gatx_gemm_planes", N, sh.K_aug + C, sh.F_in, ptr(x), sh.F_in, ptr(W_aug),
+                 sh.F_in, pp, ptr(Wh), sh.Dp, sh.Dp, ptr(S), max(sh.H2, 1), sh.K_aug, ptr(R), C,
+                 0, None, 0, 0, None, 0, None, *gemm_workspace(N, sh.K_aug + C, sh.F_in, dev), s)
     elif fold_scores_into_gemm(sh):
         with _span("gemm", (N, sh.K_aug, sh.F_in, sh.NH, sh.F)):
-            call("gatx_projection_gemm", N, sh.K_aug, sh.F_in, ptr(x), sh.F_in, 1, ptr(W_aug), 1,
-                 sh.F_in, ptr(Wh), sh.Dp, sh.Dp, ptr(S), max(sh.H2, 1),
-                 *gemm_workspace(N, sh.K_aug, sh.F_in, dev), s)
+            call("gatx_gemm_planes", N, sh.K_aug, sh.F_in, ptr(x), sh.F_in, ptr(W_aug), sh.F_in,
+                 pp, ptr(Wh), sh.Dp, sh.Dp, ptr(S), max(sh.H2, 1), -1, None, 0, 0, None, 0, 0,
+                 None, 0, None, *gemm_workspace(N, sh.K_aug, sh.F_in, dev), s)
     elif _env_int("GATX_FUSED_SCORES", 1):
         # S reduced from the projection's accumulators in its epilogue (no second read of Wh)
         with _span("gemm", (N, sh.Dp, sh.F_in, sh.NH, sh.F)):
             nb = lib.gatx_projection_scores_workspace_bytes(N, sh.Dp, sh.F_in, sh.NH)
             ws = torch.empty(max(nb, 1), dtype=torch.uint8, device=dev)
-            call("gatx_projection_gemm_scores", N, sh.Dp, sh.F_in, ptr(x), sh.F_in, 1,
-                 ptr(W_aug), 1, sh.F_in, ptr(Wh), sh.Dp, ptr(a), sh.NH, sh.F, ptr(S), ptr(ws),
-                 nb, s)
+            call("gatx_gemm_planes", N, sh.Dp, sh.F_in, ptr(x), sh.F_in, ptr(W_aug), sh.F_in, pp,
+                 ptr(Wh), sh.Dp, sh.Dp, None, 0, -1, None, 0, 0, ptr(a), sh.NH, sh.F, ptr(S), 0,
+                 None, ptr(ws), nb, s)
     else:
         with _span("gemm", (N, sh.Dp, sh.F_in, sh.NH, sh.F)):
             call("gatx_projection_gemm", N, sh.Dp, sh.F_in, ptr(x), sh.F_in, 1, ptr(W_aug), 1,
@@ -611,16 +664,36 @@ def layer_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShape, 
         with _span("bwd_colsum", binfo):
             call("gatx_colsum", src_p, N, sh.out_cols, src_ld, ptr(g_bias), s)
     fold = resid_is_x and need_x and g_pre is not None
+    # exact max |.| of G_aug's rows (the g_x GEMM's row scales) and columns (the weight-gradient
+    # GEMM's), from ONE read of G_aug (gatx_absmax_rows_cols); computed on first use
+    stats_box = []
+
+    def g_aug_stats():
+        if not stats_box:
+            rowmax = torch.empty(N, **f32)
+            colmax = torch.empty(KC, **f32) if KC <= 2048 else None
+            with _span("bwd_gaug_stats", binfo):
+                call("gatx_absmax_rows_cols", ptr(G_aug), N, KC, ldg, ptr(rowmax),
+                     ptr(colmax) if colmax is not None else None, s)
+            stats_box.append((rowmax, colmax))
+        return stats_box[0]
     if need_x:
         g_x = g_pre if fold else torch.empty((N, sh.F_in), **f32)
         with _span("bwd_gemm_gx", binfo + (bool(fold),)):
             if N * sh.F_in * KC >= (1 << 27):
                 # W_aug^T (F_in x K_aug, 4 MB at PPI): both GEMM operands k-contiguous (the
-                # n-contiguous B staging of W_aug as stored ran this product ~25% slower)
+                # n-contiguous B staging of W_aug as stored ran this product ~25% slower), and
+                # pre-split into fp16 planes for the f16x3 kernel (gemm_f16p.hip)
                 W_augT = torch.empty((sh.F_in, ldg), **f32)
                 call("gatx_transpose_f32", KC, sh.F_in, ptr(W_aug), sh.F_in, ptr(W_augT), ldg, s)
-                call("gatx_gemm_f32", N, sh.F_in, KC, ptr(G_aug), ldg, 1, ptr(W_augT), 1,
-                     ldg, ptr(g_x), sh.F_in, sh.F_in, None, 0, int(fold),
+                planes_t = None
+                if use_weight_planes(sh.F_in, KC, N):
+                    planes_t = build_weight_planes(W_augT, sh.F_in, KC, ldg)
+                    stats = g_aug_stats()
+                call("gatx_gemm_planes", N, sh.F_in, KC, ptr(G_aug), ldg, ptr(W_augT), ldg,
+                     ptr(planes_t) if planes_t is not None else None, ptr(g_x), sh.F_in,
+                     sh.F_in, None, 0, -1, None, 0, int(fold), None, 0, 0, None, 1,
+                     ptr(stats[0]) if planes_t is not None else None,
                      *gemm_workspace(N, sh.F_in, KC, dev), s)
             else:   # small layers are launch-bound: read W_aug as stored (no transpose launch)
                 call("gatx_gemm_f32", N, sh.F_in, KC, ptr(G_aug), ldg, 1, ptr(W_aug), sh.F_in,
@@ -630,9 +703,15 @@ def layer_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShape, 
         gW_aug = torch.empty((KC, sh.F_in), **f32)
         ws_bytes = lib.gatx_gemm_splitk_workspace_bytes(KC, sh.F_in, N)
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+        # the f16x3 weight-gradient kernel needs G_aug's exact column maxima
+        colmax = g_aug_stats()[1] if use_wgrad_f16(KC, sh.F_in, N) else None
         with _span("bwd_gemm_gw", binfo):
-            call("gatx_gemm_f32_splitk", KC, sh.F_in, N, ptr(G_aug), 1, ldg, ptr(x),
-                 sh.F_in, 1, ptr(gW_aug), sh.F_in, 0, ptr(ws), ws_bytes, s)
+            if colmax is not None:
+                call("gatx_gemm_wgrad", KC, sh.F_in, N, ptr(G_aug), ldg, ptr(x), sh.F_in,
+                     ptr(colmax), ptr(gW_aug), sh.F_in, ptr(ws), ws_bytes, s)
+            else:
+                call("gatx_gemm_f32_splitk", KC, sh.F_in, N, ptr(G_aug), 1, ldg, ptr(x),
+                     sh.F_in, 1, ptr(gW_aug), sh.F_in, 0, ptr(ws), ws_bytes, s)
         g_W = torch.empty_like(W)
         g_a = torch.empty_like(a) if a is not None else None
         with _span("bwd_weight_grads", binfo):

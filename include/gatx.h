@@ -136,6 +136,46 @@ int gatx_transpose_f32(int64_t rows, int64_t cols, const float* src, int64_t ld_
  * 0 = "f32": v_mfma_f32_32x32x2_f32. */
 void gatx_set_gemm_mode(int mode);
 int gatx_get_gemm_mode(void);
+/* Pre-split weight planes for the f16x3 GEMMs (gemm_f16p.hip): W (rows x K, row stride ld) as two
+ * fp16 planes per element with one power-of-two scale for the whole matrix, plus a 256-byte
+ * header (the scale and per-256-row-tile range flags). Built once per weight version (the
+ * projection's W_aug, the backward's W_aug^T) and passed to gatx_gemm_planes; the buffer
+ * (gatx_weight_planes_bytes) must be 256-byte aligned. Replaces nothing in the reference: it is
+ * how `self.W(x)` (models/gat_layer.py:64) keeps fp32 accuracy on the fp16 matrix cores. */
+size_t gatx_weight_planes_bytes(int64_t rows, int64_t K);
+int gatx_weight_planes(const float* W, int64_t rows, int64_t K, int64_t ld, void* planes,
+                       gatx_stream_t stream);
+/* C = A . B^T for k-contiguous A (M x K, row stride lda) and B (N x K, row stride ldb) with B's
+ * planes from gatx_weight_planes (NULL: the in-loop split kernel), into up to three column
+ * ranges as gatx_projection_gemm3 (C0 below n_split, C1 below n_split2, C2 beyond), optionally
+ * accumulating into C0. a != NULL: the forward projection with the node scores fused, exactly
+ * gatx_projection_gemm_scores (then C0 is the packed Wh and the only output). gradient != 0:
+ * A is a gradient (G_aug): its rows are scaled into the fp16 range (models/gat_layer.py:64's
+ * backward, g_x = G_aug W_aug), by its exact max a_rowmax[row] when given (NULL: by its first
+ * K-tile's). Shapes the pre-split kernel does not take (other arithmetic modes, unaligned rows,
+ * small outputs) run the regular kernels with the same result. */
+int gatx_gemm_planes(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                     const float* B, int64_t ldb, const void* b_planes, float* C0, int64_t ldc0,
+                     int64_t n_split, float* C1, int64_t ldc1, int64_t n_split2, float* C2,
+                     int64_t ldc2, int accumulate, const float* a, int NH, int F, float* S,
+                     int gradient, const float* a_rowmax, void* workspace,
+                     size_t workspace_bytes, gatx_stream_t stream);
+/* The weight gradient C (M x N) = A^T-layout product for row-contiguous A (element (m, k) at
+ * A[k * lda + m]) and B (element (n, k) at B[k * ldb + n]): g_W_aug = G_aug^T x with M = the
+ * G_aug columns, K = the nodes (models/gat_layer.py:64's weight gradient). a_rowmax[m] = the
+ * exact max |A row m| (gatx_absmax_rows_cols' colmax of G_aug): f16x3 arithmetic with those
+ * rows scaled into the fp16 range (gemm_f16p.hip); split-K slabs in the workspace
+ * (gatx_gemm_splitk_workspace_bytes), summed in a fixed order. Other arithmetic modes / shapes
+ * run the x3 / f32 kernels with the same result. */
+int gatx_gemm_wgrad(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                    const float* B, int64_t ldb, const float* a_rowmax, float* C, int64_t ldc,
+                    void* workspace, size_t workspace_bytes, gatx_stream_t stream);
+/* Exact max |x| of every row (rowmax[rows]) and, when colmax != NULL, every column
+ * (colmax[cols], cols <= 2048; nan counts as inf) of X (rows x cols, row stride ld): the
+ * per-row / per-column power-of-two scales of the f16x3 gradient GEMMs (G_aug's rows for
+ * g_x = G_aug W_aug, its columns for g_W_aug = G_aug^T x), in one read of G_aug. */
+int gatx_absmax_rows_cols(const float* X, int64_t rows, int64_t cols, int64_t ld, float* rowmax,
+                          float* colmax, gatx_stream_t stream);
 /* The arithmetic (2 f16x3, 1 x3, 0 f32) the tiled GEMMs run for an operand layout: a_kc / b_kc
  * = whether A's rows / B's columns are k-contiguous (the weight gradient G_aug^T x has neither). */
 int gatx_gemm_layout_mode(int a_kc, int b_kc);

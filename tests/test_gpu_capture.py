@@ -79,10 +79,15 @@ def test_captured_pattern_train_step_equals_eager(device):
     s1 = make_step(m1, o1)
     losses = [float(s1()) for _ in range(2 + 6)]   # CapturedStep warms up twice, then 6 replays
     m2, o2 = make()
-    cap = CapturedStep(make_step(m2, o2), warmup=2)   # capture itself runs no step
-    for _ in range(6):
-        last = cap()
-    torch.cuda.synchronize()
+    import warnings
+    with warnings.catch_warnings():
+        # the captured backward must accumulate on the stream that created the AccumulateGrad
+        # nodes (CapturedStep: warm-ups and capture on one stream), not across streams
+        warnings.filterwarnings("error", message=".*AccumulateGrad node's stream")
+        cap = CapturedStep(make_step(m2, o2), warmup=2)   # capture itself runs no step
+        for _ in range(6):
+            last = cap()
+        torch.cuda.synchronize()
     # capture ran the step once more (the captured pass's own work is not executed at capture),
     # so the 6 replays are steps 3..8, like the eager run's last six
     assert abs(float(last) - losses[-1]) <= 1e-6 * max(1.0, abs(losses[-1]))

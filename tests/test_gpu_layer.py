@@ -774,3 +774,152 @@ def test_model_backward_vs_oracle(name, device):
             r = ref["skip"][j]
             err = np.abs(s.weight.grad.cpu().numpy() - r).max()
             assert err <= tol * max(1.0, np.abs(r).max()), (name, "skip", j, err)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gradient", [0, 1])
+def test_gemm_f16p_accuracy(gradient, device):
+    """The pre-split f16x3 kernel (gemm_f16p.hip: the weight operand as fp16 planes from
+    gatx_weight_planes, the activation / gradient split in the loop) against float64 beside the
+    fp32-MFMA kernel on the same data: error relative to sum|a||b| at the fp32 GEMM's level
+    (<= 1.25x f32's) on the projection / g_x shapes, partial K-tiles (K = 1032), ragged M and N,
+    tail-split waves, operands of any scale (gradients ~1e-7 and 1e4 rows scaled per row; a
+    weight 1e-12 below its matrix max, whose residual plane would be subnormal, flags its tile
+    for the x3 recomputation), rows growing 10^6-fold along K (x3 recomputation), three output
+    ranges and the accumulate epilogue; results bitwise repeatable and equal with the planes
+    cached or rebuilt; the fallback counter counts exactly the recomputed workgroups."""
+    from gatx._lib import call, lib, ptr, stream
+    from gatx.functional import build_weight_planes, gemm_workspace
+    torch.manual_seed(12)
+    lib.gatx_set_gemm_mode(2)
+    fb = torch.zeros(1, dtype=torch.int64, device=device)
+    # (256 x 256 tiles need N within 15% of a multiple of 256, else the in-loop kernel runs)
+    cases = [(4490, 1024, 1024, 1.0, 1.0), (3000, 744, 1024, 1.0, 1.0),
+             (2000, 1024, 1032, 1e-7, 1.0), (1900, 768, 1100, 1e4, 1.0),
+             (700, 1024, 512, "ramp", 1.0), (1000, 1024, 256, 1.0, "tiny_row"),
+             (2100, 512, 96, 1.0, 1e-3)]
+    for (M, N, K, amp, bamp) in cases:
+        if amp == "ramp":
+            A = torch.randn(M, K, device=device) * torch.logspace(-3, 3, K, device=device)
+        else:
+            A = torch.randn(M, K, device=device) * torch.rand(M, 1, device=device) * amp
+        B = (torch.rand(N, K, device=device) * 2 - 1) * 0.05
+        if bamp == "tiny_row":
+            B[7] *= 1e-12
+        else:
+            B = B * bamp
+        ref = A.double() @ B.double().t()
+        S = (A.double().abs() @ B.double().abs().t()).clamp_min(1e-30)
+        planes = build_weight_planes(B, N, K, K)
+        # gradients: rows scaled by their exact max (gatx_absmax_rows_cols) or, for the ramp,
+        # by their first K-tile's (which the later tiles overflow: x3 recomputation)
+        exact = gradient and amp != "ramp"
+        rowmax = torch.empty(M, device=device)
+        call("gatx_absmax_rows_cols", ptr(A), M, K, K, ptr(rowmax), None, stream())
+        rel = {}
+        for mode in (0, 2):
+            lib.gatx_set_gemm_mode(mode)
+            outs = []
+            for _ in range(2):
+                C = torch.full((M, N), float("nan"), device=device)
+                call("gatx_gemm_fallback_read", ptr(fb), 1, stream())
+                call("gatx_gemm_planes", M, N, K, ptr(A), K, ptr(B), K,
+                     ptr(planes) if mode == 2 else None, ptr(C), N, N, None, 0, -1, None, 0, 0,
+                     None, 0, 0, None, gradient, ptr(rowmax) if exact else None,
+                     *gemm_workspace(M, N, K, device), stream())
+                outs.append(C)
+            torch.cuda.synchronize()
+            assert torch.equal(outs[0], outs[1]), (M, N, K, mode)
+            rel[mode] = ((outs[0].double() - ref).abs() / S).max().item()
+            if mode == 2:
+                call("gatx_gemm_fallback_read", ptr(fb), 1, stream())
+                n_fb = int(fb.item())
+                if amp == "ramp" or bamp == "tiny_row":
+                    assert n_fb > 0, (M, N, K, amp, bamp)
+        lib.gatx_set_gemm_mode(2)
+        r = rel[2]
+        assert r <= max(1.25 * rel[0], 2e-7) and r < 1e-6, (M, N, K, amp, bamp, rel)
+    # three output ranges + accumulate (g_x with the identity-skip gradient folded in)
+    M, N, K = 1200, 1032, 1024
+    A = torch.randn(M, K, device=device)
+    B = (torch.rand(N, K, device=device) * 2 - 1) * 0.05
+    planes = build_weight_planes(B, N, K, K)
+    C0 = torch.randn(M, 1000, device=device)
+    C1 = torch.randn(M, 24, device=device)
+    C2 = torch.randn(M, 8, device=device)
+    init = torch.cat([C0, C1, C2], 1).double()   # accumulate applies to every output range
+    call("gatx_gemm_planes", M, N, K, ptr(A), K, ptr(B), K, ptr(planes), ptr(C0), 1000, 1000,
+         ptr(C1), 24, 1024, ptr(C2), 8, 1, None, 0, 0, None, gradient, None,
+         *gemm_workspace(M, N, K, device), stream())
+    torch.cuda.synchronize()
+    ref = A.double() @ B.double().t()
+    S = A.double().abs() @ B.double().abs().t()
+    got = torch.cat([C0, C1, C2], 1).double() - init
+    assert ((got - ref).abs() / S).max().item() < 1e-6
+
+
+@pytest.mark.gpu
+def test_absmax_rows_cols(device):
+    """gatx_absmax_rows_cols: exact per-row and per-column max |x| (nan as inf), any ld, ragged
+    shapes (the scales of the f16x3 gradient GEMMs)."""
+    from gatx._lib import call, ptr, stream
+    torch.manual_seed(13)
+    for rows, cols, ld in ((44900, 1036, 1036), (300, 13, 17), (1, 2048, 2048), (129, 756, 760)):
+        X = torch.randn(rows, ld, device=device) * torch.logspace(-8, 3, ld, device=device)
+        if rows > 10:
+            X[7, 3] = float("nan")
+        rm = torch.empty(rows, device=device)
+        cm = torch.full((cols,), -1.0, device=device)
+        call("gatx_absmax_rows_cols", ptr(X), rows, cols, ld, ptr(rm), ptr(cm), stream())
+        A = X[:, :cols].abs().nan_to_num(nan=float("inf"))
+        assert torch.equal(rm, A.max(1).values)
+        assert torch.equal(cm, A.max(0).values)
+
+
+@pytest.mark.gpu
+def test_gemm_wgrad_accuracy(device):
+    """The f16x3 weight-gradient kernel (gatx_gemm_wgrad: g_W_aug = G_aug^T x, both operands
+    row-contiguous, K = nodes, split-K; G_aug's columns scaled by their exact maxima from
+    gatx_absmax_rows_cols) against float64 beside the fp32-MFMA kernel: <= 1.25x f32's error
+    relative to sum|a||b| on the PPI shapes, with gradient columns spanning 1e-9 .. 1e3 and
+    ragged K; an x column below 2^-13 throughout (a dead feature) takes the x3 recomputation
+    (counted) and stays exact; repeated launches are bitwise identical."""
+    from gatx._lib import call, lib, ptr, stream
+    torch.manual_seed(14)
+    fb = torch.zeros(1, dtype=torch.int64, device=device)
+    for (KC, F_in, N, case) in ((1032, 1024, 44900, "ppi_l1"), (756, 1024, 9001, "ppi_l2"),
+                                (1032, 1024, 20000, "dead_feature")):
+        G = torch.randn(N, KC, device=device) * 1e-6
+        G[:, :KC // 3] *= torch.logspace(-3, 3, KC // 3, device=device)   # 1e-9 .. 1e-3
+        G[:, -8:] *= 1e9                                                   # score columns ~1e3
+        x = torch.nn.functional.elu(torch.randn(N, F_in, device=device))
+        if case == "dead_feature":
+            x[:, 5] = 1e-6 * torch.rand(N, device=device)
+        ldg = (KC + 3) // 4 * 4
+        Gp = torch.zeros(N, ldg, device=device)
+        Gp[:, :KC] = G
+        ref = Gp[:, :KC].double().t() @ x.double()
+        S = (Gp[:, :KC].double().abs().t() @ x.double().abs()).clamp_min(1e-300)
+        rowmax = torch.empty(N, device=device)
+        colmax = torch.empty(KC, device=device)
+        call("gatx_absmax_rows_cols", ptr(Gp), N, KC, ldg, ptr(rowmax), ptr(colmax), stream())
+        wsb = lib.gatx_gemm_splitk_workspace_bytes(KC, F_in, N)
+        ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=device)
+        rel = {}
+        for mode in (0, 2):
+            lib.gatx_set_gemm_mode(mode)
+            outs = []
+            for _ in range(2):
+                C = torch.full((KC, F_in), float("nan"), device=device)
+                call("gatx_gemm_fallback_read", ptr(fb), 1, stream())
+                call("gatx_gemm_wgrad", KC, F_in, N, ptr(Gp), ldg, ptr(x), F_in, ptr(colmax),
+                     ptr(C), F_in, ptr(ws), wsb, stream())
+                call("gatx_gemm_fallback_read", ptr(fb), 1, stream())
+                outs.append(C)
+            torch.cuda.synchronize()
+            assert torch.equal(outs[0], outs[1]), (case, mode)
+            rel[mode] = ((outs[0].double() - ref).abs() / S).max().item()
+            if mode == 2:
+                assert (int(fb.item()) > 0) == (case == "dead_feature"), (case, int(fb.item()))
+        lib.gatx_set_gemm_mode(2)
+        assert rel[2] <= max(1.25 * rel[0], 2e-7) and rel[2] < 1e-6, (case, rel)

@@ -1,0 +1,265 @@
+// GEMM lab (tuning only, not part of libgatx.so): an f16x3 mainloop with the weight operand
+// pre-split into fp16 planes and the activation split in the loop by v_fma_mix, the hi planes
+// carrying the 2^11 factor (A x 64, B x 32), so the MFMA phase has no scaling multiplies.
+//   C[M][N] = A[M][K] . B[N][K]^T, A fp32 k-contiguous, B given as planes (lab_split_b).
+// Built standalone (tools/gemm_lab/build.sh) and timed against the library kernel by
+// tools/gemm_lab/run_lab.py.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int TBM = 256, TBN = 256, NT = 512, WGM = 2, WGN = 4, MB = 4, NB = 2;
+
+// One fp16 plane image of 256 rows x BK k: 16-byte (8-k) slots, slot-major; odd slots' rows XOR'd
+// by 12 (conflict-free ds_read_b128 fragment reads, as gemm_x3.hip's PlaneImg).
+template <int BK>
+struct Img {
+  static constexpr int BYTES = 256 * BK * 2;
+  static __device__ inline int off(int r, int k) {
+    const int s = k >> 3;
+    return s * (256 * 16) + ((r ^ ((s & 1) * 12)) << 4) + ((k & 4) << 1);
+  }
+};
+
+__device__ inline __amdgpu_buffer_rsrc_t rsrc(const void* base, int64_t bytes) {
+  const int nr = (int)(bytes > 0x7fffffff ? 0x7fffffff : bytes);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, nr, 0x00020000);
+}
+
+// h = fp16_rn(x c), l = fp16_rn(x c - h) for a pair (x in the low halves): four v_fma_mix.
+__device__ inline void split_mix(float x, float y, float c, uint32_t& h, uint32_t& l) {
+  asm volatile(
+      "v_fma_mixlo_f16 %0, %2, %4, 0 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixhi_f16 %0, %3, %4, 0 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixlo_f16 %1, %2, %4, -%0 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %1, %3, %4, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(h), "=&v"(l)
+      : "v"(x), "v"(y), "v"(c));
+}
+
+__device__ inline void tile_of(int64_t b, int64_t T, int64_t tiles_n, int64_t& tm, int64_t& tn) {
+  const int64_t q = T / 8, r = T % 8;
+  const int64_t xcd = b % 8, j = b / 8;
+  const int64_t t = (xcd < r) ? xcd * (q + 1) + j : r * (q + 1) + (xcd - r) * q + j;
+  tm = t / tiles_n;
+  tn = t % tiles_n;
+}
+
+struct LabArgs {
+  const float* A; int64_t lda;
+  const uint16_t* Bp; int64_t brow;   // planes: row n at Bp + n * brow bytes: [K/8][2][8] fp16
+  int64_t M, N, K;
+  float* C; int64_t ldc;
+  float binv;                          // 2^-11 / sB
+  int* bad;                            // rows out of the fp16 range seen (lab: counted only)
+};
+
+template <int BK, bool SCALE>
+__global__ void __launch_bounds__(NT, 1) f16v2_kernel(LabArgs g) {
+  using I = Img<BK>;
+  constexpr int PB = I::BYTES;
+  constexpr int STAGE = 4 * PB;               // A_h A_l B_h B_l
+  constexpr int NVA = BK / 8, NVB = BK / 8;   // float4 (A) / 16-B (B) loads per thread
+  constexpr int TPR = BK / 4;                 // threads per row in staging
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 256 * 4];
+  float* inv = (float*)(smem + 2 * STAGE);
+
+  const int64_t T = ((g.M + TBM - 1) / TBM) * ((g.N + TBN - 1) / TBN);
+  int64_t tm, tn;
+  tile_of(blockIdx.x, T, (g.N + TBN - 1) / TBN, tm, tn);
+  const int64_t m0 = tm * TBM, n0 = tn * TBN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+
+  const int64_t arows = g.M - m0 < TBM ? g.M - m0 : TBM;
+  const int64_t brows = g.N - n0 < TBN ? g.N - n0 : TBN;
+  const auto ra = rsrc(g.A + m0 * g.lda, arows * g.lda * 4);
+  const auto rb = rsrc((const char*)g.Bp + n0 * g.brow, brows * g.brow);
+  // per-thread global byte offsets and LDS byte offsets of its staging pieces
+  int voa[NVA], vob[NVB], oa[NVA], ob[NVB];
+#pragma unroll
+  for (int c = 0; c < NVA; ++c) {
+    const int idx = tid + NT * c;
+    const int r = idx / TPR, k = 4 * (idx % TPR);
+    voa[c] = (r * (int)g.lda + k) * 4;
+    oa[c] = I::off(r, k);
+  }
+#pragma unroll
+  for (int c = 0; c < NVB; ++c) {
+    const int idx = tid + NT * c;
+    const int r = idx / TPR, j = idx % TPR;   // slot j >> 1, plane j & 1
+    vob[c] = r * (int)g.brow + (j >> 1) * 32 + (j & 1) * 16;
+    ob[c] = (2 + (j & 1)) * PB + I::off(r, 8 * (j >> 1));
+  }
+  float4 va[NVA];
+  uint4 vb[NVB];
+  auto load = [&](int kt) {
+#pragma unroll
+    for (int c = 0; c < NVA; ++c)
+      va[c] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ra, voa[c], kt * BK * 4, 0));
+#pragma unroll
+    for (int c = 0; c < NVB; ++c)
+      vb[c] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rb, vob[c], kt * BK * 4, 0));
+  };
+  float cs[NVA], amax[NVA];
+#pragma unroll
+  for (int c = 0; c < NVA; ++c) { cs[c] = 64.f; amax[c] = 0.f; }
+  auto store = [&](char* st) {
+#pragma unroll
+    for (int c = 0; c < NVA; ++c) {
+      const float4 v = va[c];
+      amax[c] = fmaxf(amax[c], fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+      uint32_t h0, l0, h1, l1;
+      split_mix(v.x, v.y, cs[c], h0, l0);
+      split_mix(v.z, v.w, cs[c], h1, l1);
+      *(uint2*)(st + oa[c]) = make_uint2(h0, h1);
+      *(uint2*)(st + PB + oa[c]) = make_uint2(l0, l1);
+    }
+#pragma unroll
+    for (int c = 0; c < NVB; ++c) *(uint4*)(st + ob[c]) = vb[c];
+  };
+  floatx16 acc[MB][NB];
+#pragma unroll
+  for (int i = 0; i < MB; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nk = (int)(g.K / BK);
+  load(0);
+  if constexpr (SCALE) {
+#pragma unroll
+    for (int c = 0; c < NVA; ++c) {
+      const float4 v = va[c];
+      float m = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+#pragma unroll
+      for (int o = 1; o < TPR; o <<= 1) m = fmaxf(m, __shfl_xor(m, o));
+      int e = 0;
+      (void)frexpf(m, &e);
+      const float sc = (m > 0.f && m <= 3.0e38f) ? ldexpf(1.f, 8 - e) : 1.f;
+      cs[c] = 64.f * sc;
+      if ((tid % TPR) == 0) inv[(tid + NT * c) / TPR] = 1.f / sc;
+    }
+  } else {
+    if (tid < 256) inv[tid] = 1.f;
+  }
+  store(smem);
+  if (nk > 1) load(1);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* cur = smem + (kt & 1) * STAGE;
+    char* nxt = smem + ((kt & 1) ^ 1) * STAGE;
+#pragma unroll
+    for (int q = 0; q < BK / 16; ++q) {
+      f16x8 fa[MB][2], fb[NB][2];
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+#pragma unroll
+        for (int x = 0; x < MB; ++x)
+          fa[x][p] = *(const f16x8*)(cur + p * PB +
+                                     I::off(wm * (MB * 32) + x * 32 + (lane & 31), 16 * q + 8 * (lane >> 5)));
+#pragma unroll
+        for (int x = 0; x < NB; ++x)
+          fb[x][p] = *(const f16x8*)(cur + (2 + p) * PB +
+                                     I::off(wn * (NB * 32) + x * 32 + (lane & 31), 16 * q + 8 * (lane >> 5)));
+      }
+      if (q == 0) {
+        if (kt + 1 < nk) store(nxt);
+        if (kt + 2 < nk) load(kt + 2);
+      }
+#pragma unroll
+      for (int mi = 0; mi < MB; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NB; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][1], fa[mi][0], acc[mi][ni], 0, 0, 0);
+#pragma unroll
+      for (int mi = 0; mi < MB; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NB; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][0], fa[mi][1], acc[mi][ni], 0, 0, 0);
+#pragma unroll
+      for (int mi = 0; mi < MB; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NB; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][0], fa[mi][0], acc[mi][ni], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // range check (lab: count only): a row max over 1023 (64 a_h must be a finite fp16) or a
+  // nonzero row max below 2^-9 (its residual plane would be subnormal)
+  bool bad = false;
+#pragma unroll
+  for (int c = 0; c < NVA; ++c) {
+    float m = amax[c];
+#pragma unroll
+    for (int o = 1; o < TPR; o <<= 1) m = fmaxf(m, __shfl_xor(m, o));
+    const float s = cs[c] * (1.f / 64.f);
+    bad |= !(m * s <= 1023.f) || (m > 0.f && m * s < 0x1p-9f);
+  }
+  if (__syncthreads_or(bad) && tid == 0) atomicAdd(g.bad, 1);
+  const int lr = lane & 31, lc = 4 * (lane >> 5);
+#pragma unroll
+  for (int mi = 0; mi < MB; ++mi) {
+    const int rl = wm * (MB * 32) + mi * 32 + lr;
+    const int64_t row = m0 + rl;
+    if (row >= g.M) continue;
+    const float f = inv[rl] * g.binv;
+#pragma unroll
+    for (int ni = 0; ni < NB; ++ni) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t col = n0 + wn * (NB * 32) + ni * 32 + 8 * j + lc;
+        if (col + 3 < g.N) {
+          *(float4*)(g.C + row * g.ldc + col) =
+              make_float4(acc[mi][ni][4 * j] * f, acc[mi][ni][4 * j + 1] * f,
+                          acc[mi][ni][4 * j + 2] * f, acc[mi][ni][4 * j + 3] * f);
+        }
+      }
+    }
+  }
+}
+
+// B planes: row n, slot s (8 k): fp16 h[8] = fp16(32 sB b), then l[8] = fp16(32 sB b - h).
+__global__ void split_b_kernel(const float* B, int64_t N, int64_t K, int64_t ldb, float c,
+                               uint16_t* Bp, int64_t brow) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;   // (row, slot)
+  const int64_t slots = K / 8;
+  if (i >= N * slots) return;
+  const int64_t n = i / slots, s = i % slots;
+  const float* p = B + n * ldb + 8 * s;
+  uint32_t h[4], l[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) split_mix(p[2 * j], p[2 * j + 1], c, h[j], l[j]);
+  uint4* d = (uint4*)((char*)Bp + n * brow + s * 32);
+  d[0] = make_uint4(h[0], h[1], h[2], h[3]);
+  d[1] = make_uint4(l[0], l[1], l[2], l[3]);
+}
+
+}  // namespace
+
+extern "C" int lab_split_b(const float* B, int64_t N, int64_t K, int64_t ldb, float c,
+                           uint16_t* Bp, hipStream_t s) {
+  const int64_t n = N * (K / 8);
+  split_b_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(B, N, K, ldb, c, Bp, K * 4);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lab_gemm(int bk, int scale, const float* A, int64_t lda, const uint16_t* Bp,
+                        int64_t M, int64_t N, int64_t K, float binv, float* C, int64_t ldc,
+                        int* bad, hipStream_t s) {
+  LabArgs g{A, lda, Bp, K * 4, M, N, K, C, ldc, binv, bad};
+  const unsigned grid = (unsigned)(((M + 255) / 256) * ((N + 255) / 256));
+  if (bk == 16) {
+    if (scale) f16v2_kernel<16, true><<<grid, NT, 0, s>>>(g);
+    else f16v2_kernel<16, false><<<grid, NT, 0, s>>>(g);
+  } else {
+    if (scale) f16v2_kernel<32, true><<<grid, NT, 0, s>>>(g);
+    else f16v2_kernel<32, false><<<grid, NT, 0, s>>>(g);
+  }
+  return (int)hipGetLastError();
+}
