@@ -164,7 +164,20 @@ def survey_bytes(N, E2, F_in, NH, F, concat):
     return b_gemm, f_gemm, b_edge
 
 
-def layer_dataflow(N, E2, F_in, NH, F, concat, resid, alpha=True):
+def distinct_sources_per_chunk(graph, chunk):
+    """Sum over the edge pass's node chunks (`chunk` consecutive destinations, the unit one XCD
+    sweeps per head group: edge_fwd.hip's chunked items) of the distinct source ids their edges
+    gather: the rows a chunk must bring from beyond the L2, read again by the next chunk only
+    from the MALL or HBM. Device-side sort, once per graph, outside any timing."""
+    E2 = graph.num_edges
+    key = (graph.rowidx[:E2].to(torch.int64) // chunk) * graph.num_nodes \
+        + graph.col[:E2].to(torch.int64)
+    n = int(torch.unique(key).numel())
+    del key
+    return n
+
+
+def layer_dataflow(N, E2, F_in, NH, F, concat, resid, alpha=True, gather_rows=None):
     """Per-kernel COMPULSORY bytes and flops of one gatx layer forward, following the dataflow the
     library actually runs (gatx.functional.layer_forward): the reassociated first layer gathers
     4*round4(F_in)-byte x rows, the others 4*NH*Fp-byte Wh rows. Gathered rows count once per
@@ -173,7 +186,9 @@ def layer_dataflow(N, E2, F_in, NH, F, concat, resid, alpha=True):
     in random order, so every gather is an HBM read; hub sources aside). Every other array is
     read or written once. alpha=False: the inference forward defers the alpha pass to the first
     read of normalised_attention_coeffs (gatx.functional.LazyAlpha), so a step that never reads
-    it does not run it. Returns [(kernel, bytes, flops)]."""
+    it does not run it. gather_rows: the gathered-row count beyond the MALL when known
+    (distinct_sources_per_chunk: a source's row is read once per node chunk that gathers it, not
+    once per edge). Returns [(kernel, bytes, flops)]."""
     from gatx.functional import LayerShape, _env_int, fold_scores_into_gemm, use_reassociation
     sh = LayerShape(NH, F, F_in, concat, False)
     H2, Fp, Dp = 2 * NH, sh.Fp, sh.Dp
@@ -192,7 +207,7 @@ def layer_dataflow(N, E2, F_in, NH, F, concat, resid, alpha=True):
             ("gemm_out", 4 * (N * NH * Fin_p + NH * F * Fin_p + N * oc + N * r),
              2 * N * Fin_p * NH * F),
         ]
-    gath = N * Dp if N * Dp * 4 <= MALL_BYTES else E2 * Dp
+    gath = N * Dp if N * Dp * 4 <= MALL_BYTES else (gather_rows or E2) * Dp
     out = []
     if fold_scores_into_gemm(sh):
         out.append(("gemm", 4 * (N * F_in + (Dp + H2) * F_in + N * Dp + N * H2),
@@ -647,7 +662,13 @@ def run_rmat(args, world, rank, dev):
     E2 = graph_cache.get(ei, N, True).num_edges
     elapsed, summ, n_instr = run_timed(step, args.steps, world, dev)
     step_s = elapsed / args.steps
-    flow = layer_dataflow(N, E2, FIN, NH, F, True, False)
+    # gathered Wh rows (20 GB of them, far beyond the MALL): a source's row comes from HBM once
+    # per destination chunk that gathers it (R-MAT hubs are gathered by almost every chunk, but
+    # re-read within one only from L2), not once per edge
+    from gatx.functional import _env_int
+    chunk = _env_int("GATX_EDGE_CHUNK", 2048)
+    g_rows = distinct_sources_per_chunk(graph_cache.get(ei, N, True), chunk)
+    flow = layer_dataflow(N, E2, FIN, NH, F, True, False, gather_rows=g_rows)
     uniq = sum(b for _, b, _ in flow) + graph_build_bytes(E, E2, N)
     peak = gemm_roof()["peak"] * 1e12
     t_roof = sum(max(b / (HBM_PEAK_GBS * 1e9), f / peak) for _, b, f in flow) \
@@ -668,6 +689,9 @@ def run_rmat(args, world, rank, dev):
                 "permuted, x ~ N(0,1), xavier weights",
         "config": {"workload": f"RMAT {N} nodes / {E} edges, GATLayer 512 -> 8x64 concat, "
                                f"self-loops, {'fwd+bwd' if train else 'eval'}, CSR built per step",
+                   "gathered_rows_per_layer": g_rows,
+                   "gather_model": f"a source row once per {chunk}-destination chunk that "
+                                   "gathers it (distinct_sources_per_chunk), not once per edge",
                    "hub_split_backward": train and os.environ.get("GATX_BWD_HUBS") != "0",
                    "nodes": N, "edges_in": int(ei.size(1)), "edges_per_layer": E2,
                    "parallelism": "replicas" if world > 1 else "single GPU"},

@@ -161,7 +161,7 @@ struct EdgeFwdArgs {
   float* hub_part;         // [slot][g_count][HS*Fp + HS]
   int64_t n_items_main;
   int64_t hub_blocks;      // blocks [0, hub_blocks) run hub pieces (hub_bound * g_count waves)
-  // destinations done by the graph-local pass (gatx_edge_forward_local): skip[n] != 0 -> no item
+  // destinations the caller serves another way: skip[n] != 0 -> no item
   const uint8_t* skip;
 };
 

@@ -58,13 +58,6 @@ SIGNATURES = {
     "gatx_edge_forward_skip": (c_i, [P, c_i64, c_i64, P, P, P, P, P, c_i64, c_i, c_i, c_i, c_i,
                                      c_i, c_i, c_i, c_i, P, c_f, P, P, c_i64, P, c_i64, c_i, P,
                                      c_i64, c_i, P, P, c_i64, P, c_f, P, P, P]),
-    "gatx_local_max_nodes": (c_i, []),
-    "gatx_graph_windows_workspace_bytes": (c_sz, [c_i64]),
-    "gatx_graph_windows": (c_i, [P, P, c_i64, c_i, P, P, P, P, c_sz, P]),
-    "gatx_edge_forward_local_part_bytes": (c_sz, [c_i64, c_i, c_i, c_i]),
-    "gatx_edge_forward_local": (c_i, [P, c_i64, P, P, P, P, P, c_i64, c_i, c_i, c_i, c_i, P, c_f,
-                                      P, P, c_i64, P, c_i64, c_i, P, c_f, P, P, P, P, c_i64, P,
-                                      P]),
     "gatx_edge_forward_hub_part_bytes": (c_sz, [c_i64, c_i, c_i, c_i, c_i]),
     "gatx_graph_hub_bound": (c_i64, [c_i64, c_i]),
     "gatx_graph_hub_plan": (c_i, [P, c_i64, c_i, P, c_i64, P, P]),

@@ -331,44 +331,11 @@ def bwd_hub_args(graph: Graph, NH: int, F: int, dev, source: bool):
     return (T, ptr(hubs), ptr(count), bound, ptr(part))
 
 
-def local_plan(graph: Graph, sh: LayerShape):
-    """(starts, count, in_window) of the graph-local edge pass (csrc/edge_local.hip: each
-    self-contained node component's source rows staged in LDS) or None. Opt-in (GATX_LOCAL=1):
-    measured on MI355X it does not beat the generic L2-gather pass (PPI L1 311 vs 285 us, the
-    head-mean L2 255 vs 193-246 us: the per-edge broadcast / address / 4-float FMA work of a
-    16-float chunk costs more issue than the L2 gathers it saves). For graphs of
-    at most GATX_LOCAL_MAX_GRAPH (2^18) nodes below the hub-splitting threshold; nodes of
-    components larger than gatx_local_max_nodes() stay on the generic pass."""
-    if _env_int("GATX_LOCAL", 0) == 0:
-        return None
-    if (graph.num_nodes == 0 or graph.num_nodes > _env_int("GATX_LOCAL_MAX_GRAPH", 1 << 18)
-            or graph.num_input_edges > _env_int("GATX_HUB_MIN_EDGES", 1 << 22)):
-        return None
-    return graph.window_plan()
-
-
 def _edge_pass(rows, row_stride, S, M_ord, graph, sh, bias, p, seed, out, resid_p, elu, den,
                chunk, drop_args, dev, s):
-    """The edge pass of a non-reassociated layer (concat, or head mean over head groups):
-    graph-local windows first (LDS-staged rows), the generic pass for the remaining nodes."""
+    """The edge pass of a non-reassociated layer (concat, or head mean over head groups)."""
     N = graph.num_nodes
-    plan = local_plan(graph, sh)
-    skip = None
-    if plan is not None:
-        windows, wcount, inw = plan
-        part = None
-        if not sh.concat:
-            nb = lib.gatx_edge_forward_local_part_bytes(N, sh.NH, sh.F, 0)
-            part = torch.empty(max(nb // 4, 1), dtype=torch.float32, device=dev)
-        call("gatx_edge_forward_local", ptr(rows), row_stride, ptr(S), ptr(M_ord),
-             ptr(graph.rowptr), ptr(graph.col), ptr(graph.perm), N, sh.NH, sh.F,
-             int(sh.concat), int(sh.const), ptr(bias), float(p), ptr(seed), ptr(out),
-             sh.out_cols, resid_p, sh.out_cols, int(elu), ptr(den), *drop_args,
-             ptr(windows), ptr(wcount), ptr(inw), N, ptr(part), s)
-        skip = ptr(inw)
     hs = edge_heads_per_item(sh)
-    if skip is not None and not sh.concat and sh.NH <= 8 and sh.NH * sh.Fp <= 2048:
-        hs = sh.NH   # the few non-window nodes of a head-mean layer: one launch, all heads
     ng = sh.NH // hs
     if sh.concat or ng == 1:
         hub = hub_args(graph, sh, hs, ng, dev)
@@ -376,7 +343,7 @@ def _edge_pass(rows, row_stride, S, M_ord, graph, sh, bias, p, seed, out, resid_
              ptr(graph.rowptr), ptr(graph.col), ptr(graph.perm), N, sh.NH, sh.F, hs,
              0, 0, 0, int(sh.concat), int(sh.const), ptr(bias), float(p), ptr(seed),
              ptr(out), sh.out_cols, resid_p, sh.out_cols, int(elu), ptr(den), chunk, *hub,
-             *drop_args, skip, s)
+             *drop_args, None, s)
     else:   # head mean over groups: one launch per group, accumulated in stream order
         hub = hub_args(graph, sh, hs, 1, dev)
         for gi in range(ng):
@@ -387,7 +354,7 @@ def _edge_pass(rows, row_stride, S, M_ord, graph, sh, bias, p, seed, out, resid_
                  gi, 1, mode, 0, int(sh.const), ptr(bias) if last else None, float(p),
                  ptr(seed), ptr(out), sh.out_cols, resid_p if last else None, sh.out_cols,
                  int(elu) if last else 0, ptr(den), chunk, *hub,
-                 *(drop_args if last else (0.0, None)), skip, s)
+                 *(drop_args if last else (0.0, None)), None, s)
 
 
 def fold_scores_into_gemm(sh: LayerShape) -> bool:

@@ -207,25 +207,6 @@ class Graph:
             plan = self._hub_plans[key] = (hubs, count, bound)
         return plan
 
-    def window_plan(self):
-        """(starts, count, in_window) of gatx_graph_windows for this CSR: the self-contained node
-        components (starts[0..count], starts[count] = N) and the flags of the nodes in
-        components of at most gatx_local_max_nodes() nodes, which the graph-local edge pass
-        serves (device-side; built once per graph)."""
-        plan = self._hub_plans.get("windows")
-        if plan is None:
-            N, dev = self.num_nodes, self.device
-            windows = torch.empty((max(N, 1), 2), dtype=torch.int32, device=dev)
-            count = torch.empty(1, dtype=torch.int32, device=dev)
-            inw = torch.empty(max(N, 1), dtype=torch.uint8, device=dev)
-            wsb = _lib.lib.gatx_graph_windows_workspace_bytes(N)
-            ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
-            call("gatx_graph_windows", ptr(self.rowptr), ptr(self.col), N,
-                 _lib.lib.gatx_local_max_nodes(), ptr(windows), ptr(count), ptr(inw), ptr(ws),
-                 wsb, stream())
-            plan = self._hub_plans["windows"] = (windows, count, inw)
-        return plan
-
     def csr_host(self):
         """(rowptr, col, perm) as CPU tensors — for tests."""
         E2 = self.num_edges

@@ -341,7 +341,7 @@ int gatx_edge_forward_drop(const float* rows, int64_t row_stride, int64_t head_s
                            const int32_t* hub_count, int64_t hub_bound, float* hub_part,
                            float out_p, const uint64_t* out_seed, gatx_stream_t stream);
 /* gatx_edge_forward_drop that leaves out the destinations with skip[n] != 0 (no output, no den:
- * the graph-local pass below has them). skip = NULL: every destination. */
+ * for a caller that serves them another way). skip = NULL: every destination. */
 int gatx_edge_forward_skip(const float* rows, int64_t row_stride, int64_t head_stride,
                            const float* S, const uint32_t* M_ord, const int32_t* rowptr,
                            const int32_t* col, const int32_t* perm, int64_t num_nodes,
@@ -353,37 +353,6 @@ int gatx_edge_forward_skip(const float* rows, int64_t row_stride, int64_t head_s
                            const int32_t* hub_count, int64_t hub_bound, float* hub_part,
                            float out_p, const uint64_t* out_seed, const uint8_t* skip,
                            gatx_stream_t stream);
-/* Self-contained node components of a destination CSR (the graphs of a collated batch): the node
- * order is cut wherever no edge crosses (no destination before the cut has a source after it or
- * vice versa). windows (an [N][2] int32 buffer) receives the component starts P[0..C] (P[C] = N),
- * *win_count = C; in_window[n] = 1 for the nodes of components of at most max_nodes
- * (<= gatx_local_max_nodes()) nodes, 0 otherwise. Device-side (no host sync, capturable). Used
- * by the opt-in graph-local edge pass below. */
-int gatx_local_max_nodes(void);
-size_t gatx_graph_windows_workspace_bytes(int64_t num_nodes);
-int gatx_graph_windows(const int32_t* rowptr, const int32_t* col, int64_t num_nodes,
-                       int max_nodes, int32_t* windows, int32_t* win_count, uint8_t* in_window,
-                       void* workspace, size_t workspace_bytes, gatx_stream_t stream);
-/* The edge pass of gatx_edge_forward_drop (models/gat_layer.py:66-135 for every head) for the
- * destinations of the in_window components above (windows / win_count: gatx_graph_windows'
- * starts and count), with each component's source rows staged in LDS in 16-float chunks (one
- * workgroup per (component, head, chunk), persistent over a CU-sized grid): the same
- * attention weights, softmax denominators (den), dropout masks and fused epilogue (bias, resid,
- * ELU, next layer's dropout); rows = Wh [N][row_stride] with head h at column h*round4(F).
- * concat = 0 (head mean): part (gatx_edge_forward_local_part_bytes) holds the normalised head
- * outputs, combined in head order for the in_window nodes. max_items: a bound on *win_count
- * (e.g. num_nodes), for the grid. Pair with gatx_edge_forward_skip(..., in_window) for the rest. */
-size_t gatx_edge_forward_local_part_bytes(int64_t num_nodes, int num_heads, int out_features,
-                                          int concat);
-int gatx_edge_forward_local(const float* rows, int64_t row_stride, const float* S,
-                            const uint32_t* M_ord, const int32_t* rowptr, const int32_t* col,
-                            const int32_t* perm, int64_t num_nodes, int num_heads,
-                            int out_features, int concat, int const_attention, const float* bias,
-                            float dropout_p, const uint64_t* seed, float* out, int64_t out_ld,
-                            const float* resid, int64_t resid_ld, int elu, float* den,
-                            float out_p, const uint64_t* out_seed, const int32_t* windows,
-                            const int32_t* win_count, const uint8_t* in_window,
-                            int64_t max_items, float* part, gatx_stream_t stream);
 /* GATModel's input dropout (models/GATModel.py:130, F.dropout) as a counter-based mask on the
  * element index (the attention dropout's splitmix64 hash): y[i] = keep(seed, i) ? x[i]/(1-p) : 0.
  * The gradient is the same call on g_y. In place (y == x) is allowed. */

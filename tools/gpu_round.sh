@@ -26,5 +26,10 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "GRBM_GUI_ACTIVE
   i=$((i+1))
   step pmc$i timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace -d "$OUT/pmc_p$i" -o run --output-format csv -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc_p$i.log" 2>&1
 done
+i=0
+for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "GRBM_GUI_ACTIVE SQ_WAVES"; do
+  i=$((i+1))
+  step pmct$i timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace -d "$OUT/pmct_p$i" -o run --output-format csv -- python3 "$R/bench.py" --mode train --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmct_p$i.log" 2>&1
+done
 step pmc_rmat bash "$R/tools/gpu_pmc_rmat.sh" "$1"
 echo "all done"

@@ -16,6 +16,8 @@ for p in fwd train rmat pattern; do
 done
 PMC_SOURCE="bench.py --steps 3 --warmup 1" \
   python tools/pmc_summary.py "$S/pmc" profiles/pmc_latest.json > "$D/fwd_pmc_summary.txt"
+PMC_SOURCE="bench.py --mode train --steps 3 --warmup 1" \
+  python tools/pmc_summary.py "$S/pmct" profiles/pmc_train.json > "$D/train_pmc_summary.txt"
 PMC_SOURCE="bench.py --workload rmat --steps 1 --warmup 2" \
   python tools/pmc_summary.py "$S/pmcr" profiles/pmc_rmat.json > "$D/rmat_pmc_summary.txt"
 echo "snapshot in $D"
