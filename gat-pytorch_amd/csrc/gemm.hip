@@ -641,7 +641,8 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
     g.s_h2 = 2 * sc->nh; g.s_part = s_part;
   }
   if (b_planes && gemm_mode() == 2 && f16p_enabled() && kd.id == 2 && batch == 1 && a_kc &&
-      b_kc && g.a_vec && g.b_vec && g.splits == 1 && tag != 2 && g.lda < (1 << 20)) {
+      b_kc && g.a_vec && g.b_vec && g.splits == 1 && tag != 2 && g.lda < (1 << 20) &&
+      N <= 60 * 256) {   // (the planes' header holds 60 tile flags)
     g.b_planes = (const char*)b_planes + 256;   // past the planes' header (gemm_f16p.hip)
     g.b_prow = round_up(K, (int64_t)32) * 4;
   }

@@ -625,7 +625,8 @@ __global__ void __launch_bounds__(256) planes_split_kernel(const float* __restri
 // Exact max |x| per row and per column of X (rows x cols, row stride ld): one wave per row at a
 // time (the row's max by a wave reduction), every lane keeping its columns' running max over the
 // block's rows; the block's 4 waves combine in LDS, then one atomicMax per column (non-negative
-// floats order as their bit patterns; nan counts as inf). colmax must be zero on entry.
+// floats order as their bit patterns; nan counts as inf). colmax must be zero on entry. Either
+// output may be NULL.
 constexpr int kStatRows = 128;   // rows per block
 __global__ void __launch_bounds__(256) absmax_rows_cols_kernel(const float* __restrict__ X,
                                                                int64_t rows, int64_t cols,
@@ -664,8 +665,9 @@ __global__ void __launch_bounds__(256) absmax_rows_cols_kernel(const float* __re
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-    if (lane == 0) rowmax[r] = m;
+    if (lane == 0 && rowmax) rowmax[r] = m;
   }
+  if (!colmax) return;   // (uniform over the block: no barrier is skipped by part of it)
 #pragma unroll
   for (int j = 0; j < CH; ++j)
     if (j < nch) *(float4*)&red[wave][256 * j + 4 * lane] = cm[j];
