@@ -672,9 +672,13 @@ extern "C" void gatx_set_gemm_mode(int mode) { g_gemm_mode = mode <= 0 ? 0 : mod
 extern "C" int gatx_get_gemm_mode(void) { return gemm_mode(); }
 
 extern "C" int gatx_gemm_layout_mode(int a_kc, int b_kc) {
-  // f16x3 needs k-contiguous operand pairs (gemm_x3.hip f16_mainloop); other layouts run x3
+  // f16x3 runs on k-contiguous operand pairs (gemm_x3.hip f16_mainloop, gemm_f16p.hip) and on
+  // the weight gradient's row-contiguous pair (gatx_gemm_wgrad with G_aug's column maxima,
+  // gemm_f16p.hip f16rc); the mixed layouts run x3
   const int m = gemm_mode();
-  return m == 2 && !(a_kc && b_kc) ? 1 : m;
+  if (m != 2) return m;
+  if (a_kc && b_kc) return 2;
+  return !a_kc && !b_kc && f16p_enabled() ? 2 : 1;
 }
 
 extern "C" int gatx_gemm_fallback_read(uint64_t* dst, int reset, gatx_stream_t stream) {

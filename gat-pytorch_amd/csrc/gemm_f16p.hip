@@ -622,58 +622,86 @@ __global__ void __launch_bounds__(256) planes_split_kernel(const float* __restri
   }
 }
 
-// Exact max |x| per row and per column of X (rows x cols, row stride ld): one wave per row at a
-// time (the row's max by a wave reduction), every lane keeping its columns' running max over the
-// block's rows; the block's 4 waves combine in LDS, then one atomicMax per column (non-negative
-// floats order as their bit patterns; nan counts as inf). colmax must be zero on entry. Either
-// output may be NULL.
-constexpr int kStatRows = 128;   // rows per block
-__global__ void __launch_bounds__(256) absmax_rows_cols_kernel(const float* __restrict__ X,
+// Exact max |x| per row and per column of X (rows x cols, row stride ld): a wave takes two rows
+// at a time, all their float4 loads issued before any is used (the pass is latency-bound
+// otherwise: one row's 4 KB per wave in flight reached ~2 TB/s), the row max by a wave
+// reduction, every lane keeping its columns' running max over the block's rows; the block's 8
+// waves combine in LDS, then one atomicMax per column (non-negative floats order as their bit
+// patterns; nan counts as inf; 256-B wave-instructions at the memory side). colmax must be zero
+// on entry. Either output may be NULL.
+// VEC (ld % 4 == 0, X 16-byte aligned): unconditional float4 loads (a column index past cols
+// reads column 0 of the row and is zeroed; a partial last float4 stays inside the row stride).
+constexpr int kStatRows = 128;   // rows per block (16 per wave)
+template <bool VEC>
+__global__ void __launch_bounds__(512) absmax_rows_cols_kernel(const float* __restrict__ X,
                                                                int64_t rows, int64_t cols,
                                                                int64_t ld, float* rowmax,
                                                                uint32_t* colmax) {
   constexpr int CH = 8;                       // 256-column chunks held per lane (cols <= 2048)
-  __shared__ float red[4][CH * 256];
+  __shared__ float red[8][CH * 256];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nch = (int)((cols + 255) / 256);
-  const bool vec = (ld % 4 == 0) && ((uintptr_t)X % 16 == 0);
   float4 cm[CH];
 #pragma unroll
   for (int j = 0; j < CH; ++j) cm[j] = make_float4(0.f, 0.f, 0.f, 0.f);
   auto absn = [](float v) { return v != v ? __int_as_float(0x7f800000) : fabsf(v); };
-  const int64_t r0 = blockIdx.x * (int64_t)kStatRows;
-  for (int64_t r = r0 + wave; r < rows && r < r0 + kStatRows; r += 4) {
-    const float* x = X + r * ld;
-    float m = 0.f;
+  auto load = [&](const float* x, int64_t c) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (VEC) {
+      v = *(const float4*)(x + (c < cols ? c : 0));
+      v.x = c < cols ? v.x : 0.f;
+      v.y = c + 1 < cols ? v.y : 0.f;
+      v.z = c + 2 < cols ? v.z : 0.f;
+      v.w = c + 3 < cols ? v.w : 0.f;
+    } else {
+      if (c < cols) v.x = x[c];
+      if (c + 1 < cols) v.y = x[c + 1];
+      if (c + 2 < cols) v.z = x[c + 2];
+      if (c + 3 < cols) v.w = x[c + 3];
+    }
+    return v;
+  };
+  const int64_t r0 = blockIdx.x * (int64_t)kStatRows, rend = min(rows, r0 + kStatRows);
+  for (int64_t r = r0 + 2 * wave; r < rend; r += 16) {
+    const bool two = r + 1 < rend;
+    const float* x0 = X + r * ld;
+    const float* x1 = X + (two ? r + 1 : r) * ld;
+    float4 v0[CH], v1[CH];
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
-      if (j >= nch) break;
       const int64_t c = 256 * j + 4 * lane;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (vec && c + 3 < cols) {
-        v = *(const float4*)(x + c);
-      } else {
-        if (c < cols) v.x = x[c];
-        if (c + 1 < cols) v.y = x[c + 1];
-        if (c + 2 < cols) v.z = x[c + 2];
-        if (c + 3 < cols) v.w = x[c + 3];
-      }
-      v = make_float4(absn(v.x), absn(v.y), absn(v.z), absn(v.w));
-      cm[j] = make_float4(fmaxf(cm[j].x, v.x), fmaxf(cm[j].y, v.y), fmaxf(cm[j].z, v.z),
-                          fmaxf(cm[j].w, v.w));
-      m = fmaxf(m, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+      v0[j] = j < nch ? load(x0, c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      v1[j] = j < nch && two ? load(x1, c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    float m0 = 0.f, m1 = 0.f;
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      const float4 a = make_float4(absn(v0[j].x), absn(v0[j].y), absn(v0[j].z), absn(v0[j].w));
+      const float4 b = make_float4(absn(v1[j].x), absn(v1[j].y), absn(v1[j].z), absn(v1[j].w));
+      cm[j] = make_float4(fmaxf(cm[j].x, fmaxf(a.x, b.x)), fmaxf(cm[j].y, fmaxf(a.y, b.y)),
+                          fmaxf(cm[j].z, fmaxf(a.z, b.z)), fmaxf(cm[j].w, fmaxf(a.w, b.w)));
+      m0 = fmaxf(m0, fmaxf(fmaxf(a.x, a.y), fmaxf(a.z, a.w)));
+      m1 = fmaxf(m1, fmaxf(fmaxf(b.x, b.y), fmaxf(b.z, b.w)));
     }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-    if (lane == 0 && rowmax) rowmax[r] = m;
+    for (int o = 32; o > 0; o >>= 1) {
+      m0 = fmaxf(m0, __shfl_xor(m0, o));
+      m1 = fmaxf(m1, __shfl_xor(m1, o));
+    }
+    if (lane == 0 && rowmax) {
+      rowmax[r] = m0;
+      if (two) rowmax[r + 1] = m1;
+    }
   }
   if (!colmax) return;   // (uniform over the block: no barrier is skipped by part of it)
 #pragma unroll
   for (int j = 0; j < CH; ++j)
     if (j < nch) *(float4*)&red[wave][256 * j + 4 * lane] = cm[j];
   __syncthreads();
-  for (int c = threadIdx.x; c < cols; c += 256) {
-    const float v = fmaxf(fmaxf(red[0][c], red[1][c]), fmaxf(red[2][c], red[3][c]));
+  for (int c = threadIdx.x; c < cols; c += 512) {
+    float v = red[0][c];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) v = fmaxf(v, red[w][c]);
     atomicMax(colmax + c, __float_as_uint(v));
   }
 }
@@ -685,8 +713,11 @@ int absmax_rows_cols(const float* X, int64_t rows, int64_t cols, int64_t ld, flo
   GATX_REQUIRE(cols <= 2048, "absmax_rows_cols: at most 2048 columns");
   if (colmax) GATX_CALL(hipMemsetAsync(colmax, 0, cols * sizeof(float), stream));
   if (rows == 0) return 0;
-  absmax_rows_cols_kernel<<<(unsigned)ceil_div(rows, (int64_t)kStatRows), 256, 0, stream>>>(
-      X, rows, cols, ld, rowmax, (uint32_t*)colmax);
+  const unsigned nb = (unsigned)ceil_div(rows, (int64_t)kStatRows);
+  if (ld % 4 == 0 && (uintptr_t)X % 16 == 0)
+    absmax_rows_cols_kernel<true><<<nb, 512, 0, stream>>>(X, rows, cols, ld, rowmax, (uint32_t*)colmax);
+  else
+    absmax_rows_cols_kernel<false><<<nb, 512, 0, stream>>>(X, rows, cols, ld, rowmax, (uint32_t*)colmax);
   GATX_LAUNCH_CHECK("absmax_rows_cols");
   return 0;
 }

@@ -133,7 +133,9 @@ __global__ void __launch_bounds__(256) graph_meta_kernel(const long long* part, 
 // stats block's contiguous input range 256 edges at a time and place each surviving edge at
 // boff[b] + (kept edges before it in the range) (wave ballots + per-round wave totals in LDS);
 // the blocks after them fill slot q in [E2 - num_loops, E2) with the loop (i, i),
-// i = q - (E2 - num_loops), and the padding slots q >= E2 (dst = N: sorts after every real key).
+// i = q - (E2 - num_loops), and the padding slots q >= E2 (src = dst = N: sorts after every real
+// key, in the destination sort and in the backward's source sort alike, so col's padding slots
+// hold N and serve as the transpose's keys as they are).
 // edge_index' is written flat with its exact size: sources at [p], destinations at [E2 + p],
 // so edge_index'[:2*E2].view(2, E2) is the reference's contiguous (2, E') tensor.
 template <typename I>
@@ -141,7 +143,7 @@ __global__ void __launch_bounds__(256) compact_kernel(const void* ei, int64_t E,
                                                        int drop_loops, const long long* meta,
                                                        int64_t E_bound, int64_t num_nodes,
                                                        int64_t* ei_out, int32_t* src32,
-                                                       int32_t* dst32, int32_t* iota) {
+                                                       int32_t* dst32) {
   const int64_t E2 = meta[0], num_loops = meta[1];
   const bool ok = meta[2] == 0;
   const int nb = (int)meta[6];
@@ -171,7 +173,6 @@ __global__ void __launch_bounds__(256) compact_kernel(const void* ei, int64_t E,
         if (ei_out) { ei_out[p] = s; ei_out[E2 + p] = d; }
         src32[p] = (int32_t)s;
         dst32[p] = (int32_t)d;
-        iota[p] = (int32_t)p;
       }
       run += wtot[0] + wtot[1] + wtot[2] + wtot[3];
       __syncthreads();
@@ -183,28 +184,14 @@ __global__ void __launch_bounds__(256) compact_kernel(const void* ei, int64_t E,
        q += ((int64_t)gridDim.x - nb) * blockDim.x) {
     if (q < 0) continue;
     if (q >= E2) {   // padding slot
-      src32[q] = 0;
+      src32[q] = (int32_t)num_nodes;
       dst32[q] = (int32_t)num_nodes;
-      iota[q] = (int32_t)q;
       continue;
     }
     const int64_t v = q - first;
     if (ei_out) { ei_out[q] = v; ei_out[E2 + q] = v; }
     src32[q] = (int32_t)v;
     dst32[q] = (int32_t)v;
-    iota[q] = (int32_t)q;
-  }
-}
-
-// transpose sort keys: the source id of each dst-CSR slot, N for the padding slots
-__global__ void __launch_bounds__(256) tkeys_kernel(const int32_t* col, const long long* e2p,
-                                                    int64_t E_bound, int64_t num_nodes,
-                                                    int32_t* keys, int32_t* iota) {
-  const int64_t E2 = *e2p;
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E_bound;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    keys[e] = e < E2 ? col[e] : (int32_t)num_nodes;
-    iota[e] = (int32_t)e;
   }
 }
 
@@ -284,18 +271,52 @@ __global__ void __launch_bounds__(256) radix_hist_kernel(const int32_t* __restri
     hist[(int64_t)(threadIdx.x + 256 * j) * nblocks + blockIdx.x] = h[threadIdx.x + 256 * j];
 }
 
-template <int BITS, bool V2 = false>
+// DS (digit scan, one-pass sorts): offs holds each digit's exclusive prefix over the blocks and
+// dtot (R) the digit totals (radix_digit_scan_kernel); the digit bases come from a scan of dtot
+// here. They are also the row pointers of the sorted keys (row d starts after every key < d), so
+// block 0 writes rowptr[0 .. num_rows] when rowptr is given: no separate pass over the keys.
+template <int BITS, bool V2 = false, bool DS = false>
 __global__ void __launch_bounds__(256) radix_scatter_kernel(
     const int32_t* __restrict__ keys, const int32_t* __restrict__ vals, int64_t n, int shift,
     int items, int64_t nblocks, const uint32_t* __restrict__ offs, int32_t* __restrict__ keys_out,
     int32_t* __restrict__ vals_out, const int32_t* __restrict__ vals2 = nullptr,
-    int32_t* __restrict__ vals2_out = nullptr) {
+    int32_t* __restrict__ vals2_out = nullptr, const uint32_t* __restrict__ dtot = nullptr,
+    int32_t* __restrict__ rowptr = nullptr, int64_t num_rows = 0) {
   constexpr int R = 1 << BITS, PER = R / 256;
   __shared__ uint32_t base[R];
   __shared__ uint32_t cnt[4][R];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if constexpr (DS) {
+    __shared__ uint32_t wsum[4];
+    uint32_t v[PER], sum = 0;   // thread t: digits [PER t, PER t + PER)
 #pragma unroll
-  for (int j = 0; j < PER; ++j) base[tid + 256 * j] = offs[(int64_t)(tid + 256 * j) * nblocks + blockIdx.x];
+    for (int j = 0; j < PER; ++j) {
+      v[j] = dtot[PER * tid + j];
+      sum += v[j];
+    }
+    uint32_t x = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    uint32_t run = x - sum;
+    for (int w = 0; w < wave; ++w) run += wsum[w];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int d = PER * tid + j;
+      base[d] = run;
+      if (rowptr && blockIdx.x == 0 && d <= num_rows) rowptr[d] = (int32_t)run;
+      run += v[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PER; ++j) base[tid + 256 * j] += offs[(int64_t)(tid + 256 * j) * nblocks + blockIdx.x];
+  } else {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) base[tid + 256 * j] = offs[(int64_t)(tid + 256 * j) * nblocks + blockIdx.x];
+  }
 #pragma unroll
   for (int w = 0; w < 4; ++w)
 #pragma unroll
@@ -632,7 +653,7 @@ inline int64_t hist_entries(int64_t n, unsigned bits) {
 
 size_t sort_bytes(int64_t n, unsigned bits, bool v2 = false) {  // keys in [0, 2^bits)
   const int64_t m = hist_entries(n, bits);
-  return 2 * align256(sizeof(uint32_t) * (m + kRadix)) + (v2 ? 3 : 2) * align256(sizeof(int32_t) * (n > 0 ? n : 1)) +
+  return 2 * align256(sizeof(uint32_t) * (m + (1 << kWideBits))) + (v2 ? 3 : 2) * align256(sizeof(int32_t) * (n > 0 ? n : 1)) +
          align256(radix_scan_bytes(m)) + 256;
 }
 
@@ -640,8 +661,8 @@ SortWs carve_sort(void* ws, int64_t n, unsigned bits, bool v2 = false) {
   const int64_t m = hist_entries(n, bits);
   char* p = (char*)ws;
   SortWs w;
-  w.hist = (uint32_t*)p; p += align256(sizeof(uint32_t) * (m + kRadix));
-  w.offs = (uint32_t*)p; p += align256(sizeof(uint32_t) * (m + kRadix));   // + digit totals
+  w.hist = (uint32_t*)p; p += align256(sizeof(uint32_t) * (m + (1 << kWideBits)));
+  w.offs = (uint32_t*)p; p += align256(sizeof(uint32_t) * (m + (1 << kWideBits)));   // + digit totals
   w.tk = (int32_t*)p; p += align256(sizeof(int32_t) * (n > 0 ? n : 1));
   w.tv = (int32_t*)p; p += align256(sizeof(int32_t) * (n > 0 ? n : 1));
   w.tv2 = nullptr;
@@ -656,9 +677,14 @@ SortWs carve_sort(void* ws, int64_t n, unsigned bits, bool v2 = false) {
 // in the output.
 // vals2_in / vals2_out (nullable): a second value carried along (the graph build's source ids,
 // so the CSR's col needs no gather through perm afterwards).
+// rowptr (nullable, keys in [0, num_rows]): the one-pass (12-bit) sort with a second value also
+// writes the row pointers of the sorted keys and sets *rowptr_done; otherwise the caller runs
+// rowptr_kernel.
 int sort_pairs(const int32_t* keys_in, const int32_t* vals_in, int32_t* keys_out,
                int32_t* vals_out, int64_t n, unsigned bits, void* ws, hipStream_t stream,
-               const int32_t* vals2_in = nullptr, int32_t* vals2_out = nullptr) {
+               const int32_t* vals2_in = nullptr, int32_t* vals2_out = nullptr,
+               int32_t* rowptr = nullptr, int64_t num_rows = 0, bool* rowptr_done = nullptr) {
+  if (rowptr_done) *rowptr_done = false;
   if (n <= 0) return 0;
   GATX_REQUIRE(n < (1ll << 31), "sort: too many keys");
   const bool v2 = vals2_in != nullptr;
@@ -695,8 +721,12 @@ int sort_pairs(const int32_t* keys_in, const int32_t* vals_in, int32_t* keys_out
       return !(e && strcmp(e, "0") == 0);
     }();
     const bool dscan = big && lds_tiles && dscan_on && nb <= 4096;
-    if (dscan) {
-      radix_digit_scan_kernel<<<kRadix, 256, 0, stream>>>(w.hist, nb, w.offs, w.offs + m);
+    // the one-pass sort: per-digit scans (4096 digits) + the digit-total scan in the scatter,
+    // which also writes rowptr — three launches for the whole sort instead of five
+    const bool wscan = wide && v2 && dscan_on && nb <= 4096 && num_rows < (1 << kWideBits);
+    if (dscan || wscan) {
+      radix_digit_scan_kernel<<<wscan ? (1u << kWideBits) : (unsigned)kRadix, 256, 0, stream>>>(
+          w.hist, nb, w.offs, w.offs + m);
       GATX_LAUNCH_CHECK("radix_digit_scan");
     } else {
       // (a single-workgroup LDS scan over all 256 * nb counts measured 35 us on PPI's 80 K
@@ -720,6 +750,10 @@ int sort_pairs(const int32_t* keys_in, const int32_t* vals_in, int32_t* keys_out
       else
         radix_scatter_lds16_kernel<false><<<(unsigned)nb, 1024, 0, stream>>>(
             ck, cv, n, shift, items, nb, w.offs, w.hist, ok, ov);
+    } else if (wscan) {
+      radix_scatter_kernel<kWideBits, true, true><<<(unsigned)nb, 256, 0, stream>>>(
+          ck, cv, n, 0, items, nb, w.offs, ok, ov, cv2, ov2, w.offs + m, rowptr, num_rows);
+      if (rowptr_done) *rowptr_done = rowptr != nullptr;
     } else if (v2 && wide)   // (the wide LDS tile has no room for a second value)
       radix_scatter_kernel<kWideBits, true><<<(unsigned)nb, 256, 0, stream>>>(
           ck, cv, n, 0, items, nb, w.offs, ok, ov, cv2, ov2);
@@ -754,27 +788,29 @@ int graph_build_impl(const void* ei, int64_t E, int64_t ld, int add_loops, int64
                      int64_t E_bound, const long long* meta, int64_t* ei_out, int32_t* rowptr,
                      int32_t* col, int32_t* rowidx, int32_t* perm, void* ws, size_t ws_bytes,
                      hipStream_t stream) {
-  // workspace carve: src32 [Eb] | dst32 [Eb] | iota [Eb] | sort workspace
+  // workspace carve: src32 [Eb] | dst32 [Eb] | sort workspace (perm: the sort's identity values)
   char* p = (char*)ws;
   int32_t* src32 = (int32_t*)p; p += align256(sizeof(int32_t) * (E_bound > 0 ? E_bound : 1));
   int32_t* dst32 = (int32_t*)p; p += align256(sizeof(int32_t) * (E_bound > 0 ? E_bound : 1));
-  int32_t* iota = (int32_t*)p;  p += align256(sizeof(int32_t) * (E_bound > 0 ? E_bound : 1));
   size_t used = (size_t)(p - (char*)ws);
   GATX_REQUIRE(used <= ws_bytes, "graph_build: workspace too small");
   void* tmp = p;
+  bool done = false;
   if (E_bound > 0) {
     // the stats launch's block count (meta[6]) is <= kStatsBlocks: that many range blocks, then
     // the loop / padding slot blocks
     const int64_t slot_blocks = std::max<int64_t>(1, std::min<int64_t>(ceil_div(E_bound, 256), 4096));
     compact_kernel<I><<<(unsigned)(stats_blocks(E) + slot_blocks), 256, 0, stream>>>(
-        ei, E, ld, add_loops, meta, E_bound, N, ei_out, src32, dst32, iota);
+        ei, E, ld, add_loops, meta, E_bound, N, ei_out, src32, dst32);
     GATX_LAUNCH_CHECK("compact");
     // src ids ride along as a second value: col comes out of the sort (no gather through perm)
-    GATX_CALL(sort_pairs(dst32, iota, rowidx, perm, E_bound, bits_for(N + 1), tmp, stream, src32,
-                         col));
+    GATX_CALL(sort_pairs(dst32, nullptr, rowidx, perm, E_bound, bits_for(N + 1), tmp, stream, src32,
+                         col, rowptr, N, &done));
   }
-  rowptr_kernel<<<grid_for(E_bound + 1), 256, 0, stream>>>(rowidx, E_bound, N, rowptr);
-  GATX_LAUNCH_CHECK("rowptr");
+  if (!done) {
+    rowptr_kernel<<<grid_for(E_bound + 1), 256, 0, stream>>>(rowidx, E_bound, N, rowptr);
+    GATX_LAUNCH_CHECK("rowptr");
+  }
   return 0;
 }
 
@@ -828,7 +864,7 @@ extern "C" int gatx_graph_meta(const void* edge_index, int is64, int64_t E, int6
 
 extern "C" size_t gatx_graph_build_workspace_bytes(int64_t E, int64_t E_bound, int64_t N) {
   (void)E;
-  size_t b = 3 * align256(sizeof(int32_t) * (E_bound > 0 ? E_bound : 1));
+  size_t b = 2 * align256(sizeof(int32_t) * (E_bound > 0 ? E_bound : 1));
   return b + align256(sort_bytes(E_bound, bits_for(N + 1), true)) + 256;
 }
 
@@ -851,7 +887,7 @@ extern "C" int gatx_graph_build(const void* edge_index, int is64, int64_t E, int
 }
 
 extern "C" size_t gatx_graph_transpose_workspace_bytes(int64_t E_bound, int64_t N) {
-  return 3 * align256(sizeof(int32_t) * (E_bound > 0 ? E_bound : 1)) +
+  return align256(sizeof(int32_t) * (E_bound > 0 ? E_bound : 1)) +
          align256(sort_bytes(E_bound, bits_for(N + 1), true)) + 256;
 }
 
@@ -860,22 +896,23 @@ extern "C" int gatx_graph_transpose(const int32_t* col, const int32_t* rowidx, i
                                     int32_t* scol, int32_t* seid, void* ws, size_t ws_bytes,
                                     gatx_stream_t s) {
   hipStream_t stream = (hipStream_t)s;
+  (void)e2;   // (col's padding slots hold N: gatx_graph_build)
   char* p = (char*)ws;
-  int32_t* iota = (int32_t*)p;  p += align256(sizeof(int32_t) * (E_bound > 0 ? E_bound : 1));
-  int32_t* keys = (int32_t*)p;  p += align256(sizeof(int32_t) * (E_bound > 0 ? E_bound : 1));
   int32_t* skeys = (int32_t*)p; p += align256(sizeof(int32_t) * (E_bound > 0 ? E_bound : 1));
   size_t used = (size_t)(p - (char*)ws);
   GATX_REQUIRE(used <= ws_bytes, "graph_transpose: workspace too small");
+  bool done = false;
   if (E_bound > 0) {
-    tkeys_kernel<<<grid_for(E_bound), 256, 0, stream>>>(col, (const long long*)e2, E_bound, N,
-                                                        keys, iota);
-    GATX_LAUNCH_CHECK("tkeys");
-    // each slot's destination rides through the sort as a second value: scol comes out sorted
-    GATX_CALL(sort_pairs(keys, iota, skeys, seid, E_bound, bits_for(N + 1), (void*)p, stream,
-                         rowidx, scol));
+    // the keys are col itself (N in the padding slots, which sort last); seid = the slots (the
+    // sort's identity values); each slot's destination rides through the sort as a second
+    // value: scol comes out sorted
+    GATX_CALL(sort_pairs(col, nullptr, skeys, seid, E_bound, bits_for(N + 1), (void*)p, stream,
+                         rowidx, scol, srowptr, N, &done));
   }
-  rowptr_kernel<<<grid_for(E_bound + 1), 256, 0, stream>>>(skeys, E_bound, N, srowptr);
-  GATX_LAUNCH_CHECK("srowptr");
+  if (!done) {
+    rowptr_kernel<<<grid_for(E_bound + 1), 256, 0, stream>>>(skeys, E_bound, N, srowptr);
+    GATX_LAUNCH_CHECK("srowptr");
+  }
   return 0;
 }
 

@@ -637,30 +637,35 @@ def layer_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShape, 
 
     def g_aug_stats():
         if not stats_box:
+            if KC > 2048:   # (the pass holds at most 2048 columns per lane set; the GEMMs then
+                stats_box.append((None, None))   # scale rows by their first K-tile)
+                return stats_box[0]
             rowmax = torch.empty(N, **f32)
-            colmax = torch.empty(KC, **f32) if KC <= 2048 else None
+            colmax = torch.empty(KC, **f32)
             with _span("bwd_gaug_stats", binfo):
-                call("gatx_absmax_rows_cols", ptr(G_aug), N, KC, ldg, ptr(rowmax),
-                     ptr(colmax) if colmax is not None else None, s)
+                call("gatx_absmax_rows_cols", ptr(G_aug), N, KC, ldg, ptr(rowmax), ptr(colmax), s)
             stats_box.append((rowmax, colmax))
         return stats_box[0]
     if need_x:
         g_x = g_pre if fold else torch.empty((N, sh.F_in), **f32)
+        big = N * sh.F_in * KC >= (1 << 27)
+        with_planes = big and use_weight_planes(sh.F_in, KC, N)
+        # (G_aug's row maxima before the span: the statistics pass has its own)
+        stats = g_aug_stats() if with_planes else None
         with _span("bwd_gemm_gx", binfo + (bool(fold),)):
-            if N * sh.F_in * KC >= (1 << 27):
+            if big:
                 # W_aug^T (F_in x K_aug, 4 MB at PPI): both GEMM operands k-contiguous (the
                 # n-contiguous B staging of W_aug as stored ran this product ~25% slower), and
                 # pre-split into fp16 planes for the f16x3 kernel (gemm_f16p.hip)
                 W_augT = torch.empty((sh.F_in, ldg), **f32)
                 call("gatx_transpose_f32", KC, sh.F_in, ptr(W_aug), sh.F_in, ptr(W_augT), ldg, s)
                 planes_t = None
-                if use_weight_planes(sh.F_in, KC, N):
+                if with_planes:
                     planes_t = build_weight_planes(W_augT, sh.F_in, KC, ldg)
-                    stats = g_aug_stats()
                 call("gatx_gemm_planes", N, sh.F_in, KC, ptr(G_aug), ldg, ptr(W_augT), ldg,
                      ptr(planes_t) if planes_t is not None else None, ptr(g_x), sh.F_in,
                      sh.F_in, None, 0, -1, None, 0, int(fold), None, 0, 0, None, 1,
-                     ptr(stats[0]) if planes_t is not None else None,
+                     ptr(stats[0]) if planes_t is not None and stats[0] is not None else None,
                      *gemm_workspace(N, sh.F_in, KC, dev), s)
             else:   # small layers are launch-bound: read W_aug as stored (no transpose launch)
                 call("gatx_gemm_f32", N, sh.F_in, KC, ptr(G_aug), ldg, 1, ptr(W_aug), sh.F_in,

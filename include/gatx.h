@@ -64,7 +64,7 @@ int gatx_graph_meta(const void* edge_index, int index_is_int64, int64_t E, int64
  * edge_index' = [edges with src != dst in input order | (i, i) for i < num_loops] when
  * add_self_loops (models/utils.py:47-67), else edge_index unchanged. The host allocates for
  * E_bound >= E (+ num_nodes with self-loops); slots past E2 are padding that sorts after every
- * real slot, and rowptr[num_nodes] = E2.
+ * real slot (col = rowidx = num_nodes there), and rowptr[num_nodes] = E2.
  * Outputs: edge_index_out (nullable) int64[2 * E_bound] holding edge_index' contiguously as
  * (2, E2): sources at [0, E2), destinations at [E2, 2*E2); and the CSR of edge_index' by
  * destination over num_nodes rows, stable in edge_index' order:
@@ -79,9 +79,10 @@ int gatx_graph_build(const void* edge_index, int index_is_int64, int64_t E, int6
                      int32_t* perm, void* workspace, size_t workspace_bytes,
                      gatx_stream_t stream);
 
-/* Source-ordered transpose of the CSR (for the backward's scatters to source nodes), E2 read
- * from the device (e2 = &meta[0]): srowptr [num_nodes+1], scol [E_bound] = destination id,
- * seid [E_bound] = dst-CSR slot. */
+/* Source-ordered transpose of the CSR built by gatx_graph_build (its padding slots hold
+ * num_nodes, so they sort last): srowptr [num_nodes+1], scol [E_bound] = destination id,
+ * seid [E_bound] = dst-CSR slot. e2 (= &meta[0]) is kept for the signature; the padding makes it
+ * unnecessary. */
 size_t gatx_graph_transpose_workspace_bytes(int64_t E_bound, int64_t num_nodes);
 int gatx_graph_transpose(const int32_t* col, const int32_t* rowidx, int64_t num_nodes,
                          int64_t E_bound, const int64_t* e2, int32_t* srowptr, int32_t* scol,
@@ -177,7 +178,8 @@ int gatx_gemm_wgrad(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda
 int gatx_absmax_rows_cols(const float* X, int64_t rows, int64_t cols, int64_t ld, float* rowmax,
                           float* colmax, gatx_stream_t stream);
 /* The arithmetic (2 f16x3, 1 x3, 0 f32) the tiled GEMMs run for an operand layout: a_kc / b_kc
- * = whether A's rows / B's columns are k-contiguous (the weight gradient G_aug^T x has neither). */
+ * = whether A's rows / B's columns are k-contiguous (the weight gradient G_aug^T x has neither:
+ * f16x3 through gatx_gemm_wgrad with the column maxima, unless GATX_F16P=0). */
 int gatx_gemm_layout_mode(int a_kc, int b_kc);
 /* Diagnostic (not on the reference path): enqueue a copy of the count of f16x3 GEMM workgroups
  * that tripped the range check and recomputed their tile as x3 (each costs ~1.5x its tile) into
