@@ -74,10 +74,14 @@ def gemm_roof():
     from gatx import _lib
     mode = _lib.lib.gatx_get_gemm_mode()
     if mode == 2:
+        f16p = os.environ.get("GATX_F16P", "1") != "0"
         return dict(mode="f16x3", peak=BF16_MFMA_PEAK_TFS / F16X3_PRODUCTS,
-                    prefix="gemm_x3_kernel<true, true, true, 0,",
-                    kernel="gemm_x3_kernel, f16x3 arithmetic (fp32 as 2 fp16 planes x 3 MFMA "
-                           "products; peak = dense fp16 2500 TF / 3)")
+                    prefix=("gemm_f16p_kernel<16, 0>", "gemm_f16p_kernel<32, 0>",
+                            "gemm_x3_kernel<true, true, true, 0,"),
+                    kernel=("gemm_f16p_kernel (weight as pre-split fp16 planes)" if f16p
+                            else "gemm_x3_kernel") +
+                           ", f16x3 arithmetic (fp32 as 2 fp16 planes x 3 MFMA products; peak = "
+                           "dense fp16 2500 TF / 3)")
     if mode == 1:
         return dict(mode="x3", peak=BF16_MFMA_PEAK_TFS / X3_PRODUCTS, prefix="gemm_x3_kernel<true, true, true, 0,",
                     kernel="gemm_x3_kernel (fp32 as 3 bf16 planes x 6 MFMA products; peak = "
@@ -101,7 +105,7 @@ def gemm_dtype():
     return "fp32 (GEMMs: v_mfma_f32_32x32x2_f32)"
 
 
-def run_timed(step, steps, world, dev, instr_step=None):
+def run_timed(step, steps, world, dev, instr_step=None, instr_outside=False):
     """The timed region: barrier + synchronize on both sides, max over ranks. Returns (elapsed,
     per-kernel HIP-event records, instrumented step count). Only the last steps // 10 (>= 1)
     steps bracket their launches with HIP events on the launch stream: each timed event record
@@ -112,7 +116,11 @@ def run_timed(step, steps, world, dev, instr_step=None):
     bracket individual launches, which a graph replay does not expose.
     The region is bracketed by two gatx_region_mark dispatches (the first carries `steps` in its
     grid size) enqueued outside the clock, so a rocprofv3 counter pass can cut exactly these
-    steps' dispatches out of its trace (tools/pmc_summary.py)."""
+    steps' dispatches out of its trace (tools/pmc_summary.py).
+    instr_outside (launch-bound captured steps: PATTERN, Planetoid): all `steps` timed steps are
+    graph replays and the instrumented eager steps run right after the clock stops — an eager
+    step of ~80 small launches is host-bound (it took ~3x a replay), so inside the clock it would
+    measure the Python launch path, not the step."""
     from gatx import _lib
     from gatx.functional import KernelTimer, set_kernel_timer
     n_instr = max(1, steps // 10)
@@ -122,8 +130,9 @@ def run_timed(step, steps, world, dev, instr_step=None):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    outside = instr_outside and instr_step is not None
     for i in range(steps):
-        if i == steps - n_instr:
+        if i == steps - n_instr and not outside:
             set_kernel_timer(timer)
             if instr_step is not None:
                 step = instr_step
@@ -134,6 +143,12 @@ def run_timed(step, steps, world, dev, instr_step=None):
     elapsed = time.perf_counter() - t0
     set_kernel_timer(None)
     _lib.call("gatx_region_mark", 1, _lib.stream())
+    if outside:
+        set_kernel_timer(timer)
+        for _ in range(n_instr):
+            instr_step()
+        torch.cuda.synchronize()
+        set_kernel_timer(None)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64,
                          device=dev if dist.get_backend() == "nccl" else "cpu")
@@ -536,8 +551,10 @@ def roofline_objects(summ, edge_bytes, pm, n_instr, pm_path="", gather_E2=None):
 # kernel-name prefix(es) its launches carry (for `traffic`)
 TRAIN_PHASES = {
     "gemm": ("mfma", None),
-    "bwd_gemm_gx": ("mfma", "gemm_x3_kernel<true, true, true, 1,"),
-    "bwd_gemm_gw": ("mfma", "gemm_x3_kernel<false, false, true, 2, 1,"),
+    # (pre-split f16x3 g_x / the in-loop kernel; the f16x3 weight gradient / its x3 form)
+    "bwd_gemm_gx": ("mfma", ("gemm_f16p_kernel<16, 1>", "gemm_f16p_kernel<32, 1>",
+                             "gemm_x3_kernel<true, true, true, 1,")),
+    "bwd_gemm_gw": ("mfma", ("gemm_f16rc_kernel<", "gemm_x3_kernel<false, false, true, 2, 1,")),
     "edge_forward": ("hbm", "edge_forward_kernel"),
     "bwd_edge_dst": ("hbm", "edge_bwd_dst"),
     "bwd_edge_src": ("hbm", "edge_bwd_src"),
@@ -617,7 +634,8 @@ def train_roofline_objects(summ, price, pm, n_instr, pm_path=""):
             if b > 0:
                 o["traffic"] = b / per_step
                 o["traffic_source"] = (f"{os.path.relpath(pm_path, ROOT) if pm_path else ''} "
-                                       f"({pm.get('source', '')}), kernels {prefix}*")
+                                       f"({pm.get('source', '')}), kernels "
+                                       + " | ".join(f"{x}*" for x in (prefix if isinstance(prefix, tuple) else (prefix,))))
         objs.append(o)
     return sorted(objs, key=lambda o: -o["ms_per_step"])
 
@@ -872,6 +890,10 @@ def main():
     def _w(t, w):   # no extra launch for the single-rank weight 1
         return t if w == 1.0 else t * w
 
+    # the loss's seed gradient, made once: backward() on a scalar would fill a fresh ones tensor
+    # every step (one launch)
+    one = torch.ones((), device=dev)
+
     def step():
         if not args.cached_graph:
             clear_graph_cache()
@@ -895,7 +917,7 @@ def main():
             attention_norm = model.calc_attention_norm(ei2, atts)
             if args.attention_penalty != 0.0:
                 loss = loss + args.attention_penalty * w_norm * attention_norm
-        loss.backward()
+        loss.backward(one)
         if reducer is not None:
             reducer.finish()
         with _span("adam", (n_params,)):
@@ -916,8 +938,10 @@ def main():
     from gatx import _lib
     fb = torch.zeros(1, dtype=torch.int64, device=dev)
     _lib.call("gatx_gemm_fallback_read", _lib.ptr(fb), 1, _lib.stream())   # reset the counter
+    # (small batches are launch-bound: their instrumented eager steps run after the clock)
+    instr_outside = use_graph and ds != "PPI"
     elapsed, summ, n_instr = run_timed(step, args.steps, world, dev,
-                                       step.eager if use_graph else None)
+                                       step.eager if use_graph else None, instr_outside)
     _lib.call("gatx_gemm_fallback_read", _lib.ptr(fb), 1, _lib.stream())
     fallback_tiles = int(fb.item())
     step_s = elapsed / args.steps
@@ -935,7 +959,8 @@ def main():
         st = CapturedStep(eager_step) if use_graph else eager_step
         for _ in range(args.warmup):
             st()
-        el, _, _ = run_timed(st, args.steps, world, dev, st.eager if use_graph else None)
+        el, _, _ = run_timed(st, args.steps, world, dev, st.eager if use_graph else None,
+                             instr_outside)
         alpha_eager_ms = el / args.steps * 1e3
         os.environ["GATX_DEFER_ALPHA"] = "1"
         gf.reset_tuning()
@@ -993,8 +1018,11 @@ def main():
                    "graphs_per_gpu": args.graphs, "nodes_per_gpu": N, "edges_per_layer": E2,
                    "parallelism": ("replicas" if planetoid and world > 1
                                    else f"graph-batch dp{world}"),
-                   "launch": "hipGraph replay (last steps//10 eager, HIP-event instrumented)"
-                             if use_graph else "eager",
+                   "launch": ("eager" if not use_graph else
+                              "hipGraph replay; kernel times from steps//10 HIP-event-instrumented "
+                              "eager steps run after the clock (launch-bound)" if instr_outside
+                              else "hipGraph replay (last steps//10 eager, HIP-event "
+                                   "instrumented)"),
                    "wiring": ("gatx (skip / ELU / dropout fused into the layers)"
                               if args.wiring == "gatx" else
                               "reference GATModel.forward around gatx GATLayers (drop-in)"),

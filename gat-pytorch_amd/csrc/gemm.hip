@@ -597,6 +597,11 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
   g.tiles_n = ceil_div(N, kd.bn);
   g.dp_blocks = 0; g.tail_rem = 0; g.tail_s = 1; g.bm = kd.bm; g.bn = kd.bn;
   g.tail_partial = nullptr;
+  // the weight gradient G_aug^T x with G_aug's exact column maxima: the row-contiguous f16x3
+  // kernel (gemm_f16p.hip), its 256-row tiles all full (a few rows past them: the thin kernel)
+  const bool wgrad_f16 = a_rowmax && tag == 2 && gemm_mode() == 2 && f16p_enabled() &&
+                         kd.id == 2 && batch == 1 && !a_kc && !b_kc && !accumulate;
+  if (wgrad_f16 && wgrad_thin_rows(M) && g.b_vec && N % 4 == 0) g.tiles_m = M / kd.bm;
   const int64_t tiles = g.tiles_m * g.tiles_n * batch;
   const int64_t slots = resident_blocks(kd);
   // fused scores: x3 tiles, one batch entry, no split-K; the partials take the workspace's end
@@ -646,10 +651,6 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
     g.b_planes = (const char*)b_planes + 256;   // past the planes' header (gemm_f16p.hip)
     g.b_prow = round_up(K, (int64_t)32) * 4;
   }
-  // the weight gradient G_aug^T x with G_aug's exact column maxima: the row-contiguous f16x3
-  // kernel (gemm_f16p.hip)
-  const bool wgrad_f16 = a_rowmax && tag == 2 && gemm_mode() == 2 && f16p_enabled() &&
-                         kd.id == 2 && batch == 1 && !a_kc && !b_kc && !accumulate;
   if (g.b_planes) GATX_CALL(launch_f16p_and_fixups(g, tag, stream));
   else if (wgrad_f16) GATX_CALL(launch_f16rc_and_reduce(g, stream));
   else if (tag == 0) GATX_CALL(launch_gemm<0>(g, a_kc, b_kc, batch, stream));
@@ -832,7 +833,9 @@ extern "C" int gatx_gemm_f32_batched(int64_t batch, int64_t M, int64_t N, int64_
 extern "C" size_t gatx_gemm_splitk_workspace_bytes(int64_t M, int64_t N, int64_t K) {
   const Kind kd = choose_kind(M, N);
   const int64_t tiles = ceil_div(M, kd.bm) * ceil_div(N, kd.bn);
-  const int sp = choose_splits(tiles, K, resident_blocks(kd));
+  int sp = choose_splits(tiles, K, resident_blocks(kd));
+  if (kd.id == 2 && wgrad_thin_rows(M))   // the f16x3 weight gradient tiles only full rows
+    sp = std::max(sp, choose_splits((M / kd.bm) * ceil_div(N, kd.bn), K, resident_blocks(kd)));
   return sp > 1 ? (size_t)sp * M * N * sizeof(float) : 0;
 }
 

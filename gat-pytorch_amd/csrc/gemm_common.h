@@ -293,6 +293,9 @@ int launch_gemm_smallk(const gk::GemmArgs& g, int batch, hipStream_t stream);
 // gemm_f16p.hip: the f16x3 kernel with B given as pre-split fp16 planes (tags 0 and 1)
 int launch_gemm_f16p(const gk::GemmArgs& g, int tag, hipStream_t stream);
 int launch_gemm_f16rc(const gk::GemmArgs& g, hipStream_t stream);
+// rows past the last multiple of 256 of a weight gradient that the f16x3 kernel leaves to its
+// VALU thin-row kernel (0: none)
+int wgrad_thin_rows(int64_t M);
 size_t weight_planes_bytes(int64_t rows, int64_t K);
 int absmax_rows_cols(const float* X, int64_t rows, int64_t cols, int64_t ld, float* rowmax,
                      float* colmax, hipStream_t stream);

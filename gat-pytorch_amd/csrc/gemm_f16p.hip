@@ -554,57 +554,77 @@ __global__ void __launch_bounds__(512, 1) gemm_f16rc_kernel(GemmArgs g) {
 }
 
 // ---- weight planes (gatx_weight_planes) ---------------------------------------------------------
-// Header (kPlanesHeader bytes) then rows x prow bytes: row n = K_pad / 8 slots of 32 bytes, each
-// h[8] then l[8] (fp16), K_pad = round_up(K, 32), zero past K.
+// Header (kPlanesHeader bytes: [0] 2^-11 / s_B, [1] s_B, [16..] one flag per 256-row tile), then
+// rows x prow bytes of planes: row n = K_pad / 8 slots of 32 bytes, each h[8] then l[8] (fp16),
+// K_pad = round_up(K, 32), zero past K; then the scratch of the two build launches: rows row
+// maxima and ceil(rows / 4) block maxima. Two launches, no memset and no atomics: every header
+// word is written by the second launch (identical values from the blocks of one tile).
 
+// One wave per row: the row's max |w| (nan -> inf) and, per block of 4 rows, their max.
 __global__ void __launch_bounds__(256) planes_max_kernel(const float* __restrict__ W, int64_t rows,
-                                                         int64_t K, int64_t ld, uint32_t* gmax) {
-  float m = 0.f;
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < rows * K; i += gridDim.x * 256ll) {
-    const int64_t r = i / K, k = i - r * K;
-    const float v = fabsf(W[r * ld + k]);
-    m = (v > m || v != v) ? (v != v ? __int_as_float(0x7f800000) : v) : m;   // nan -> inf
-  }
+                                                         int64_t K, int64_t ld,
+                                                         float* __restrict__ rowmax,
+                                                         float* __restrict__ blockmax) {
   __shared__ float red[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t row = blockIdx.x * 4ll + wave;
+  float m = 0.f;
+  if (row < rows) {
+    const float* w = W + row * ld;
+    for (int64_t k = lane; k < K; k += 64) {
+      const float v = fabsf(w[k]);
+      m = (v > m || v != v) ? (v != v ? __int_as_float(0x7f800000) : v) : m;
+    }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    atomicMax(gmax, __float_as_uint(m));   // non-negative floats order as their bit patterns
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if (lane == 0) rowmax[row] = m;
   }
+  if (lane == 0) red[wave] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) blockmax[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
 }
 
-// One wave per row: scale s_B from the global max, the row's max for its tile flag, the planes.
+// One wave per row: the global max from the block maxima, s_B, the row's tile flag (from the
+// tile's row maxima), the planes.
 __global__ void __launch_bounds__(256) planes_split_kernel(const float* __restrict__ W,
                                                            int64_t rows, int64_t K, int64_t ld,
-                                                           char* __restrict__ planes) {
+                                                           char* __restrict__ planes,
+                                                           const float* __restrict__ rowmax,
+                                                           const float* __restrict__ blockmax,
+                                                           int64_t nblk) {
   char* hdr = planes - kPlanesHeader;
-  const float gm = __uint_as_float(*(const uint32_t*)(hdr + 8));
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float gm = 0.f;
+  for (int64_t i = lane; i < nblk; i += 64) gm = fmaxf(gm, blockmax[i]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) gm = fmaxf(gm, __shfl_xor(gm, o));
   int e = 0;
   (void)frexpf(gm, &e);
   const bool finite = gm <= 3.0e38f;
   const float sB = (gm > 0.f && finite) ? ldexpf(1.f, 10 - e) : 1.f;
   const float c = 32.f * sB;
-  const int64_t row = blockIdx.x * 4ll + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     ((float*)hdr)[0] = 0x1p-11f / sB;
     ((float*)hdr)[1] = sB;
   }
+  // the tile flag: a nonzero row whose residual plane would go subnormal (max s_B < 2^-8), or a
+  // non-finite value anywhere (the global max is then inf): the tile recomputes as x3. Wave 0 of
+  // the first block of each tile's rows (every block of a tile would write the same value).
+  const int64_t row0 = blockIdx.x * 4ll;
+  if (wave == 0 && row0 % 256 == 0) {
+    bool bad = !finite;
+    for (int64_t r = row0 + lane; r < rows && r < row0 + 256; r += 64) {
+      const float m = rowmax[r];
+      bad |= m > 0.f && m * sB < 0x1p-8f;
+    }
+    bad = __any(bad);
+    if (lane == 0) ((uint32_t*)(hdr + 16))[row0 / 256] = bad ? 1u : 0u;
+  }
+  const int64_t row = row0 + wave;
   if (row >= rows) return;
   const int64_t kpad = round_up(K, (int64_t)32);
   const int64_t prow = kpad * 4;
   const float* w = W + row * ld;
-  float m = 0.f;
-  for (int64_t k = lane; k < K; k += 64) m = fmaxf(m, fabsf(w[k]));
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-  // a nonzero row whose residual plane would go subnormal (max s_B < 2^-8), or any non-finite
-  // value anywhere (the global max then is inf): the row's 256-row tile recomputes as x3
-  if (lane == 0 && (!finite || (m > 0.f && m * sB < 0x1p-8f)))
-    atomicOr((uint32_t*)(hdr + 16) + row / 256, 1u);
   char* dst = planes + row * prow;
   for (int64_t s = lane; s < kpad / 8; s += 64) {   // one 8-k slot per lane
     float v[8];
@@ -623,24 +643,23 @@ __global__ void __launch_bounds__(256) planes_split_kernel(const float* __restri
 }
 
 // Exact max |x| per row and per column of X (rows x cols, row stride ld): a wave takes two rows
-// at a time, all their float4 loads issued before any is used (the pass is latency-bound
-// otherwise: one row's 4 KB per wave in flight reached ~2 TB/s), the row max by a wave
-// reduction, every lane keeping its columns' running max over the block's rows; the block's 8
-// waves combine in LDS, then one atomicMax per column (non-negative floats order as their bit
-// patterns; nan counts as inf; 256-B wave-instructions at the memory side). colmax must be zero
-// on entry. Either output may be NULL.
+// at a time, all their float4 loads issued before any is used, the row max by a wave reduction,
+// every lane keeping its columns' running max over the block's rows; the block's 4 waves combine
+// in LDS, then one atomicMax per column (non-negative floats order as their bit patterns; nan
+// counts as inf; 256-B wave-instructions at the memory side). Short blocks (32 rows) and CH
+// sized to the columns keep ~5 blocks per CU resident: with 128-row blocks of 8 waves (64 KB of
+// LDS, 151 VGPRs: one block per CU, two rounds of serial row pairs) the PPI pass ran at ~2 TB/s.
+// colmax must be zero on entry. Either output may be NULL.
 // VEC (ld % 4 == 0, X 16-byte aligned): unconditional float4 loads (a column index past cols
 // reads column 0 of the row and is zeroed; a partial last float4 stays inside the row stride).
-constexpr int kStatRows = 128;   // rows per block (16 per wave)
-template <bool VEC>
-__global__ void __launch_bounds__(512) absmax_rows_cols_kernel(const float* __restrict__ X,
+constexpr int kStatRows = 32;   // rows per block (8 per wave)
+template <int CH, bool VEC>     // CH: 256-column chunks per lane (cols <= 256 CH)
+__global__ void __launch_bounds__(256) absmax_rows_cols_kernel(const float* __restrict__ X,
                                                                int64_t rows, int64_t cols,
                                                                int64_t ld, float* rowmax,
                                                                uint32_t* colmax) {
-  constexpr int CH = 8;                       // 256-column chunks held per lane (cols <= 2048)
-  __shared__ float red[8][CH * 256];
+  __shared__ float red[4][CH * 256];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int nch = (int)((cols + 255) / 256);
   float4 cm[CH];
 #pragma unroll
   for (int j = 0; j < CH; ++j) cm[j] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -662,7 +681,7 @@ __global__ void __launch_bounds__(512) absmax_rows_cols_kernel(const float* __re
     return v;
   };
   const int64_t r0 = blockIdx.x * (int64_t)kStatRows, rend = min(rows, r0 + kStatRows);
-  for (int64_t r = r0 + 2 * wave; r < rend; r += 16) {
+  for (int64_t r = r0 + 2 * wave; r < rend; r += 8) {
     const bool two = r + 1 < rend;
     const float* x0 = X + r * ld;
     const float* x1 = X + (two ? r + 1 : r) * ld;
@@ -670,14 +689,15 @@ __global__ void __launch_bounds__(512) absmax_rows_cols_kernel(const float* __re
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
       const int64_t c = 256 * j + 4 * lane;
-      v0[j] = j < nch ? load(x0, c) : make_float4(0.f, 0.f, 0.f, 0.f);
-      v1[j] = j < nch && two ? load(x1, c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      v0[j] = load(x0, c);
+      v1[j] = load(x1, c);
     }
     float m0 = 0.f, m1 = 0.f;
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
       const float4 a = make_float4(absn(v0[j].x), absn(v0[j].y), absn(v0[j].z), absn(v0[j].w));
-      const float4 b = make_float4(absn(v1[j].x), absn(v1[j].y), absn(v1[j].z), absn(v1[j].w));
+      float4 b = make_float4(absn(v1[j].x), absn(v1[j].y), absn(v1[j].z), absn(v1[j].w));
+      if (!two) b = make_float4(0.f, 0.f, 0.f, 0.f);
       cm[j] = make_float4(fmaxf(cm[j].x, fmaxf(a.x, b.x)), fmaxf(cm[j].y, fmaxf(a.y, b.y)),
                           fmaxf(cm[j].z, fmaxf(a.z, b.z)), fmaxf(cm[j].w, fmaxf(a.w, b.w)));
       m0 = fmaxf(m0, fmaxf(fmaxf(a.x, a.y), fmaxf(a.z, a.w)));
@@ -695,15 +715,24 @@ __global__ void __launch_bounds__(512) absmax_rows_cols_kernel(const float* __re
   }
   if (!colmax) return;   // (uniform over the block: no barrier is skipped by part of it)
 #pragma unroll
-  for (int j = 0; j < CH; ++j)
-    if (j < nch) *(float4*)&red[wave][256 * j + 4 * lane] = cm[j];
+  for (int j = 0; j < CH; ++j) *(float4*)&red[wave][256 * j + 4 * lane] = cm[j];
   __syncthreads();
-  for (int c = threadIdx.x; c < cols; c += 512) {
-    float v = red[0][c];
-#pragma unroll
-    for (int w = 1; w < 8; ++w) v = fmaxf(v, red[w][c]);
+  for (int c = threadIdx.x; c < cols; c += 256) {
+    const float v = fmaxf(fmaxf(red[0][c], red[1][c]), fmaxf(red[2][c], red[3][c]));
     atomicMax(colmax + c, __float_as_uint(v));
   }
+}
+
+template <int CH>
+void launch_absmax(const float* X, int64_t rows, int64_t cols, int64_t ld, float* rowmax,
+                   float* colmax, hipStream_t stream) {
+  const unsigned nb = (unsigned)ceil_div(rows, (int64_t)kStatRows);
+  if (ld % 4 == 0 && (uintptr_t)X % 16 == 0)
+    absmax_rows_cols_kernel<CH, true><<<nb, 256, 0, stream>>>(X, rows, cols, ld, rowmax,
+                                                             (uint32_t*)colmax);
+  else
+    absmax_rows_cols_kernel<CH, false><<<nb, 256, 0, stream>>>(X, rows, cols, ld, rowmax,
+                                                              (uint32_t*)colmax);
 }
 
 }  // namespace
@@ -713,41 +742,119 @@ int absmax_rows_cols(const float* X, int64_t rows, int64_t cols, int64_t ld, flo
   GATX_REQUIRE(cols <= 2048, "absmax_rows_cols: at most 2048 columns");
   if (colmax) GATX_CALL(hipMemsetAsync(colmax, 0, cols * sizeof(float), stream));
   if (rows == 0) return 0;
-  const unsigned nb = (unsigned)ceil_div(rows, (int64_t)kStatRows);
-  if (ld % 4 == 0 && (uintptr_t)X % 16 == 0)
-    absmax_rows_cols_kernel<true><<<nb, 512, 0, stream>>>(X, rows, cols, ld, rowmax, (uint32_t*)colmax);
-  else
-    absmax_rows_cols_kernel<false><<<nb, 512, 0, stream>>>(X, rows, cols, ld, rowmax, (uint32_t*)colmax);
+  if (cols <= 512) launch_absmax<2>(X, rows, cols, ld, rowmax, colmax, stream);
+  else if (cols <= 1024) launch_absmax<4>(X, rows, cols, ld, rowmax, colmax, stream);
+  else if (cols <= 1280) launch_absmax<5>(X, rows, cols, ld, rowmax, colmax, stream);
+  else launch_absmax<8>(X, rows, cols, ld, rowmax, colmax, stream);
   GATX_LAUNCH_CHECK("absmax_rows_cols");
   return 0;
 }
 
 size_t weight_planes_bytes(int64_t rows, int64_t K) {
-  return (size_t)kPlanesHeader + (size_t)rows * round_up(K, (int64_t)32) * 4;
+  return (size_t)kPlanesHeader + (size_t)rows * round_up(K, (int64_t)32) * 4 +
+         4 * (size_t)(rows + ceil_div(rows, (int64_t)4));
 }
 
 int build_weight_planes(const float* W, int64_t rows, int64_t K, int64_t ld, void* buf,
                         hipStream_t stream) {
   GATX_REQUIRE(rows <= 60 * 256, "weight planes: at most 15360 rows (tile flags in the header)");
-  GATX_CALL(hipMemsetAsync(buf, 0, kPlanesHeader, stream));
   char* planes = (char*)buf + kPlanesHeader;
-  const int64_t n = rows * K;
-  const unsigned gb = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, 256 * 8), 1024));
-  planes_max_kernel<<<gb, 256, 0, stream>>>(W, rows, K, ld, (uint32_t*)((char*)buf + 8));
+  float* rowmax = (float*)(planes + rows * round_up(K, (int64_t)32) * 4);
+  const int64_t nblk = ceil_div(rows, (int64_t)4);
+  float* blockmax = rowmax + rows;
+  planes_max_kernel<<<(unsigned)nblk, 256, 0, stream>>>(W, rows, K, ld, rowmax, blockmax);
   GATX_LAUNCH_CHECK("weight_planes max");
-  planes_split_kernel<<<(unsigned)ceil_div(rows, (int64_t)4), 256, 0, stream>>>(W, rows, K, ld,
-                                                                               planes);
+  planes_split_kernel<<<(unsigned)nblk, 256, 0, stream>>>(W, rows, K, ld, planes, rowmax,
+                                                          blockmax, nblk);
   GATX_LAUNCH_CHECK("weight_planes split");
   return 0;
 }
 
+// The weight gradient's thin rows: C rows [256 tiles_m, M) (at most kThinRows: G_aug's score-
+// gradient columns past a multiple of 256, e.g. PPI L1's 1024 + 8) in plain fp32 on the VALU, so
+// the MFMA kernel's tiles are all full (a 256-row tile for 8 rows cost a fifth of PPI L1's weight
+// gradient). C[m][n] = sum_k A[k][m] B[k][n] over this split's K range: 16 waves x 4 k-groups of
+// lanes walk the rows (each lane 4 columns of a 64-column chunk, 256-B row segments), partials
+// summed over the 64 (wave, group) slices in fixed order through LDS. Writes the split's slab (or
+// C when there is no split), which splitk_reduce_kernel sums with the MFMA kernel's rows.
+constexpr int kThinRows = 8;
+__global__ void __launch_bounds__(1024) wgrad_thin_kernel(GemmArgs g) {
+  constexpr int T = kThinRows, KG = 4, NW = 16, CW = 64;
+  __shared__ float red[NW * KG][T][CW];   // 128 KB
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int kg = lane >> 4, cq = lane & 15;
+  const int64_t m0 = g.tiles_m * 256;
+  const int64_t n = blockIdx.x * (int64_t)CW + 4 * cq;
+  const int z = blockIdx.y;
+  const int64_t kb = (int64_t)z * g.k_per_split, ke = min(g.K, kb + g.k_per_split);
+  const bool nv = n < g.N;   // (N % 4 == 0: the vector path)
+  const int64_t T_rows = g.M - m0;
+  float acc[T][4];
+#pragma unroll
+  for (int t = 0; t < T; ++t) acc[t][0] = acc[t][1] = acc[t][2] = acc[t][3] = 0.f;
+  const float* B = g.B + (nv ? n : 0);
+  const float* A = g.A + m0;
+  constexpr int U = 4, STEP = NW * KG;   // rows per slice per iteration; slices
+  for (int64_t k0 = kb + wave * KG + kg; k0 < ke; k0 += (int64_t)STEP * U) {
+    float4 b[U];
+    float a[U][T];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t k = k0 + (int64_t)u * STEP;
+      const bool ok = k < ke;
+      const int64_t kk = ok ? k : kb;
+      b[u] = *(const float4*)(B + kk * g.ldb);
+      if (!ok || !nv) b[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int t = 0; t < T; ++t) a[u][t] = t < T_rows ? A[kk * g.lda + t] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        acc[t][0] = fmaf(a[u][t], b[u].x, acc[t][0]);
+        acc[t][1] = fmaf(a[u][t], b[u].y, acc[t][1]);
+        acc[t][2] = fmaf(a[u][t], b[u].z, acc[t][2]);
+        acc[t][3] = fmaf(a[u][t], b[u].w, acc[t][3]);
+      }
+  }
+  const int slice = wave * KG + kg;
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+    *(float4*)&red[slice][t][4 * cq] = make_float4(acc[t][0], acc[t][1], acc[t][2], acc[t][3]);
+  __syncthreads();
+  if (threadIdx.x < T * CW) {
+    const int t = threadIdx.x / CW, c = threadIdx.x % CW;
+    float v = 0.f;
+    for (int s2 = 0; s2 < NW * KG; ++s2) v += red[s2][t][c];
+    const int64_t row = m0 + t, col = blockIdx.x * (int64_t)CW + c;
+    if (row < g.M && col < g.N) {
+      if (g.splits > 1) g.partial[(int64_t)z * g.M * g.N + row * g.N + col] = v;
+      else g.C0[row * g.ldc0 + col] = v;
+    }
+  }
+}
+
+int wgrad_thin_rows(int64_t M) {
+  const int64_t r = M % 256;
+  return (M > 256 && r > 0 && r <= kThinRows) ? (int)r : 0;
+}
+
 // The weight-gradient kernel (row-contiguous A and B, split-K slabs; g.a_rowmax = the exact
-// max of every A row, i.e. of every G_aug column).
+// max of every A row, i.e. of every G_aug column); rows past 256 tiles_m (< M: the thin rows,
+// see wgrad_thin_rows) by wgrad_thin_kernel.
 int launch_gemm_f16rc(const gk::GemmArgs& g, hipStream_t stream) {
   dim3 grid((unsigned)(g.tiles_m * g.tiles_n), 1u, (unsigned)g.splits);
   if (g.a_vec && g.b_vec) gemm_f16rc_kernel<true><<<grid, 512, 0, stream>>>(g);
   else gemm_f16rc_kernel<false><<<grid, 512, 0, stream>>>(g);
   GATX_LAUNCH_CHECK("gemm_f16rc");
+  if (g.tiles_m * 256 < g.M) {
+    GATX_REQUIRE(g.M - g.tiles_m * 256 <= kThinRows && g.b_vec && g.N % 4 == 0,
+                 "gemm_f16rc: thin rows out of range");
+    wgrad_thin_kernel<<<dim3((unsigned)ceil_div(g.N, (int64_t)64), (unsigned)g.splits), 1024, 0,
+                        stream>>>(g);
+    GATX_LAUNCH_CHECK("wgrad_thin");
+  }
   return 0;
 }
 

@@ -138,8 +138,9 @@ int gatx_transpose_f32(int64_t rows, int64_t cols, const float* src, int64_t ld_
 void gatx_set_gemm_mode(int mode);
 int gatx_get_gemm_mode(void);
 /* Pre-split weight planes for the f16x3 GEMMs (gemm_f16p.hip): W (rows x K, row stride ld) as two
- * fp16 planes per element with one power-of-two scale for the whole matrix, plus a 256-byte
- * header (the scale and per-256-row-tile range flags). Built once per weight version (the
+ * fp16 planes per element with one power-of-two scale for the whole matrix, a 256-byte header
+ * (the scale and per-256-row-tile range flags) and the build's scratch (row maxima; two launches,
+ * no memset). Built once per weight version (the
  * projection's W_aug, the backward's W_aug^T) and passed to gatx_gemm_planes; the buffer
  * (gatx_weight_planes_bytes) must be 256-byte aligned. Replaces nothing in the reference: it is
  * how `self.W(x)` (models/gat_layer.py:64) keeps fp32 accuracy on the fp16 matrix cores. */

@@ -305,14 +305,17 @@ def test_gemm_tail_split(device):
             assert (outs[0] - outs[2]).abs().max().item() < 2e-4 * K ** 0.5
 
 
-@pytest.mark.parametrize("variant", ["counting", "hubs", "no_rewrite", "degree_64"])
+@pytest.mark.parametrize("variant", ["counting", "hubs", "no_rewrite", "degree_64", "two_pass"])
 def test_graph_build_matches_oracle(variant, device):
     """edge_index' and both CSRs against the oracle's rewrite and numpy stable sorts: random
     graphs with self-loops, duplicates and isolated nodes, hub nodes of degree 300 (one wave per
-    segment must loop over many 64-edge batches), with and without the self-loop rewrite."""
+    segment must loop over many 64-edge batches), with and without the self-loop rewrite; up to
+    4095 nodes the sorts take one 12-bit pass whose scatter writes rowptr itself, "two_pass"
+    (6007 nodes) the 8-bit passes and rowptr_kernel. The padding slots past E' hold N in col and
+    rowidx (the transpose sorts col as its keys)."""
     gatx = _gatx()
     from gatx import data as gd
-    b = gd.uniform_graph_batch(3, 500, 4000, 4)
+    b = gd.uniform_graph_batch(3, 2000 if variant == "two_pass" else 500, 4000, 4)
     N = b.num_nodes + 7                 # trailing isolated nodes too
     ei = b.edge_index.copy()
     ei[:, :50] = ei[0, :50]            # some self-loops
@@ -341,11 +344,17 @@ def test_graph_build_matches_oracle(variant, device):
     np.testing.assert_array_equal(col, ref[0][order])
     np.testing.assert_array_equal(g.rowidx[:g.num_edges].cpu().numpy(), dst[order])
     np.testing.assert_array_equal(np.diff(rowptr), counts)
+    assert rowptr[0] == 0 and rowptr[-1] == g.num_edges
+    E2 = g.num_edges
+    if rewrite:
+        assert g.col.numel() > E2   # (50 self-loops dropped: padding slots exist)
+    assert bool((g.col[E2:] == N).all()) and bool((g.rowidx[E2:] == N).all())
     g.ensure_transpose()
     srow = g.srowptr.cpu().numpy()
     scol = g.scol[:g.num_edges].cpu().numpy()
     seid = g.seid[:g.num_edges].cpu().numpy()
     np.testing.assert_array_equal(np.diff(srow), np.bincount(ref[0], minlength=N))
+    assert srow[0] == 0 and srow[-1] == E2
     np.testing.assert_array_equal(seid, np.argsort(col, kind="stable"))
     np.testing.assert_array_equal(scol, dst[order][seid])
 
@@ -887,8 +896,9 @@ def test_gemm_wgrad_accuracy(device):
     from gatx._lib import call, lib, ptr, stream
     torch.manual_seed(14)
     fb = torch.zeros(1, dtype=torch.int64, device=device)
+    # (ppi_l1 and thin4: rows past the last multiple of 256 go to the VALU thin-row kernel)
     for (KC, F_in, N, case) in ((1032, 1024, 44900, "ppi_l1"), (756, 1024, 9001, "ppi_l2"),
-                                (1032, 1024, 20000, "dead_feature")):
+                                (1032, 1024, 20000, "dead_feature"), (516, 1000, 5003, "thin4")):
         G = torch.randn(N, KC, device=device) * 1e-6
         G[:, :KC // 3] *= torch.logspace(-3, 3, KC // 3, device=device)   # 1e-9 .. 1e-3
         G[:, -8:] *= 1e9                                                   # score columns ~1e3

@@ -224,6 +224,157 @@ __global__ void __launch_bounds__(NT, 1) f16v2_kernel(LabArgs g) {
   }
 }
 
+// v3: the same staging with 32-deep K-tiles, the MFMA phase on v_mfma_f32_16x16x32_f16 (one
+// instruction per plane pair covers the whole K-tile; the guide measures ~1.12-1.15x the FLOP/s of
+// 32x32x16 under load at equal cycles, from the clock the chip holds). Wave tile 128 x 64 =
+// 8 x 4 blocks of 16 x 16; A fragments read just in time per 16-row block (register budget).
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+template <bool SCALE>
+__global__ void __launch_bounds__(NT, 1) f16v3_kernel(LabArgs g) {
+  constexpr int BK = 32;
+  using I = Img<BK>;
+  constexpr int PB = I::BYTES;
+  constexpr int STAGE = 4 * PB;
+  constexpr int NVA = BK / 8, NVB = BK / 8, TPR = BK / 4;
+  constexpr int M16 = 8, N16 = 4;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 256 * 4];
+  float* inv = (float*)(smem + 2 * STAGE);
+  const int64_t T = ((g.M + TBM - 1) / TBM) * ((g.N + TBN - 1) / TBN);
+  int64_t tm, tn;
+  tile_of(blockIdx.x, T, (g.N + TBN - 1) / TBN, tm, tn);
+  const int64_t m0 = tm * TBM, n0 = tn * TBN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int64_t arows = g.M - m0 < TBM ? g.M - m0 : TBM;
+  const int64_t brows = g.N - n0 < TBN ? g.N - n0 : TBN;
+  const auto ra = rsrc(g.A + m0 * g.lda, arows * g.lda * 4);
+  const auto rb = rsrc((const char*)g.Bp + n0 * g.brow, brows * g.brow);
+  int voa[NVA], vob[NVB], oa[NVA], ob[NVB];
+#pragma unroll
+  for (int c = 0; c < NVA; ++c) {
+    const int idx = tid + NT * c;
+    const int r = idx / TPR, k = 4 * (idx % TPR), j = idx % TPR;
+    voa[c] = (r * (int)g.lda + k) * 4;
+    oa[c] = I::off(r, k);
+    vob[c] = r * (int)g.brow + (j >> 1) * 32 + (j & 1) * 16;
+    ob[c] = (2 + (j & 1)) * PB + I::off(r, 8 * (j >> 1));
+  }
+  float4 va[NVA];
+  uint4 vb[NVB];
+  auto load = [&](int kt) {
+#pragma unroll
+    for (int c = 0; c < NVA; ++c)
+      va[c] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ra, voa[c], kt * BK * 4, 0));
+#pragma unroll
+    for (int c = 0; c < NVB; ++c)
+      vb[c] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rb, vob[c], kt * BK * 4, 0));
+  };
+  float cs[NVA], amax[NVA];
+#pragma unroll
+  for (int c = 0; c < NVA; ++c) { cs[c] = 64.f; amax[c] = 0.f; }
+  auto store = [&](char* st) {
+#pragma unroll
+    for (int c = 0; c < NVA; ++c) {
+      const float4 v = va[c];
+      amax[c] = fmaxf(amax[c], fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+      uint32_t h0, l0, h1, l1;
+      split_mix(v.x, v.y, cs[c], h0, l0);
+      split_mix(v.z, v.w, cs[c], h1, l1);
+      *(uint2*)(st + oa[c]) = make_uint2(h0, h1);
+      *(uint2*)(st + PB + oa[c]) = make_uint2(l0, l1);
+    }
+#pragma unroll
+    for (int c = 0; c < NVB; ++c) *(uint4*)(st + ob[c]) = vb[c];
+  };
+  floatx4 acc[M16][N16];
+#pragma unroll
+  for (int i = 0; i < M16; ++i)
+#pragma unroll
+    for (int j = 0; j < N16; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int nk = (int)(g.K / BK);
+  load(0);
+  if constexpr (SCALE) {
+#pragma unroll
+    for (int c = 0; c < NVA; ++c) {
+      const float4 v = va[c];
+      float m = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+#pragma unroll
+      for (int o = 1; o < TPR; o <<= 1) m = fmaxf(m, __shfl_xor(m, o));
+      int e = 0;
+      (void)frexpf(m, &e);
+      const float sc = (m > 0.f && m <= 3.0e38f) ? ldexpf(1.f, 8 - e) : 1.f;
+      cs[c] = 64.f * sc;
+      if ((tid % TPR) == 0) inv[(tid + NT * c) / TPR] = 1.f / sc;
+    }
+  } else {
+    if (tid < 256) inv[tid] = 1.f;
+  }
+  store(smem);
+  if (nk > 1) load(1);
+  __syncthreads();
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* cur = smem + (kt & 1) * STAGE;
+    char* nxt = smem + ((kt & 1) ^ 1) * STAGE;
+    f16x8 fb[N16][2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int x = 0; x < N16; ++x)
+        fb[x][p] = *(const f16x8*)(cur + (2 + p) * PB + I::off(wn * 64 + x * 16 + fr, fk));
+    f16x8 fa0[2], fa1[2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) fa0[p] = *(const f16x8*)(cur + p * PB + I::off(wm * 128 + fr, fk));
+    if (kt + 1 < nk) store(nxt);
+    if (kt + 2 < nk) load(kt + 2);
+#pragma unroll
+    for (int mi = 0; mi < M16; ++mi) {
+      if (mi + 1 < M16) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+          fa1[p] = *(const f16x8*)(cur + p * PB + I::off(wm * 128 + (mi + 1) * 16 + fr, fk));
+      }
+#pragma unroll
+      for (int ni = 0; ni < N16; ++ni)
+        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[ni][1], fa0[0], acc[mi][ni], 0, 0, 0);
+#pragma unroll
+      for (int ni = 0; ni < N16; ++ni)
+        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[ni][0], fa0[1], acc[mi][ni], 0, 0, 0);
+#pragma unroll
+      for (int ni = 0; ni < N16; ++ni)
+        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[ni][0], fa0[0], acc[mi][ni], 0, 0, 0);
+      fa0[0] = fa1[0];
+      fa0[1] = fa1[1];
+    }
+    __syncthreads();
+  }
+  bool bad = false;
+#pragma unroll
+  for (int c = 0; c < NVA; ++c) {
+    float m = amax[c];
+#pragma unroll
+    for (int o = 1; o < TPR; o <<= 1) m = fmaxf(m, __shfl_xor(m, o));
+    const float s = cs[c] * (1.f / 64.f);
+    bad |= !(m * s <= 1023.f) || (m > 0.f && m * s < 0x1p-9f);
+  }
+  if (__syncthreads_or(bad) && tid == 0) atomicAdd(g.bad, 1);
+  // lane -> output row (lane & 15) of the block, registers -> 4 consecutive columns
+#pragma unroll
+  for (int mi = 0; mi < M16; ++mi) {
+    const int rl = wm * 128 + mi * 16 + fr;
+    const int64_t row = m0 + rl;
+    if (row >= g.M) continue;
+    const float f = inv[rl] * g.binv;
+#pragma unroll
+    for (int ni = 0; ni < N16; ++ni) {
+      const int64_t col = n0 + wn * 64 + ni * 16 + 4 * (lane >> 4);
+      if (col + 3 < g.N)
+        *(float4*)(g.C + row * g.ldc + col) =
+            make_float4(acc[mi][ni][0] * f, acc[mi][ni][1] * f, acc[mi][ni][2] * f, acc[mi][ni][3] * f);
+    }
+  }
+}
+
 // B planes: row n, slot s (8 k): fp16 h[8] = fp16(32 sB b), then l[8] = fp16(32 sB b - h).
 __global__ void split_b_kernel(const float* B, int64_t N, int64_t K, int64_t ldb, float c,
                                uint16_t* Bp, int64_t brow) {
@@ -254,7 +405,10 @@ extern "C" int lab_gemm(int bk, int scale, const float* A, int64_t lda, const ui
                         int* bad, hipStream_t s) {
   LabArgs g{A, lda, Bp, K * 4, M, N, K, C, ldc, binv, bad};
   const unsigned grid = (unsigned)(((M + 255) / 256) * ((N + 255) / 256));
-  if (bk == 16) {
+  if (bk == 33) {   // v3: 32-deep K-tiles on 16x16x32 MFMAs
+    if (scale) f16v3_kernel<true><<<grid, NT, 0, s>>>(g);
+    else f16v3_kernel<false><<<grid, NT, 0, s>>>(g);
+  } else if (bk == 16) {
     if (scale) f16v2_kernel<16, true><<<grid, NT, 0, s>>>(g);
     else f16v2_kernel<16, false><<<grid, NT, 0, s>>>(g);
   } else {

@@ -59,9 +59,10 @@ def main():
                  ptr(ws) if wsb else None, wsb, stream())
 
         variants = {"lib f16x3": lib_run}
-        for bk in (16, 32):
-            for sc in (0, 1):
-                variants[f"v2 bk{bk} scale{sc}"] = (
+        for bk in (16, 32, 33):
+            for sc in (0,):
+                name_ = f"v2 bk{bk} scale{sc}" if bk != 33 else f"v3 16x16x32 scale{sc}"
+                variants[name_] = (
                     lambda bk=bk, sc=sc: lab.lab_gemm(bk, sc, ptr(A), K, ptr(Bp), M, N, K,
                                                       2.0 ** -11 / sB, ptr(C), N, ptr(bad),
                                                       stream()))

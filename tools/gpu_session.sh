@@ -14,15 +14,27 @@ fi
 step bench timeout -k 10 300 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
 step bench_train timeout -k 10 300 python bench.py --mode train --no-cpu-baseline > "$OUT/bench_train.json" 2> "$OUT/bench_train.err"
 step bench_train_nof16p env GATX_F16P=0 timeout -k 10 300 python bench.py --mode train --no-cpu-baseline > "$OUT/bench_train_nof16p.json" 2> "$OUT/bench_train_nof16p.err"
+if [ "${BK32:-0}" = 1 ]; then
+  step bench_bk32 env GATX_F16P_BK=32 timeout -k 10 300 python bench.py --no-cpu-baseline > "$OUT/bench_bk32.json" 2> "$OUT/bench_bk32.err"
+  step bench_train_bk32 env GATX_F16P_BK=32 timeout -k 10 300 python bench.py --mode train --no-cpu-baseline > "$OUT/bench_train_bk32.json" 2> "$OUT/bench_train_bk32.err"
+fi
 step bench_pattern timeout -k 10 300 python bench.py --workload pattern --graphs 8 --mode train --no-cpu-baseline > "$OUT/bench_pattern_train.json" 2> "$OUT/bench_pattern_train.err"
 cd /tmp && export TMPDIR=/tmp
 step prof_train timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_train" -o run --output-format csv -- python3 "$R/bench.py" --mode train --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/prof_train.log" 2>&1
 step prof_pattern timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_pattern" -o run --output-format csv -- python3 "$R/bench.py" --workload pattern --graphs 8 --mode train --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/prof_pattern.log" 2>&1
 cd "$R"
+if [ "${LAB:-1}" = 1 ]; then
+  step lab timeout -k 10 300 python tools/gemm_lab/run_lab.py > "$OUT/lab.txt" 2>&1
+  cat "$OUT/lab.txt" >&3
+fi
 python - "$OUT" >&3 <<'PY'
 import json, sys
 o = sys.argv[1]
-for f in ("bench", "bench_train", "bench_train_nof16p", "bench_pattern_train"):
+import os
+for f in ("bench", "bench_train", "bench_train_nof16p", "bench_bk32", "bench_train_bk32",
+          "bench_pattern_train"):
+    if not os.path.exists(f"{o}/{f}.json"):
+        continue
     d = json.load(open(f"{o}/{f}.json"))
     print(f, d["ms_per_step"], d["roofline"]["kernel"], d["roofline"]["frac"], d.get("roofline_time_frac"))
     print("  ", {k: round(v["total_ms_per_step"], 4) for k, v in d.get("kernels", {}).items()})
