@@ -37,6 +37,57 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(GemmArgs g, int batc
   }
 }
 
+// The same reduction four columns at a time for a plain output (one batch entry, one output
+// range, no bias / residual / ELU; N % 4 == 0, C0 16-byte aligned, ldc0 % 4 == 0): float4 slab
+// loads, slabs summed in the same order (z ascending), so the result equals splitk_reduce_kernel's.
+__global__ void __launch_bounds__(256) splitk_reduce4_kernel(GemmArgs g) {
+  const int64_t MN = g.M * g.N, total4 = MN / 4, n4 = g.N / 4;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total4;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = t / n4, col = 4 * (t - row * n4);
+    const float* p = g.partial + row * g.N + col;
+    float4 v = *(const float4*)p;
+    int z = 1;
+    for (; z + 4 <= g.splits; z += 4) {
+      const float4 a = *(const float4*)(p + (int64_t)z * MN);
+      const float4 b = *(const float4*)(p + (int64_t)(z + 1) * MN);
+      const float4 c = *(const float4*)(p + (int64_t)(z + 2) * MN);
+      const float4 d = *(const float4*)(p + (int64_t)(z + 3) * MN);
+      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+      v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+      v.x += c.x; v.y += c.y; v.z += c.z; v.w += c.w;
+      v.x += d.x; v.y += d.y; v.z += d.z; v.w += d.w;
+    }
+    for (; z < g.splits; ++z) {
+      const float4 a = *(const float4*)(p + (int64_t)z * MN);
+      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+    }
+    float* o = g.C0 + row * g.ldc0 + col;
+    if (g.accumulate) {
+      const float4 c = *(const float4*)o;
+      v.x += c.x; v.y += c.y; v.z += c.z; v.w += c.w;
+    }
+    *(float4*)o = v;
+  }
+}
+
+inline bool reduce4_ok(const GemmArgs& g, int batch) {
+  return batch == 1 && g.N % 4 == 0 && g.n_split >= g.N && !g.bias && !g.resid && !g.elu &&
+         g.ldc0 % 4 == 0 && (uintptr_t)g.C0 % 16 == 0;
+}
+
+void launch_splitk_reduce(const GemmArgs& g, int batch, hipStream_t stream) {
+  if (reduce4_ok(g, batch)) {
+    const int64_t total4 = g.M * g.N / 4;
+    splitk_reduce4_kernel<<<(unsigned)std::min<int64_t>(ceil_div(total4, 256), 8192), 256, 0,
+                            stream>>>(g);
+  } else {
+    const int64_t total = g.M * g.N * batch;
+    splitk_reduce_kernel<<<(unsigned)std::min<int64_t>(ceil_div(total, 256), 8192), 256, 0,
+                           stream>>>(g, batch);
+  }
+}
+
 // Tiny products (K <= 64, M N K <= 2^25 multiply-adds: PATTERN's projections) on the VALU in
 // plain fp32: the tiled MFMA kernels spend 10-14 us there on prologue,
 // barriers and a handful of K-tiles for a few MFLOP, while this is launch-bound (~3 us). Each
@@ -334,9 +385,7 @@ int launch_f16p_and_fixups(const GemmArgs& g, int tag, hipStream_t stream) {
 int launch_f16rc_and_reduce(const GemmArgs& g, hipStream_t stream) {
   GATX_CALL(launch_gemm_f16rc(g, stream));
   if (g.splits > 1) {
-    const int64_t total = g.M * g.N;
-    const unsigned rg = (unsigned)std::min<int64_t>(ceil_div(total, 256), 8192);
-    splitk_reduce_kernel<<<rg, 256, 0, stream>>>(g, 1);
+    launch_splitk_reduce(g, 1, stream);
     GATX_LAUNCH_CHECK("splitk_reduce");
   }
   return 0;
@@ -374,9 +423,7 @@ int launch_gemm(const GemmArgs& g0, bool a_kc, bool b_kc, int batch, hipStream_t
     GATX_LAUNCH_CHECK("gemm_f32");
   }
   if (g.splits > 1) {
-    const int64_t total = g.M * g.N * batch;
-    const unsigned rg = (unsigned)std::min<int64_t>(ceil_div(total, 256), 8192);
-    splitk_reduce_kernel<<<rg, 256, 0, stream>>>(g, batch);
+    launch_splitk_reduce(g, batch, stream);
     GATX_LAUNCH_CHECK("splitk_reduce");
   }
   if (g.tail_s > 1 && g.s_part) {
@@ -601,7 +648,7 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
   // kernel (gemm_f16p.hip), its 256-row tiles all full (a few rows past them: the thin kernel)
   const bool wgrad_f16 = a_rowmax && tag == 2 && gemm_mode() == 2 && f16p_enabled() &&
                          kd.id == 2 && batch == 1 && !a_kc && !b_kc && !accumulate;
-  if (wgrad_f16 && wgrad_thin_rows(M) && g.b_vec && N % 4 == 0) g.tiles_m = M / kd.bm;
+  if (wgrad_f16 && wgrad_thin_rows(M) && g.a_vec && g.b_vec && N % 4 == 0) g.tiles_m = M / kd.bm;
   const int64_t tiles = g.tiles_m * g.tiles_n * batch;
   const int64_t slots = resident_blocks(kd);
   // fused scores: x3 tiles, one batch entry, no split-K; the partials take the workspace's end

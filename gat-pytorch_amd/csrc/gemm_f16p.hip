@@ -508,9 +508,15 @@ __global__ void __launch_bounds__(512, 1) gemm_f16rc_kernel(GemmArgs g) {
   constexpr int SMEM = 2 * 5 * (256 * 16 * 2) > 2 * 3 * 2 * (256 + 256) * 16
                            ? 2 * 5 * (256 * 16 * 2) : 2 * 3 * 2 * (256 + 256) * 16;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
-  int64_t tm, tn;
-  tile_of(blockIdx.x, g.tiles_m * g.tiles_n, g.tiles_n, tm, tn);
-  const int64_t kb = blockIdx.z * g.k_per_split;
+  // 1-D grid over (split, tile), XCD-contiguous: the tiles of one K-split (which read the same
+  // G_aug and x rows at about the same time) share an XCD and its L2 — round-robin placement put
+  // them on different XCDs and fetched each operand slab ~3x
+  const int64_t TT = g.tiles_m * g.tiles_n;
+  int64_t z, tile, tm, tn;
+  tile_of(blockIdx.x, TT * g.splits, TT, z, tile);
+  tm = tile / g.tiles_n;
+  tn = tile - tm * g.tiles_n;
+  const int64_t kb = z * g.k_per_split;
   const int64_t K = min(g.K, kb + g.k_per_split);
   const int64_t m0 = tm * C::TBM, n0 = tn * C::TBN;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -550,7 +556,7 @@ __global__ void __launch_bounds__(512, 1) gemm_f16rc_kernel(GemmArgs g) {
                                             acc);
     }
   }
-  write_tile_t<C::MB, C::NB, C::TBM, C::TBN>(g, acc, -1, 0, m0, n0, wm, wn, lane);
+  write_tile_t<C::MB, C::NB, C::TBM, C::TBN>(g, acc, -1, 0, m0, n0, wm, wn, lane, z);
 }
 
 // ---- weight planes (gatx_weight_planes) ---------------------------------------------------------
@@ -794,6 +800,7 @@ __global__ void __launch_bounds__(1024) wgrad_thin_kernel(GemmArgs g) {
   for (int t = 0; t < T; ++t) acc[t][0] = acc[t][1] = acc[t][2] = acc[t][3] = 0.f;
   const float* B = g.B + (nv ? n : 0);
   const float* A = g.A + m0;
+  static_assert(T == 8, "two float4 loads per row");
   constexpr int U = 4, STEP = NW * KG;   // rows per slice per iteration; slices
   for (int64_t k0 = kb + wave * KG + kg; k0 < ke; k0 += (int64_t)STEP * U) {
     float4 b[U];
@@ -805,8 +812,16 @@ __global__ void __launch_bounds__(1024) wgrad_thin_kernel(GemmArgs g) {
       const int64_t kk = ok ? k : kb;
       b[u] = *(const float4*)(B + kk * g.ldb);
       if (!ok || !nv) b[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      // the row's thin A values as 16-byte loads (a_vec: lda % 4 == 0 and A aligned; m0 % 256
+      // == 0); columns past M are masked and stay inside the row stride (lda >= round4(M)), the
+      // second load only when more than 4 rows remain
+      const float4 a0 = *(const float4*)(A + kk * g.lda);
+      const float4 a1 = T_rows > 4 ? *(const float4*)(A + kk * g.lda + 4)
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+      a[u][0] = a0.x; a[u][1] = a0.y; a[u][2] = a0.z; a[u][3] = a0.w;
+      a[u][4] = a1.x; a[u][5] = a1.y; a[u][6] = a1.z; a[u][7] = a1.w;
 #pragma unroll
-      for (int t = 0; t < T; ++t) a[u][t] = t < T_rows ? A[kk * g.lda + t] : 0.f;
+      for (int t = 0; t < T; ++t) a[u][t] = t < T_rows ? a[u][t] : 0.f;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -844,12 +859,12 @@ int wgrad_thin_rows(int64_t M) {
 // max of every A row, i.e. of every G_aug column); rows past 256 tiles_m (< M: the thin rows,
 // see wgrad_thin_rows) by wgrad_thin_kernel.
 int launch_gemm_f16rc(const gk::GemmArgs& g, hipStream_t stream) {
-  dim3 grid((unsigned)(g.tiles_m * g.tiles_n), 1u, (unsigned)g.splits);
+  dim3 grid((unsigned)(g.tiles_m * g.tiles_n * g.splits), 1u, 1u);
   if (g.a_vec && g.b_vec) gemm_f16rc_kernel<true><<<grid, 512, 0, stream>>>(g);
   else gemm_f16rc_kernel<false><<<grid, 512, 0, stream>>>(g);
   GATX_LAUNCH_CHECK("gemm_f16rc");
   if (g.tiles_m * 256 < g.M) {
-    GATX_REQUIRE(g.M - g.tiles_m * 256 <= kThinRows && g.b_vec && g.N % 4 == 0,
+    GATX_REQUIRE(g.M - g.tiles_m * 256 <= kThinRows && g.a_vec && g.b_vec && g.N % 4 == 0,
                  "gemm_f16rc: thin rows out of range");
     wgrad_thin_kernel<<<dim3((unsigned)ceil_div(g.N, (int64_t)64), (unsigned)g.splits), 1024, 0,
                         stream>>>(g);

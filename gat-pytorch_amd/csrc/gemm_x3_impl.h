@@ -556,10 +556,11 @@ __device__ inline float4 f4_of(const floatx16& a, int j) {
   return make_float4(a[4 * j], a[4 * j + 1], a[4 * j + 2], a[4 * j + 3]);
 }
 
+// slab (split-K): the partial slab this block writes; -1 = blockIdx.z (x gridDim.y + y).
 template <int MB, int NB, int TBM, int TBN>
 __device__ inline void write_tile_t(const GemmArgs& g, floatx16 (&acc)[MB][NB], int tail_z,
                                     int64_t tail_ti, int64_t m0, int64_t n0, int wm, int wn,
-                                    int lane) {
+                                    int lane, int64_t slab = -1) {
   const int lr = lane & 31, lc = 4 * (lane >> 5);
   const int64_t M = g.M, N = g.N;
   if (tail_z >= 0) {   // tail slice: tile-local partial [TBM][TBN], summed by tail_fixup_kernel
@@ -576,7 +577,9 @@ __device__ inline void write_tile_t(const GemmArgs& g, floatx16 (&acc)[MB][NB], 
     return;
   }
   if (g.splits > 1) {   // partial slab z: plain [M][N], reduced by splitk_reduce_kernel
-    float* P = g.partial + ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * M * N;
+    const int64_t z = slab >= 0 ? slab : (int64_t)blockIdx.z * gridDim.y + blockIdx.y;
+    float* P = g.partial + z * M * N;
+    const bool v4 = (N & 3) == 0;   // (the slab base is 16-byte aligned: M N floats per slab)
 #pragma unroll
     for (int mi = 0; mi < MB; ++mi)
 #pragma unroll
@@ -584,9 +587,15 @@ __device__ inline void write_tile_t(const GemmArgs& g, floatx16 (&acc)[MB][NB], 
         const int64_t row = m0 + wm * (MB * 32) + mi * 32 + lr;
         if (row >= M) continue;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int64_t col = n0 + wn * (NB * 32) + ni * 32 + 8 * (r >> 2) + lc + (r & 3);
-          if (col < N) P[row * N + col] = acc[mi][ni][r];
+        for (int j = 0; j < 4; ++j) {
+          const int64_t col = n0 + wn * (NB * 32) + ni * 32 + 8 * j + lc;
+          if (v4 && col + 3 < N) {
+            *(float4*)(P + row * N + col) = f4_of(acc[mi][ni], j);
+          } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              if (col + i < N) P[row * N + col + i] = acc[mi][ni][4 * j + i];
+          }
         }
       }
     return;
