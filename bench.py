@@ -495,7 +495,14 @@ def roofline_objects(summ, edge_bytes, pm, n_instr, pm_path="", gather_E2=None):
         ms_ = sum(t for _, t in gem)
         tfs = fl / (ms_ * 1e-3) / 1e12
         gr = gemm_roof()
-        roofs["gemm"] = {"bound": "mfma", "kernel": gr["kernel"] + ", projection x.W_aug^T",
+        from gatx.functional import use_weight_planes
+        label = gr["kernel"]
+        if gr["mode"] == "f16x3" and not any(use_weight_planes(nh * f + 2 * nh, fin, n)
+                                             for (n, _, fin, nh, f), _ in gem):
+            # (small layers: the tiled / small-K / tiny kernels the library picks by shape)
+            label = ("tiled / small-K GEMM kernels by shape, f16x3 arithmetic where tiled (peak "
+                     "= dense fp16 2500 TF / 3)")
+        roofs["gemm"] = {"bound": "mfma", "kernel": label + ", projection x.W_aug^T",
                          "achieved": round(tfs, 2), "peak": round(gr["peak"], 1),
                          "unit": "TFLOP/s", "frac": round(tfs / gr["peak"], 4), "traffic": None,
                          # the same fp32 flops against the native fp32 MFMA peak (context only:

@@ -31,8 +31,20 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(GemmArgs g, int batc
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t b = t / MN, mn = t - b * MN, row = mn / g.N, col = mn - row * g.N;
+    // slabs summed in order z = 0, 1, ...; eight loads issued before their adds (a small output
+    // split 64 ways waited one load latency per slab)
+    const float* p = g.partial + b * MN + mn;
+    const int64_t zs = (int64_t)batch * MN;
     float v = 0.f;
-    for (int z = 0; z < g.splits; ++z) v += g.partial[((int64_t)z * batch + b) * MN + mn];
+    int z = 0;
+    for (; z + 8 <= g.splits; z += 8) {
+      float x[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) x[i] = p[(z + i) * zs];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v += x[i];
+    }
+    for (; z < g.splits; ++z) v += p[z * zs];
     store_out(g, b, row, col, v);
   }
 }
@@ -86,6 +98,73 @@ void launch_splitk_reduce(const GemmArgs& g, int batch, hipStream_t stream) {
     splitk_reduce_kernel<<<(unsigned)std::min<int64_t>(ceil_div(total, 256), 8192), 256, 0,
                            stream>>>(g, batch);
   }
+}
+
+// Skinny weight gradients: C = A^T B with both operands row-contiguous (A(m, k) = A[k lda + m],
+// B(k, n) = B[k ldb + n]), at most 8 output rows and a long K (PPI's first-layer score gradient
+// G_s^T x: 8 x 50 over 44,900 nodes, which the 128 x 128 x3 tiles ran in 60 us for 11 MB of
+// operands). Plain fp32 on the VALU: lane = output column (256-B row segments per wave), the 16
+// waves of a block interleave this split's K range, four rows in flight each, A's <= 8 values
+// per row wave-uniform; waves summed in fixed order through LDS into the split's slab.
+constexpr int kSkinnyRows = 8;
+__global__ void __launch_bounds__(1024) gemm_skinny_rc_kernel(GemmArgs g) {
+  constexpr int T = kSkinnyRows, NW = 16, U = 4;
+  __shared__ float red[NW][T][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t n = blockIdx.x * 64ll + lane;
+  const int z = blockIdx.y;
+  const int64_t kb = (int64_t)z * g.k_per_split, ke = min(g.K, kb + g.k_per_split);
+  const bool nv = n < g.N;
+  const int M = (int)g.M;
+  float acc[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t) acc[t] = 0.f;
+  for (int64_t k0 = kb + wave; k0 < ke; k0 += (int64_t)NW * U) {
+    float b[U], a[U][T];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t k = k0 + (int64_t)u * NW;
+      const bool ok = k < ke;
+      const int64_t kk = ok ? k : kb;
+      b[u] = g.B[kk * g.ldb + (nv ? n : 0)];
+      if (!ok || !nv) b[u] = 0.f;
+#pragma unroll
+      for (int t = 0; t < T; ++t) a[u][t] = (t < M && ok) ? g.A[kk * g.lda + t] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int t = 0; t < T; ++t) acc[t] = fmaf(a[u][t], b[u], acc[t]);
+  }
+#pragma unroll
+  for (int t = 0; t < T; ++t) red[wave][t][lane] = acc[t];
+  __syncthreads();
+  if (threadIdx.x < T * 64) {
+    const int t = threadIdx.x / 64, c = threadIdx.x % 64;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) v += red[w][t][c];
+    const int64_t col = blockIdx.x * 64ll + c;
+    if (t < M && col < g.N) {
+      if (g.splits > 1) g.partial[(int64_t)z * g.M * g.N + t * g.N + col] = v;
+      else store_out(g, 0, t, col, v);
+    }
+  }
+}
+
+// Split-K reduction with one wave per output element: lane l sums slabs l, l + 64, ... in order,
+// then a fixed butterfly over the lanes (deterministic; for small outputs over many slabs, where
+// a thread per element waited one load latency per slab).
+__global__ void __launch_bounds__(256) splitk_reduce_lanes_kernel(GemmArgs g) {
+  const int lane = threadIdx.x & 63;
+  const int64_t MN = g.M * g.N;
+  const int64_t t = blockIdx.x * 4ll + (threadIdx.x >> 6);
+  if (t >= MN) return;   // (whole waves: t is wave-uniform)
+  float v = 0.f;
+  for (int z = lane; z < g.splits; z += 64) v += g.partial[(int64_t)z * MN + t];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if (lane == 0) store_out(g, 0, t / g.N, t % g.N, v);
 }
 
 // Tiny products (K <= 64, M N K <= 2^25 multiply-adds: PATTERN's projections) on the VALU in
@@ -662,6 +741,24 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
       s_part = (float*)((char*)workspace + off);
       workspace_bytes = off;
     }
+  }
+  // skinny weight gradient (<= 8 output rows, row-contiguous operands, long K): the VALU kernel
+  if (tag == 2 && batch == 1 && !a_kc && !b_kc && M <= kSkinnyRows && K >= 4096 && N <= 4096) {
+    const int64_t chunks = ceil_div(N, (int64_t)64);
+    int sp = (int)std::min<int64_t>(std::max<int64_t>(1, 256 / chunks), K / 256);
+    while (sp > 1 && (!workspace || (size_t)sp * M * N * sizeof(float) > workspace_bytes)) --sp;
+    g.splits = sp < 1 ? 1 : sp;
+    g.k_per_split = ceil_div(K, (int64_t)g.splits);
+    g.splits = (int)ceil_div(K, g.k_per_split);
+    g.partial = g.splits > 1 ? (float*)workspace : nullptr;
+    g.tiles_m = g.tiles_n = 1;
+    gemm_skinny_rc_kernel<<<dim3((unsigned)chunks, (unsigned)g.splits), 1024, 0, stream>>>(g);
+    GATX_LAUNCH_CHECK("gemm_skinny_rc");
+    if (g.splits > 1) {
+      splitk_reduce_lanes_kernel<<<(unsigned)ceil_div(M * N, (int64_t)4), 256, 0, stream>>>(g);
+      GATX_LAUNCH_CHECK("splitk_reduce_lanes");
+    }
+    return 0;
   }
   if (workspace && tag == 2) {   // explicit split-K into [M][N] slabs
     int sp = choose_splits(tiles, K, slots);

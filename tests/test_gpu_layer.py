@@ -933,3 +933,33 @@ def test_gemm_wgrad_accuracy(device):
                 assert (int(fb.item()) > 0) == (case == "dead_feature"), (case, int(fb.item()))
         lib.gatx_set_gemm_mode(2)
         assert rel[2] <= max(1.25 * rel[0], 2e-7) and rel[2] < 1e-6, (case, rel)
+
+
+@pytest.mark.gpu
+def test_gemm_skinny_weight_gradient(device):
+    """Weight gradients with at most 8 output rows over a long K (the first layer's score
+    gradient G_s^T x) take the VALU skinny kernel + a lane-parallel split-K reduction: fp32
+    products, within fp32 summation error of float64, ragged N and unaligned strides, accumulate,
+    and bitwise repeatable."""
+    from gatx._lib import call, lib, ptr, stream
+    torch.manual_seed(15)
+    for (M, N, K, lda, ldb, acc) in ((8, 50, 44900, 8, 50, 0), (3, 130, 5000, 7, 131, 0),
+                                     (1, 64, 9001, 1, 64, 1), (8, 1000, 20000, 8, 1000, 0)):
+        A = torch.randn(K, lda, device=device)       # A(m, k) = A[k][m]: G_s rows
+        B = torch.randn(K, ldb, device=device)       # B(k, n) = B[k][n]: x rows
+        ref = A[:, :M].double().t() @ B[:, :N].double()
+        S = A[:, :M].double().abs().t() @ B[:, :N].double().abs()
+        wsb = lib.gatx_gemm_splitk_workspace_bytes(M, N, K)
+        ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=device)
+        outs = []
+        for _ in range(2):
+            C0 = torch.randn(M, N, device=device) if acc else torch.full((M, N), float("nan"),
+                                                                          device=device)
+            C = C0.clone()
+            call("gatx_gemm_f32_splitk", M, N, K, ptr(A), 1, lda, ptr(B), ldb, 1, ptr(C), N, acc,
+                 ptr(ws), wsb, stream())
+            torch.cuda.synchronize()
+            got = C.double() - (C0.double() if acc else 0)
+            assert ((got - ref).abs() / S.clamp_min(1e-30)).max().item() < 1e-5, (M, N, K)
+            outs.append(C)
+        assert torch.equal(outs[0], outs[1])
