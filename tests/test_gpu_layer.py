@@ -952,9 +952,9 @@ def test_gemm_skinny_weight_gradient(device):
         wsb = lib.gatx_gemm_splitk_workspace_bytes(M, N, K)
         ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=device)
         outs = []
+        C0 = torch.randn(M, N, device=device) if acc else torch.full((M, N), float("nan"),
+                                                                      device=device)
         for _ in range(2):
-            C0 = torch.randn(M, N, device=device) if acc else torch.full((M, N), float("nan"),
-                                                                          device=device)
             C = C0.clone()
             call("gatx_gemm_f32_splitk", M, N, K, ptr(A), 1, lda, ptr(B), ldb, 1, ptr(C), N, acc,
                  ptr(ws), wsb, stream())
