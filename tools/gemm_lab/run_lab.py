@@ -19,6 +19,7 @@ lab = ctypes.CDLL(os.path.join(HERE, "libf16lab.so"))
 P, I64, I, F = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_float
 lab.lab_split_b.argtypes = [P, I64, I64, I64, F, P, P]
 lab.lab_gemm.argtypes = [I, I, P, I64, P, I64, I64, I64, F, P, I64, P, P]
+lab.lab_gemm_pp.argtypes = [I, P, P, P, I64, I64, I64, F, P, I64, P]
 dev = torch.device("cuda:0")
 
 
@@ -58,7 +59,13 @@ def main():
             call("gatx_gemm_f32", M, N, K, ptr(A), K, 1, ptr(B), 1, K, ptr(C), N, N, None, 0, 0,
                  ptr(ws) if wsb else None, wsb, stream())
 
+        Ap = torch.empty(M * K * 2, dtype=torch.uint16, device=dev)
+        lab.lab_split_b(ptr(A), M, K, K, 64.0, ptr(Ap), stream())   # A planes, Ah = fp16(64 a)
         variants = {"lib f16x3": lib_run}
+        for bk in (16, 32):
+            variants[f"v4 A+B planes bk{bk}"] = (
+                lambda bk=bk: lab.lab_gemm_pp(bk, None, ptr(Ap), ptr(Bp), M, N, K, 2.0 ** -11 / sB,
+                                              ptr(C), N, stream()))
         for bk in (16, 32, 33):
             for sc in (0,):
                 name_ = f"v2 bk{bk} scale{sc}" if bk != 33 else f"v3 16x16x32 scale{sc}"
