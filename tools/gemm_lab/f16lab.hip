@@ -492,6 +492,110 @@ __global__ void __launch_bounds__(NT, 1) f16v4_kernel(LabArgs g, const uint16_t*
   }
 }
 
+// v5: both operands as planes (v4), staged by LDS-DMA (global_load_lds_dwordx4, no VGPR round
+// trip) into a ring of 4 K-tile buffers (3 tiles in flight), one raw barrier per K-tile behind a
+// counted vmcnt (never 0 in the steady state): the guide's "3-buf span" structure.
+// LDS image per buffer: [A | B][plane][slot of 8 k][256 rows][16 B] (rows contiguous: the 32x32x16
+// fragment reads are conflict-free without a swizzle).
+constexpr int V5_BUF = 2 * 2 * 2 * 256 * 16;   // 32 KB: 2 operands x 2 planes x 2 slots
+__device__ inline void v5_issue(const char* __restrict__ Ap, const char* __restrict__ Bp, int64_t brow,
+                                int64_t m0, int64_t n0, int64_t M, int64_t N, int kt, char* buf,
+                                int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int gi = wave * 4 + i;          // 32 wave-instructions per buffer
+    const int op = gi >> 4;               // 0 = A, 1 = B
+    const int c0 = (gi & 15) * 64;        // first chunk of this instruction
+    const int row = (c0 & 255) + lane, slot = (c0 >> 8) & 1, plane = c0 >> 9;
+    const int64_t r0 = op ? n0 : m0, rmax = op ? N : M;
+    int64_t gr = r0 + row;
+    gr = gr < rmax ? gr : rmax - 1;       // rows past the matrix: a valid row, never stored
+    const char* src = (op ? Bp : Ap) + gr * brow + ((int64_t)kt * 2 + slot) * 32 + plane * 16;
+    char* dst = buf + op * (V5_BUF / 2) + plane * (2 * 256 * 16) + slot * (256 * 16) + (c0 & 255) * 16;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+  }
+}
+
+__global__ void __launch_bounds__(NT, 1) f16v5_kernel(LabArgs g, const uint16_t* Ap) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * V5_BUF];
+  const int64_t T = ((g.M + TBM - 1) / TBM) * ((g.N + TBN - 1) / TBN);
+  int64_t tm, tn;
+  tile_of(blockIdx.x, T, (g.N + TBN - 1) / TBN, tm, tn);
+  const int64_t m0 = tm * TBM, n0 = tn * TBN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+  const char* A = (const char*)Ap;
+  const char* B = (const char*)g.Bp;
+  floatx16 acc[MB][NB];
+#pragma unroll
+  for (int i = 0; i < MB; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int nk = (int)(g.K / 16);
+  for (int t = 0; t < 3 && t < nk; ++t)
+    v5_issue(A, B, g.brow, m0, n0, g.M, g.N, t, smem + t * V5_BUF, wave, lane);
+  const int fr = lane & 31, fs = lane >> 5;
+  for (int kt = 0; kt < nk; ++kt) {
+    // tile kt landed (this wave's DMAs: the later tiles' 4 each may stay in flight), then every
+    // wave's (the barrier); the barrier also retires every read of tile kt - 1's buffer
+    if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + 3 < nk)
+      v5_issue(A, B, g.brow, m0, n0, g.M, g.N, kt + 3, smem + ((kt + 3) & 3) * V5_BUF, wave, lane);
+    const char* cur = smem + (kt & 3) * V5_BUF;
+    f16x8 fa[MB][2], fb[NB][2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+#pragma unroll
+      for (int x = 0; x < MB; ++x)
+        fa[x][p] = *(const f16x8*)(cur + p * (2 * 256 * 16) + fs * (256 * 16) +
+                                   (wm * (MB * 32) + x * 32 + fr) * 16);
+#pragma unroll
+      for (int x = 0; x < NB; ++x)
+        fb[x][p] = *(const f16x8*)(cur + V5_BUF / 2 + p * (2 * 256 * 16) + fs * (256 * 16) +
+                                   (wn * (NB * 32) + x * 32 + fr) * 16);
+    }
+#pragma unroll
+    for (int mi = 0; mi < MB; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NB; ++ni)
+        acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][1], fa[mi][0], acc[mi][ni], 0, 0, 0);
+#pragma unroll
+    for (int mi = 0; mi < MB; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NB; ++ni)
+        acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][0], fa[mi][1], acc[mi][ni], 0, 0, 0);
+#pragma unroll
+    for (int mi = 0; mi < MB; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NB; ++ni)
+        acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][0], fa[mi][0], acc[mi][ni], 0, 0, 0);
+  }
+  const int lr = lane & 31, lc = 4 * (lane >> 5);
+#pragma unroll
+  for (int mi = 0; mi < MB; ++mi) {
+    const int64_t row = m0 + wm * (MB * 32) + mi * 32 + lr;
+    if (row >= g.M) continue;
+#pragma unroll
+    for (int ni = 0; ni < NB; ++ni) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t col = n0 + wn * (NB * 32) + ni * 32 + 8 * j + lc;
+        if (col + 3 < g.N)
+          *(float4*)(g.C + row * g.ldc + col) =
+              make_float4(acc[mi][ni][4 * j] * g.binv, acc[mi][ni][4 * j + 1] * g.binv,
+                          acc[mi][ni][4 * j + 2] * g.binv, acc[mi][ni][4 * j + 3] * g.binv);
+      }
+    }
+  }
+}
+
 // B planes: row n, slot s (8 k): fp16 h[8] = fp16(32 sB b), then l[8] = fp16(32 sB b - h).
 __global__ void split_b_kernel(const float* B, int64_t N, int64_t K, int64_t ldb, float c,
                                uint16_t* Bp, int64_t brow) {
@@ -523,7 +627,8 @@ extern "C" int lab_gemm_pp(int bk, const float* A_unused, const uint16_t* Ap, co
   (void)A_unused;
   LabArgs g{nullptr, K, Bp, K * 4, M, N, K, C, ldc, binv, nullptr};
   const unsigned grid = (unsigned)(((M + 255) / 256) * ((N + 255) / 256));
-  if (bk == 32) f16v4_kernel<32><<<grid, NT, 0, s>>>(g, Ap);
+  if (bk == 5) f16v5_kernel<<<grid, NT, 0, s>>>(g, Ap);
+  else if (bk == 32) f16v4_kernel<32><<<grid, NT, 0, s>>>(g, Ap);
   else f16v4_kernel<16><<<grid, NT, 0, s>>>(g, Ap);
   return (int)hipGetLastError();
 }

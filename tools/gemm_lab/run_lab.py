@@ -62,8 +62,8 @@ def main():
         Ap = torch.empty(M * K * 2, dtype=torch.uint16, device=dev)
         lab.lab_split_b(ptr(A), M, K, K, 64.0, ptr(Ap), stream())   # A planes, Ah = fp16(64 a)
         variants = {"lib f16x3": lib_run}
-        for bk in (16, 32):
-            variants[f"v4 A+B planes bk{bk}"] = (
+        for bk in (16, 32, 5):
+            variants[f"v4 A+B planes bk{bk}" if bk != 5 else "v5 glds ring4 bk16"] = (
                 lambda bk=bk: lab.lab_gemm_pp(bk, None, ptr(Ap), ptr(Bp), M, N, K, 2.0 ** -11 / sB,
                                               ptr(C), N, stream()))
         for bk in (16, 32, 33):
