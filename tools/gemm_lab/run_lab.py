@@ -66,9 +66,9 @@ def main():
             variants[f"v4 A+B planes bk{bk}" if bk != 5 else "v5 glds ring4 bk16"] = (
                 lambda bk=bk: lab.lab_gemm_pp(bk, None, ptr(Ap), ptr(Bp), M, N, K, 2.0 ** -11 / sB,
                                               ptr(C), N, stream()))
-        for bk in (16, 32, 33):
+        for bk in (16, 32, 33, 6):
             for sc in (0,):
-                name_ = f"v2 bk{bk} scale{sc}" if bk != 33 else f"v3 16x16x32 scale{sc}"
+                name_ = {33: f"v3 16x16x32 scale{sc}", 6: "v6 ping-pong bk16"}.get(bk, f"v2 bk{bk} scale{sc}")
                 variants[name_] = (
                     lambda bk=bk, sc=sc: lab.lab_gemm(bk, sc, ptr(A), K, ptr(Bp), M, N, K,
                                                       2.0 ** -11 / sB, ptr(C), N, ptr(bad),
