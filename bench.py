@@ -76,7 +76,7 @@ def gemm_roof():
     if mode == 2:
         f16p = os.environ.get("GATX_F16P", "1") != "0"
         return dict(mode="f16x3", peak=BF16_MFMA_PEAK_TFS / F16X3_PRODUCTS,
-                    prefix=("gemm_f16p_kernel<16, 0>", "gemm_f16p_kernel<32, 0>",
+                    prefix=("gemm_f16p_kernel<16, 0", "gemm_f16p_kernel<32, 0",
                             "gemm_x3_kernel<true, true, true, 0,"),
                     kernel=("gemm_f16p_kernel (weight as pre-split fp16 planes)" if f16p
                             else "gemm_x3_kernel") +
@@ -559,7 +559,7 @@ def roofline_objects(summ, edge_bytes, pm, n_instr, pm_path="", gather_E2=None):
 TRAIN_PHASES = {
     "gemm": ("mfma", None),
     # (pre-split f16x3 g_x / the in-loop kernel; the f16x3 weight gradient / its x3 form)
-    "bwd_gemm_gx": ("mfma", ("gemm_f16p_kernel<16, 1>", "gemm_f16p_kernel<32, 1>",
+    "bwd_gemm_gx": ("mfma", ("gemm_f16p_kernel<16, 1", "gemm_f16p_kernel<32, 1",
                              "gemm_x3_kernel<true, true, true, 1,")),
     "bwd_gemm_gw": ("mfma", ("gemm_f16rc_kernel<", "gemm_x3_kernel<false, false, true, 2, 1,")),
     "edge_forward": ("hbm", "edge_forward_kernel"),

@@ -18,6 +18,10 @@ if [ "${BK32:-0}" = 1 ]; then
   step bench_bk32 env GATX_F16P_BK=32 timeout -k 10 300 python bench.py --no-cpu-baseline > "$OUT/bench_bk32.json" 2> "$OUT/bench_bk32.err"
   step bench_train_bk32 env GATX_F16P_BK=32 timeout -k 10 300 python bench.py --mode train --no-cpu-baseline > "$OUT/bench_train_bk32.json" 2> "$OUT/bench_train_bk32.err"
 fi
+if [ "${PPAB:-0}" = 1 ]; then
+  step bench_nopp env GATX_F16P_PP=0 timeout -k 10 300 python bench.py --no-cpu-baseline > "$OUT/bench_nopp.json" 2> "$OUT/bench_nopp.err"
+  step bench_train_nopp env GATX_F16P_PP=0 timeout -k 10 300 python bench.py --mode train --no-cpu-baseline > "$OUT/bench_train_nopp.json" 2> "$OUT/bench_train_nopp.err"
+fi
 step bench_pattern timeout -k 10 300 python bench.py --workload pattern --graphs 8 --mode train --no-cpu-baseline > "$OUT/bench_pattern_train.json" 2> "$OUT/bench_pattern_train.err"
 cd /tmp && export TMPDIR=/tmp
 step prof_train timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_train" -o run --output-format csv -- python3 "$R/bench.py" --mode train --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/prof_train.log" 2>&1
@@ -32,7 +36,7 @@ import json, sys
 o = sys.argv[1]
 import os
 for f in ("bench", "bench_train", "bench_train_nof16p", "bench_bk32", "bench_train_bk32",
-          "bench_pattern_train"):
+          "bench_nopp", "bench_train_nopp", "bench_pattern_train"):
     if not os.path.exists(f"{o}/{f}.json"):
         continue
     d = json.load(open(f"{o}/{f}.json"))
