@@ -408,8 +408,7 @@ __device__ inline uint32_t mix_resid(float x, float y, float cx, float cy, uint3
   return l;
 }
 
-// PP: the ping-pong form of the loop (see f16p_mainloop).
-template <bool MASK, bool PP = false>
+template <bool MASK>
 __device__ inline bool f16rc_mainloop(const GemmArgs& g, const float* __restrict__ A,
                                       const float* __restrict__ B, int64_t m0, int64_t n0,
                                       int64_t kb, int64_t K, int64_t nk, char* smem, int wm,
@@ -504,53 +503,6 @@ __device__ inline bool f16rc_mainloop(const GemmArgs& g, const float* __restrict
   };
   load(kb);
   store(smem, kb);
-  if constexpr (PP) {
-    auto barrier = [] {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    };
-    if (nk > 1) load(kb + BK);
-    barrier();               // tile 0 staged by every wave
-    if (wm == 1) barrier();  // group 1 one barrier behind
-    for (int64_t kt = 0; kt < nk; ++kt) {
-      const char* cur = smem + (kt & 1) * STAGE;
-      char* nxt = smem + ((kt & 1) ^ 1) * STAGE;
-      // (the next tile's split and stores first: the five-plane split needs registers the
-      // fragments would hold)
-      if (kt + 1 < nk) store(nxt, kb + (kt + 1) * BK);
-      if (kt + 2 < nk) load(kb + (kt + 2) * BK);
-      f16x8 fa[MB][3], fb[NB][2];
-#pragma unroll
-      for (int p = 0; p < 3; ++p)
-#pragma unroll
-        for (int x = 0; x < MB; ++x)
-          fa[x][p] = __builtin_bit_cast(f16x8, TA::frag(cur + p * PL, wm * (MB * 32) + x * 32, 0, lane));
-#pragma unroll
-      for (int p = 0; p < 2; ++p)
-#pragma unroll
-        for (int x = 0; x < NB; ++x)
-          fb[x][p] = __builtin_bit_cast(f16x8, TB::frag(cur + (3 + p) * PL, wn * (NB * 32) + x * 32, 0, lane));
-      barrier();
-#pragma unroll
-      for (int mi = 0; mi < MB; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < NB; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][1], fa[mi][0], acc[mi][ni], 0, 0, 0);
-#pragma unroll
-      for (int mi = 0; mi < MB; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < NB; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][0], fa[mi][2], acc[mi][ni], 0, 0, 0);
-#pragma unroll
-      for (int mi = 0; mi < MB; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < NB; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][0], fa[mi][1], acc[mi][ni], 0, 0, 0);
-      barrier();
-    }
-    if (wm == 0) barrier();  // balances group 1's extra barrier
-  } else {
   __syncthreads();
   for (int64_t kt = 0; kt < nk; ++kt) {
     const char* cur = smem + (kt & 1) * STAGE;
@@ -587,7 +539,6 @@ __device__ inline bool f16rc_mainloop(const GemmArgs& g, const float* __restrict
     if (more) store(nxt, kb + (kt + 1) * BK);
     __syncthreads();
   }
-  }
   // per-row range over this K-slice: a thread holds 4 rows at its k's; the 8 waves' lanes with the
   // same lane index share rows -> LDS reduction
   float* red = (float*)smem;   // [2][8][256]
@@ -615,7 +566,7 @@ __device__ inline bool f16rc_mainloop(const GemmArgs& g, const float* __restrict
   return bad;
 }
 
-template <bool VEC, bool PP = false>
+template <bool VEC>
 __global__ void __launch_bounds__(512, 1) gemm_f16rc_kernel(GemmArgs g) {
   using C = X3Cfg<1>;
   constexpr int SMEM = 2 * 5 * (256 * 16 * 2) > 2 * 3 * 2 * (256 + 256) * 16
@@ -643,7 +594,7 @@ __global__ void __launch_bounds__(512, 1) gemm_f16rc_kernel(GemmArgs g) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
   const int64_t nk = K > kb ? ceil_div(K - kb, C::BK) : 0;
   if (nk > 0) {
-    const bool x3 = f16rc_mainloop<!VEC, PP>(g, g.A, g.B, m0, n0, kb, K, nk, smem, wm, wn, lane, acc);
+    const bool x3 = f16rc_mainloop<!VEC>(g, g.A, g.B, m0, n0, kb, K, nk, smem, wm, wn, lane, acc);
     // undo 2^11 and the A rows' scales (lane -> output row = A row, write_tile_t's layout)
     const int lr = lane & 31;
 #pragma unroll
@@ -973,16 +924,8 @@ int wgrad_thin_rows(int64_t M) {
 // see wgrad_thin_rows) by wgrad_thin_kernel.
 int launch_gemm_f16rc(const gk::GemmArgs& g, hipStream_t stream) {
   dim3 grid((unsigned)(g.tiles_m * g.tiles_n * g.splits), 1u, 1u);
-  static const bool pp = [] {   // A/B: GATX_F16P_PP=0 keeps the single-phase loop
-    const char* e = getenv("GATX_F16P_PP");
-    return !(e && strcmp(e, "0") == 0);
-  }();
-  if (g.a_vec && g.b_vec) {
-    if (pp) gemm_f16rc_kernel<true, true><<<grid, 512, 0, stream>>>(g);
-    else gemm_f16rc_kernel<true><<<grid, 512, 0, stream>>>(g);
-  } else {
-    gemm_f16rc_kernel<false><<<grid, 512, 0, stream>>>(g);
-  }
+  if (g.a_vec && g.b_vec) gemm_f16rc_kernel<true><<<grid, 512, 0, stream>>>(g);
+  else gemm_f16rc_kernel<false><<<grid, 512, 0, stream>>>(g);
   GATX_LAUNCH_CHECK("gemm_f16rc");
   if (g.tiles_m * 256 < g.M) {
     GATX_REQUIRE(g.M - g.tiles_m * 256 <= kThinRows && g.a_vec && g.b_vec && g.N % 4 == 0,
