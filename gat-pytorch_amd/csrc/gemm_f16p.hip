@@ -943,25 +943,18 @@ int launch_gemm_f16p(const gk::GemmArgs& g, int tag, hipStream_t stream) {
   const int64_t tiles = g.tiles_m * g.tiles_n;
   const int64_t gx = g.tail_s > 1 ? g.dp_blocks + g.tail_rem * g.tail_s : tiles;
   dim3 grid((unsigned)gx, 1u, (unsigned)g.splits);
-  static const int bk = [] {   // tuning only: GATX_F16P_BK=32
-    const char* e = getenv("GATX_F16P_BK");
-    return e && atoi(e) == 32 ? 32 : 16;
+  // (32-deep K-tiles measured slower in the library: they spill beside the x3 fallback, bench
+  // 1.43 -> 1.61 ms, gpurun_out/r05h; lab numbers in DESIGN.md §8)
+  static const bool pp = [] {   // A/B: GATX_F16P_PP=0 keeps the single-phase loop
+    const char* e = getenv("GATX_F16P_PP");
+    return !(e && strcmp(e, "0") == 0);
   }();
-  if (bk == 32) {
-    if (tag == 0) gemm_f16p_kernel<32, 0><<<grid, 512, 0, stream>>>(g);
-    else gemm_f16p_kernel<32, 1><<<grid, 512, 0, stream>>>(g);
+  if (pp) {
+    if (tag == 0) gemm_f16p_kernel<16, 0, true><<<grid, 512, 0, stream>>>(g);
+    else gemm_f16p_kernel<16, 1, true><<<grid, 512, 0, stream>>>(g);
   } else {
-    static const bool pp = [] {   // A/B: GATX_F16P_PP=0 keeps the single-phase loop
-      const char* e = getenv("GATX_F16P_PP");
-      return !(e && strcmp(e, "0") == 0);
-    }();
-    if (pp) {
-      if (tag == 0) gemm_f16p_kernel<16, 0, true><<<grid, 512, 0, stream>>>(g);
-      else gemm_f16p_kernel<16, 1, true><<<grid, 512, 0, stream>>>(g);
-    } else {
-      if (tag == 0) gemm_f16p_kernel<16, 0><<<grid, 512, 0, stream>>>(g);
-      else gemm_f16p_kernel<16, 1><<<grid, 512, 0, stream>>>(g);
-    }
+    if (tag == 0) gemm_f16p_kernel<16, 0><<<grid, 512, 0, stream>>>(g);
+    else gemm_f16p_kernel<16, 1><<<grid, 512, 0, stream>>>(g);
   }
   GATX_LAUNCH_CHECK("gemm_f16p");
   return 0;

@@ -14,10 +14,6 @@ fi
 step bench timeout -k 10 300 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
 step bench_train timeout -k 10 300 python bench.py --mode train --no-cpu-baseline > "$OUT/bench_train.json" 2> "$OUT/bench_train.err"
 step bench_train_nof16p env GATX_F16P=0 timeout -k 10 300 python bench.py --mode train --no-cpu-baseline > "$OUT/bench_train_nof16p.json" 2> "$OUT/bench_train_nof16p.err"
-if [ "${BK32:-0}" = 1 ]; then
-  step bench_bk32 env GATX_F16P_BK=32 timeout -k 10 300 python bench.py --no-cpu-baseline > "$OUT/bench_bk32.json" 2> "$OUT/bench_bk32.err"
-  step bench_train_bk32 env GATX_F16P_BK=32 timeout -k 10 300 python bench.py --mode train --no-cpu-baseline > "$OUT/bench_train_bk32.json" 2> "$OUT/bench_train_bk32.err"
-fi
 if [ "${PPAB:-0}" = 1 ]; then
   step bench_nopp env GATX_F16P_PP=0 timeout -k 10 300 python bench.py --no-cpu-baseline > "$OUT/bench_nopp.json" 2> "$OUT/bench_nopp.err"
   step bench_train_nopp env GATX_F16P_PP=0 timeout -k 10 300 python bench.py --mode train --no-cpu-baseline > "$OUT/bench_train_nopp.json" 2> "$OUT/bench_train_nopp.err"
