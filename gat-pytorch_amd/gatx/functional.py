@@ -530,11 +530,11 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
             call("gatx_gemm_planes", N, sh.Dp, sh.F_in, ptr(x), sh.F_in, ptr(W_aug), sh.F_in, pp,
                  ptr(Wh), sh.Dp, sh.Dp, None, 0, -1, None, 0, 0, ptr(a), sh.NH, sh.F, ptr(S), 0,
                  None, ptr(ws), nb, s)
-    else:
+    else:   # (GATX_FUSED_SCORES=0: the projection alone, then the score pass over Wh)
         with _span("gemm", (N, sh.Dp, sh.F_in, sh.NH, sh.F)):
-            call("gatx_projection_gemm", N, sh.Dp, sh.F_in, ptr(x), sh.F_in, 1, ptr(W_aug), 1,
-                 sh.F_in, ptr(Wh), sh.Dp, sh.Dp, None, 0, *gemm_workspace(N, sh.Dp, sh.F_in, dev),
-                 s)
+            call("gatx_gemm_planes", N, sh.Dp, sh.F_in, ptr(x), sh.F_in, ptr(W_aug), sh.F_in, pp,
+                 ptr(Wh), sh.Dp, sh.Dp, None, 0, -1, None, 0, 0, None, 0, 0, None, 0, None,
+                 *gemm_workspace(N, sh.Dp, sh.F_in, dev), s)
         with _span("node_scores", (N, sh.NH, sh.F)):
             call("gatx_node_scores", ptr(Wh), N, sh.NH, sh.F, ptr(a), ptr(S), s)
     if not sh.const:
