@@ -606,7 +606,25 @@ def record_pricer(dims, flows, cfg):
     return price
 
 
-def train_roofline_objects(summ, price, pm, n_instr, pm_path=""):
+def train_gathered_row_bytes(phase, E2, info):
+    """Source rows one training edge record gathers through L2, one row per edge and head (None
+    for records not priced this way): the forward as gathered_row_bytes; the backward's
+    destination pass reads Wh[src] per (edge, head) (4 round4(F) B), its source pass go[dst] per
+    edge for every head of a concat layer and once for a head-mean one (go is then shared by the
+    heads). The reassociated first layer's backward is not priced (its rows are x's)."""
+    if phase == "edge_forward":
+        return gathered_row_bytes(E2, info)
+    _, _, _, nh, f, cc = info[:6]
+    if len(info) > 8 and info[8]:
+        return None
+    if phase == "bwd_edge_dst":
+        return 4 * E2 * nh * _r4(f)
+    if phase == "bwd_edge_src":
+        return 4 * E2 * (nh if cc else 1) * _r4(f)
+    return None
+
+
+def train_roofline_objects(summ, price, pm, n_instr, pm_path="", gather_E2=None):
     """Roofline objects of a training step: every TRAIN_PHASES phase with records, priced per
     record (price(phase, i, info)) and timed by its HIP events; the two with the most time per
     step come first. GEMM phases are MFMA-bound (flops / the peak of the arithmetic they run),
@@ -635,6 +653,18 @@ def train_roofline_objects(summ, price, pm, n_instr, pm_path=""):
                  "bytes_per_launch": by / len(recs)}
         o.update({"avg_launch_ms": ms_ / len(recs), "records_per_step": per_step,
                   "ms_per_step": ms_ / n_instr})
+        if gather_E2 and phase in ("edge_forward", "bwd_edge_dst", "bwd_edge_src"):
+            # the bound of these passes in cache-resident batches: the per-edge row gathers from
+            # L2, against the guide's L2-gather rate (records of unpriced layers left out)
+            pr = [(train_gathered_row_bytes(phase, gather_E2, info), t) for info, t in recs]
+            pr = [(b, t) for b, t in pr if b is not None]
+            if pr:
+                g_tbs = sum(b for b, _ in pr) / (sum(t for _, t in pr) * 1e-3) / 1e12
+                o["l2_gather"] = {"achieved": round(g_tbs, 2), "peak": L2_GATHER_TBS,
+                                  "unit": "TB/s", "frac": round(g_tbs / L2_GATHER_TBS, 4),
+                                  "basis": "one gathered row per edge (and head): Wh[src] in the "
+                                           "forward and the destination pass, go[dst] in the "
+                                           "source pass; reassociated first layer excluded"}
         if pm is not None and prefix:
             from pmc_summary import prefix_bytes_per_step
             b = prefix_bytes_per_step(pm, prefix)
@@ -1005,7 +1035,7 @@ def main():
     pm = load_pmc(pmc_path)
     if args.mode == "train" and ds == "PPI":
         ordered = train_roofline_objects(summ, record_pricer(dims, flows, cfg), pm, n_instr,
-                                         pmc_path)
+                                         pmc_path, gather_E2=E2)
     else:
         ordered = roofline_objects(summ, edge_unique, pm, n_instr, pmc_path, gather_E2=E2)
 

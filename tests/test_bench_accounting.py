@@ -235,3 +235,28 @@ def test_train_step_dataflow_covers_the_step():
     # the roofline time of the whole step is ~1.1-1.3 ms at the f16x3 peak (8 TB/s, 833 TF)
     t = sum(max(b / 8e12, f / 833e12) for _, b, f in fl)
     assert 1.0e-3 < t < 1.4e-3, t
+
+
+def test_train_edge_passes_priced_against_the_l2_gather_rate():
+    """The training step's edge passes carry an L2-gather object: Wh[src] rows per (edge, head)
+    in the forward and the destination pass, go[dst] rows in the source pass (per head for a
+    concat layer, once for a head-mean one); the reassociated first layer's backward is left
+    out."""
+    dims, summ = _ppi_train_summ(2)
+    flows = [bench.layer_dataflow(N_PPI, E2_PPI, fin, nh, f, cc, SKIP[i])
+             for i, (fin, nh, f, cc) in enumerate(dims)]
+    price = bench.record_pricer(dims, flows, PPI_CFG)
+    objs = {o["kernel"].split(" ")[0]: o for o in
+            bench.train_roofline_objects(summ, price, None, 2, gather_E2=E2_PPI)}
+    # destination pass: layers 1 (4 x 256) and 2 (6 x 124) priced, layer 0 (reassociated) not;
+    # 0.3 ms per record
+    b = 4 * E2_PPI * (4 * 256 + 6 * 124)
+    g = objs["bwd_edge_dst"]["l2_gather"]
+    assert abs(g["achieved"] - round(b / (2 * 0.3e-3) / 1e12, 2)) < 0.011
+    assert g["peak"] == bench.L2_GATHER_TBS and 0 < g["frac"] < 2
+    # source pass: layer 1 concat (4 heads), layer 2 head mean (one 124-float row per edge)
+    b = 4 * E2_PPI * (4 * 256 + 124)
+    g = objs["bwd_edge_src"]["l2_gather"]
+    assert abs(g["achieved"] - round(b / (2 * 0.3e-3) / 1e12, 2)) < 0.011
+    assert "l2_gather" in objs["edge_forward"]
+    assert "l2_gather" not in objs["bwd_gemm_gw"]
