@@ -688,35 +688,53 @@ template <int MB, int NB, int TBM, int TBN, int WGN>
 __device__ inline void scores_tile(const GemmArgs& g, const floatx16 (&acc)[MB][NB], int64_t m0,
                                    int64_t n0, int64_t tn, int wm, int wn, int lane, char* smem) {
   const int H2 = g.s_h2, lr = lane & 31, lc = 4 * (lane >> 5);
-  float* a2s = (float*)smem;              // [H2][TBN]
-  float* red = a2s + H2 * TBN;            // [WGN][TBM][H2]
-  for (int t = threadIdx.x; t < H2 * TBN; t += 64 * WGN * (TBM / (MB * 32))) {
+  const int H2p = (H2 + 1) & ~1;          // scores in pairs (zero weights past H2)
+  float* a2s = (float*)smem;              // [H2p][TBN]
+  float* red = a2s + H2p * TBN;           // [WGN][TBM][H2]
+  for (int t = threadIdx.x; t < H2p * TBN; t += 64 * WGN * (TBM / (MB * 32))) {
     const int h = t / TBN, c = t - h * TBN;
     const int64_t col = n0 + c;
-    a2s[t] = col < g.N ? score_weight(g.s_a, g.s_nh, g.s_f, g.s_fp, h, col) : 0.f;
+    a2s[t] = (h < H2 && col < g.N) ? score_weight(g.s_a, g.s_nh, g.s_f, g.s_fp, h, col) : 0.f;
   }
   __syncthreads();
-  for (int h = 0; h < H2; ++h) {
-    float t[MB];
+  // two scores per pass over the accumulators (each accumulator read H2p / 2 times, not H2;
+  // four per pass spilled: the compiler hoists every column group's weights)
+#pragma unroll 1
+  for (int h0 = 0; h0 < H2p; h0 += 2) {
+    float t[2][MB];
 #pragma unroll
-    for (int mi = 0; mi < MB; ++mi) t[mi] = 0.f;
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int mi = 0; mi < MB; ++mi) t[q][mi] = 0.f;
 #pragma unroll
     for (int ni = 0; ni < NB; ++ni)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float4 w = *(const float4*)(a2s + h * TBN + wn * (NB * 32) + ni * 32 + 8 * j + lc);
+        const int cl = wn * (NB * 32) + ni * 32 + 8 * j + lc;
+        float4 w[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) w[q] = *(const float4*)(a2s + (h0 + q) * TBN + cl);
 #pragma unroll
         for (int mi = 0; mi < MB; ++mi) {
-          t[mi] = fmaf(acc[mi][ni][4 * j], w.x, t[mi]);
-          t[mi] = fmaf(acc[mi][ni][4 * j + 1], w.y, t[mi]);
-          t[mi] = fmaf(acc[mi][ni][4 * j + 2], w.z, t[mi]);
-          t[mi] = fmaf(acc[mi][ni][4 * j + 3], w.w, t[mi]);
+          const float x0 = acc[mi][ni][4 * j], x1 = acc[mi][ni][4 * j + 1];
+          const float x2 = acc[mi][ni][4 * j + 2], x3 = acc[mi][ni][4 * j + 3];
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            t[q][mi] = fmaf(x0, w[q].x, t[q][mi]);
+            t[q][mi] = fmaf(x1, w[q].y, t[q][mi]);
+            t[q][mi] = fmaf(x2, w[q].z, t[q][mi]);
+            t[q][mi] = fmaf(x3, w[q].w, t[q][mi]);
+          }
         }
       }
 #pragma unroll
-    for (int mi = 0; mi < MB; ++mi) {
-      const float tot = t[mi] + __shfl_xor(t[mi], 32);   // the same sum in both halves
-      if (lane < 32) red[(wn * TBM + wm * (MB * 32) + mi * 32 + lr) * H2 + h] = tot;
+    for (int q = 0; q < 2; ++q) {
+      if (h0 + q >= H2) break;
+#pragma unroll
+      for (int mi = 0; mi < MB; ++mi) {
+        const float tot = t[q][mi] + __shfl_xor(t[q][mi], 32);   // the same sum in both halves
+        if (lane < 32) red[(wn * TBM + wm * (MB * 32) + mi * 32 + lr) * H2 + h0 + q] = tot;
+      }
     }
   }
   __syncthreads();
