@@ -61,7 +61,15 @@ def main():
 
         Ap = torch.empty(M * K * 2, dtype=torch.uint16, device=dev)
         lab.lab_split_b(ptr(A), M, K, K, 64.0, ptr(Ap), stream())   # A planes, Ah = fp16(64 a)
-        variants = {"lib f16x3": lib_run}
+        from gatx.functional import build_weight_planes
+        planes = build_weight_planes(B, N, K, K)
+
+        def lib_planes_run():   # the library's pre-split kernel (ping-pong loop), no scores
+            call("gatx_gemm_planes", M, N, K, ptr(A), K, ptr(B), K, ptr(planes), ptr(C), N, N,
+                 None, 0, -1, None, 0, 0, None, 0, 0, None, 0, None, ptr(ws) if wsb else None,
+                 wsb, stream())
+
+        variants = {"lib f16x3": lib_run, "lib f16p (planes, ping-pong)": lib_planes_run}
         for bk in (16, 32, 5):
             variants[f"v4 A+B planes bk{bk}" if bk != 5 else "v5 glds ring4 bk16"] = (
                 lambda bk=bk: lab.lab_gemm_pp(bk, None, ptr(Ap), ptr(Bp), M, N, K, 2.0 ** -11 / sB,
