@@ -120,9 +120,18 @@ __device__ inline bool f16p_mainloop(const GemmArgs& g, const float* __restrict_
     for (int c = 0; c < NV; ++c)
       vb[c] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rb, vob[c], so, 0));
   };
-  float cs[NV], amax[NV];
+  // range check on the hi plane itself: max |Ah| per thread as packed fp16 bit patterns (|.| by
+  // clearing the sign bits; non-negative fp16 order as unsigned integers), one AND and one
+  // v_pk_max_u16 per element pair instead of four abs / max on the fp32 values
+  float cs[NV];
+  uint32_t hmax[NV];
 #pragma unroll
-  for (int c = 0; c < NV; ++c) { cs[c] = 64.f; amax[c] = 0.f; }
+  for (int c = 0; c < NV; ++c) { cs[c] = 64.f; hmax[c] = 0u; }
+  auto pk_max_u16 = [](uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_pk_max_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+  };
   // the last K-tile may run past K: A's k >= K would read the next row (B's planes are zero
   // there, but an inf / nan in A would still poison the sums) -> zeroed
   auto mask_tail = [&](int64_t kt) {
@@ -141,10 +150,10 @@ __device__ inline bool f16p_mainloop(const GemmArgs& g, const float* __restrict_
 #pragma unroll
     for (int c = 0; c < NV; ++c) {
       const float4 v = va[c];
-      amax[c] = fmaxf(amax[c], fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
       uint32_t h0, l0, h1, l1;
       split_mix(v.x, v.y, cs[c], h0, l0);
       split_mix(v.z, v.w, cs[c], h1, l1);
+      hmax[c] = pk_max_u16(hmax[c], pk_max_u16(h0 & 0x7fff7fffu, h1 & 0x7fff7fffu));
       *(uint2*)(st + oa[c]) = make_uint2(h0, h1);
       *(uint2*)(st + PB + oa[c]) = make_uint2(l0, l1);
     }
@@ -281,14 +290,17 @@ __device__ inline bool f16p_mainloop(const GemmArgs& g, const float* __restrict_
     __syncthreads();
   }
   }
+  // a row is out of range when its largest |Ah| = |fp16(64 s a)| is inf / nan (64 s |a| past the
+  // fp16 range: |s a| > 1023) or, unless the row is zero, below 2^-3 (s |a| < 2^-9: the residual
+  // plane would go subnormal)
   bool bad = false;
 #pragma unroll
   for (int c = 0; c < NV; ++c) {
-    float m = amax[c];
+    uint32_t m = hmax[c];
 #pragma unroll
-    for (int o = 1; o < TPR; o <<= 1) m = fmaxf(m, __shfl_xor(m, o));
-    const float s = cs[c] * (1.f / 64.f);
-    bad |= !(m * s <= 1023.f) || (m > 0.f && m * s < 0x1p-9f);
+    for (int o = 1; o < TPR; o <<= 1) m = pk_max_u16(m, (uint32_t)__shfl_xor((int)m, o));
+    const uint32_t mh = (m & 0xffffu) > (m >> 16) ? (m & 0xffffu) : (m >> 16);
+    bad |= mh >= 0x7c00u || (mh > 0u && mh < 0x3000u);
   }
   return bad;
 }
