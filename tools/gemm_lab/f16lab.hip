@@ -731,6 +731,127 @@ __global__ void __launch_bounds__(NT, 1) f16v6_kernel(LabArgs g) {
   }
 }
 
+// v7: v6 with the activations pre-split too (A planes copied like B's; tuning only).
+__global__ void __launch_bounds__(NT, 1) f16v7_kernel(LabArgs g, const uint16_t* Ap) {
+  constexpr int BK = 16;
+  using I = Img<BK>;
+  constexpr int PB = I::BYTES;
+  constexpr int STAGE = 4 * PB;
+  constexpr int NVA = BK / 8, NVB = BK / 8, TPR = BK / 4;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  const int64_t T = ((g.M + TBM - 1) / TBM) * ((g.N + TBN - 1) / TBN);
+  int64_t tm, tn;
+  tile_of(blockIdx.x, T, (g.N + TBN - 1) / TBN, tm, tn);
+  const int64_t m0 = tm * TBM, n0 = tn * TBN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int64_t arows = g.M - m0 < TBM ? g.M - m0 : TBM;
+  const int64_t brows = g.N - n0 < TBN ? g.N - n0 : TBN;
+  const auto ra = rsrc((const char*)Ap + m0 * g.brow, arows * g.brow);
+  const auto rb = rsrc((const char*)g.Bp + n0 * g.brow, brows * g.brow);
+  int voa[NVA], vob[NVB], oa[NVA], ob[NVB];
+#pragma unroll
+  for (int c = 0; c < NVA; ++c) {
+    const int idx = tid + NT * c;
+    const int r = idx / TPR, j = idx % TPR;
+    voa[c] = r * (int)g.brow + (j >> 1) * 32 + (j & 1) * 16;
+    oa[c] = (j & 1) * PB + I::off(r, 8 * (j >> 1));
+    vob[c] = voa[c];
+    ob[c] = (2 + (j & 1)) * PB + I::off(r, 8 * (j >> 1));
+  }
+  uint4 va[NVA];
+  uint4 vb[NVB];
+  auto load = [&](int kt) {
+#pragma unroll
+    for (int c = 0; c < NVA; ++c)
+      va[c] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ra, voa[c], kt * BK * 4, 0));
+#pragma unroll
+    for (int c = 0; c < NVB; ++c)
+      vb[c] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rb, vob[c], kt * BK * 4, 0));
+  };
+  auto store = [&](char* st) {
+#pragma unroll
+    for (int c = 0; c < NVA; ++c) *(uint4*)(st + oa[c]) = va[c];
+#pragma unroll
+    for (int c = 0; c < NVB; ++c) *(uint4*)(st + ob[c]) = vb[c];
+  };
+  auto barrier = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  floatx16 acc[MB][NB];
+#pragma unroll
+  for (int i = 0; i < MB; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int nk = (int)(g.K / BK);
+  load(0);
+  store(smem);
+  if (nk > 1) load(1);
+  barrier();                 // tile 0 staged by everyone
+  if (wm == 1) barrier();    // group 1 runs one barrier behind
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* cur = smem + (kt & 1) * STAGE;
+    char* nxt = smem + ((kt & 1) ^ 1) * STAGE;
+    // MEM: this tile's fragments, the next tile's stores, the loads of the one after
+    f16x8 fa[MB][2], fb[NB][2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+#pragma unroll
+      for (int x = 0; x < MB; ++x)
+        fa[x][p] = *(const f16x8*)(cur + p * PB +
+                                   I::off(wm * (MB * 32) + x * 32 + (lane & 31), 8 * (lane >> 5)));
+#pragma unroll
+      for (int x = 0; x < NB; ++x)
+        fb[x][p] = *(const f16x8*)(cur + (2 + p) * PB +
+                                   I::off(wn * (NB * 32) + x * 32 + (lane & 31), 8 * (lane >> 5)));
+    }
+    if (kt + 1 < nk) store(nxt);
+    if (kt + 2 < nk) load(kt + 2);
+    barrier();
+    // MATH
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int mi = 0; mi < MB; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NB; ++ni)
+        acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][1], fa[mi][0], acc[mi][ni], 0, 0, 0);
+#pragma unroll
+    for (int mi = 0; mi < MB; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NB; ++ni)
+        acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][0], fa[mi][1], acc[mi][ni], 0, 0, 0);
+#pragma unroll
+    for (int mi = 0; mi < MB; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NB; ++ni)
+        acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][0], fa[mi][0], acc[mi][ni], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    barrier();
+  }
+  if (wm == 0) barrier();    // balance group 1's extra barrier
+  const int lr = lane & 31, lc = 4 * (lane >> 5);
+#pragma unroll
+  for (int mi = 0; mi < MB; ++mi) {
+    const int64_t row = m0 + wm * (MB * 32) + mi * 32 + lr;
+    if (row >= g.M) continue;
+#pragma unroll
+    for (int ni = 0; ni < NB; ++ni) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t col = n0 + wn * (NB * 32) + ni * 32 + 8 * j + lc;
+        if (col + 3 < g.N)
+          *(float4*)(g.C + row * g.ldc + col) =
+              make_float4(acc[mi][ni][4 * j] * g.binv, acc[mi][ni][4 * j + 1] * g.binv,
+                          acc[mi][ni][4 * j + 2] * g.binv, acc[mi][ni][4 * j + 3] * g.binv);
+      }
+    }
+  }
+}
+
 // B planes: row n, slot s (8 k): fp16 h[8] = fp16(32 sB b), then l[8] = fp16(32 sB b - h).
 __global__ void split_b_kernel(const float* B, int64_t N, int64_t K, int64_t ldb, float c,
                                uint16_t* Bp, int64_t brow) {
@@ -763,6 +884,7 @@ extern "C" int lab_gemm_pp(int bk, const float* A_unused, const uint16_t* Ap, co
   LabArgs g{nullptr, K, Bp, K * 4, M, N, K, C, ldc, binv, nullptr};
   const unsigned grid = (unsigned)(((M + 255) / 256) * ((N + 255) / 256));
   if (bk == 5) f16v5_kernel<<<grid, NT, 0, s>>>(g, Ap);
+  else if (bk == 7) f16v7_kernel<<<grid, NT, 0, s>>>(g, Ap);
   else if (bk == 32) f16v4_kernel<32><<<grid, NT, 0, s>>>(g, Ap);
   else f16v4_kernel<16><<<grid, NT, 0, s>>>(g, Ap);
   return (int)hipGetLastError();

@@ -70,8 +70,8 @@ def main():
                  wsb, stream())
 
         variants = {"lib f16x3": lib_run, "lib f16p (planes, ping-pong)": lib_planes_run}
-        for bk in (16, 32, 5):
-            variants[f"v4 A+B planes bk{bk}" if bk != 5 else "v5 glds ring4 bk16"] = (
+        for bk in (16, 5, 7):
+            variants[{5: "v5 glds ring4 bk16", 7: "v7 ping-pong, A+B planes"}.get(bk, f"v4 A+B planes bk{bk}")] = (
                 lambda bk=bk: lab.lab_gemm_pp(bk, None, ptr(Ap), ptr(Bp), M, N, K, 2.0 ** -11 / sB,
                                               ptr(C), N, stream()))
         for bk in (16, 32, 33, 6):
