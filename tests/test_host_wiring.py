@@ -58,3 +58,38 @@ def test_output_dropout_needs_an_edge_pass_epilogue():
 def test_reference_wiring_flag_defaults_to_fused():
     m = _model("PPI")
     assert m.fuse_wiring is True
+
+
+def test_split_gemm_kernel_choices(monkeypatch):
+    """Which GEMMs take the pre-split weight planes (gemm_f16p) and the f16x3 weight gradient
+    (gemm_f16rc): PPI's projection / g_x shapes do, small or unaligned weights and wide weight
+    gradients do not, and GATX_F16P=0 turns both off (no GPU call: the library only reports its
+    arithmetic mode)."""
+    from gatx import functional as gf
+    from gatx._lib import lib
+    monkeypatch.delenv("GATX_F16P", raising=False)
+    gf.reset_tuning()
+    lib.gatx_set_gemm_mode(2)
+    try:
+        assert gf.use_weight_planes(1032, 1024, 44900)        # PPI L1 projection
+        assert gf.use_weight_planes(1024, 1032, 44900)        # PPI L1 g_x (W_aug^T)
+        assert not gf.use_weight_planes(48, 1024, 44900)      # small output
+        assert not gf.use_weight_planes(1032, 50, 44900)      # k not a multiple of 4
+        assert not gf.use_weight_planes(1032, 1024, 100)      # few rows
+        assert gf.use_wgrad_f16(1032, 1024, 44900)
+        assert not gf.use_wgrad_f16(4096, 1024, 44900)        # beyond the 2048 column maxima
+        assert not gf.use_wgrad_f16(1032, 50, 44900)
+        assert lib.gatx_gemm_layout_mode(1, 1) == 2 and lib.gatx_gemm_layout_mode(0, 0) == 2
+        assert lib.gatx_gemm_layout_mode(1, 0) == 1
+        monkeypatch.setenv("GATX_F16P", "0")
+        gf.reset_tuning()
+        assert not gf.use_weight_planes(1032, 1024, 44900)
+        assert not gf.use_wgrad_f16(1032, 1024, 44900)
+        lib.gatx_set_gemm_mode(1)
+        monkeypatch.delenv("GATX_F16P")
+        gf.reset_tuning()
+        assert not gf.use_weight_planes(1032, 1024, 44900)    # x3 arithmetic: no planes
+        assert lib.gatx_gemm_layout_mode(1, 1) == 1
+    finally:
+        lib.gatx_set_gemm_mode(2)
+        gf.reset_tuning()
