@@ -852,6 +852,170 @@ __global__ void __launch_bounds__(NT, 1) f16v7_kernel(LabArgs g, const uint16_t*
   }
 }
 
+// v8: v7's ping-pong over v5's LDS-DMA ring: 4 K-tile buffers, tiles kt+1..kt+3 in flight while
+// tile kt is read, no VGPR round trip for the staging. Per K-tile each wave: MEM (issue tile kt+3's
+// DMA into the buffer tile kt-1 used, fragment reads of tile kt, counted vmcnt that retires tile
+// kt+1) | raw barrier | MATH at raised priority | raw barrier; group 1 one barrier behind.
+//   RAW: a wave's vmcnt for tile kt+1 precedes the barrier that ends its MEM(kt); group 0 reads
+//        kt+1 after b(2kt+2), which both groups' MEM(kt) precede; group 1 after b(2kt+3).
+//   WAR: tile kt-1's buffer is refilled in MEM(kt), after b(2kt) (group 0) / b(2kt+1) (group 1);
+//        the last reads of it end MEM1(kt-1), before b(2kt), with lgkmcnt(0).
+// ASPLIT: the activations arrive as fp32 ([4 quads of 4 k][256 rows][16 B]) and are split into
+// the hi / lo fp16 fragments right after the fragment reads (v_fma_mix), in the MEM phase that
+// the other group's MFMAs cover; otherwise both operands are planes (v5's image).
+constexpr int V8_BUF = 32768;
+template <bool ASPLIT>
+__device__ inline void v8_issue(const char* __restrict__ A, int64_t lda4, const char* __restrict__ Bp,
+                                int64_t brow, int64_t m0, int64_t n0, int64_t M, int64_t N, int kt,
+                                char* buf, int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int gi = wave * 4 + i;          // 32 wave-instructions per buffer, 1 KB each
+    const int op = gi >> 4;               // 0 = A (waves 0-3), 1 = B (waves 4-7)
+    // LDS image per operand: [256 rows][4 chunks of 16 B] (one K-tile row = 64 B), chunk c of
+    // row r holding the row's 16-B piece c ^ ((r >> 2) & 3); an instruction moves 16 whole rows
+    // (4 lanes per row: 16 lines touched, not 64) into 1 KB of LDS
+    char* dst = buf + gi * 1024;
+    const int row = (gi & 15) * 16 + (lane >> 2), c = lane & 3;
+    const int w = c ^ ((row >> 2) & 3);
+    const int64_t r0 = op ? n0 : m0, rmax = op ? N : M;
+    int64_t gr = r0 + row;
+    gr = gr < rmax ? gr : rmax - 1;   // rows past the matrix: a valid row, never stored
+    // piece w of the K-tile: planes [slot][plane][8 fp16] or fp32 [quad][4]: both 16 w bytes in
+    const char* src = (op == 0 ? A + gr * (ASPLIT ? lda4 : brow) : Bp + gr * brow) +
+                      (int64_t)kt * 64 + w * 16;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+  }
+}
+
+template <bool ASPLIT>
+__global__ void __launch_bounds__(NT, 1) f16v8_kernel(LabArgs g, const uint16_t* Ap) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * V8_BUF];
+  const int64_t T = ((g.M + TBM - 1) / TBM) * ((g.N + TBN - 1) / TBN);
+  int64_t tm, tn;
+  tile_of(blockIdx.x, T, (g.N + TBN - 1) / TBN, tm, tn);
+  const int64_t m0 = tm * TBM, n0 = tn * TBN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+  const char* A = ASPLIT ? (const char*)g.A : (const char*)Ap;
+  const int64_t lda4 = g.lda * 4;
+  const char* B = (const char*)g.Bp;
+  floatx16 acc[MB][NB];
+#pragma unroll
+  for (int i = 0; i < MB; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int nk = (int)(g.K / 16);
+  auto issue = [&](int t) {
+    v8_issue<ASPLIT>(A, lda4, B, g.brow, m0, n0, g.M, g.N, t,
+                     smem + (t & 3) * V8_BUF, wave, lane);
+  };
+  auto barrier = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  for (int t = 0; t < 3 && t < nk; ++t) issue(t);
+  if (nk >= 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (nk == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  barrier();                 // tile 0 landed for everyone
+  if (wm == 1) barrier();    // group 1 runs one barrier behind
+  const int fr = lane & 31, fs = lane >> 5, sw = (fr >> 2) & 3;
+  const float ca = 64.f;
+  typedef __attribute__((address_space(3))) char lds_char;
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(lds_char*)smem;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 3 < nk) issue(kt + 3);
+    const char* cur = smem + (kt & 3) * V8_BUF;
+    f16x8 fa[MB][2], fb[NB][2];
+    // fragment (row r, 16-B piece w) at r * 64 + ((w ^ sw) * 16), sw = (r >> 2) & 3 = (fr >> 2) & 3
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int x = 0; x < NB; ++x)
+        fb[x][p] = *(const f16x8*)(cur + V8_BUF / 2 + (wn * (NB * 32) + x * 32 + fr) * 64 +
+                                   (((2 * fs + p) ^ sw) * 16));
+    if (ASPLIT) {
+      // the fp32 activation fragments by inline-asm ds_read: read as plain loads, the compiler
+      // drained vmcnt (every DMA in flight) before them; the asm reads carry no such wait, the
+      // counted vmcnt + barrier order them (RAW note above)
+      typedef float f32x4 __attribute__((ext_vector_type(4)));
+      f32x4 u[MB], v[MB];
+      const uint32_t rbase = lds_base + (uint32_t)((kt & 3) * V8_BUF) + (wm * (MB * 32) + fr) * 64;
+      const uint32_t a0 = rbase + (((2 * fs) ^ sw) * 16), a1 = rbase + (((2 * fs + 1) ^ sw) * 16);
+#pragma unroll
+      for (int x = 0; x < MB; ++x)
+        asm volatile("ds_read_b128 %0, %2 offset:%4\n\tds_read_b128 %1, %3 offset:%4"
+                     : "=&v"(u[x]), "=&v"(v[x])
+                     : "v"(a0), "v"(a1), "i"(x * 2048)
+                     : "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int x = 0; x < MB; ++x) {
+        uint32_t h[4], l[4];
+        split_mix(u[x].x, u[x].y, ca, h[0], l[0]);
+        split_mix(u[x].z, u[x].w, ca, h[1], l[1]);
+        split_mix(v[x].x, v[x].y, ca, h[2], l[2]);
+        split_mix(v[x].z, v[x].w, ca, h[3], l[3]);
+        fa[x][0] = __builtin_bit_cast(f16x8, make_uint4(h[0], h[1], h[2], h[3]));
+        fa[x][1] = __builtin_bit_cast(f16x8, make_uint4(l[0], l[1], l[2], l[3]));
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int x = 0; x < MB; ++x)
+          fa[x][p] = *(const f16x8*)(cur + (wm * (MB * 32) + x * 32 + fr) * 64 +
+                                     (((2 * fs + p) ^ sw) * 16));
+    }
+    // retire tile kt+1 (this wave's DMAs of the later tiles stay in flight)
+    if (kt + 3 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int mi = 0; mi < MB; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NB; ++ni)
+        acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][1], fa[mi][0], acc[mi][ni], 0, 0, 0);
+#pragma unroll
+    for (int mi = 0; mi < MB; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NB; ++ni)
+        acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][0], fa[mi][1], acc[mi][ni], 0, 0, 0);
+#pragma unroll
+    for (int mi = 0; mi < MB; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NB; ++ni)
+        acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][0], fa[mi][0], acc[mi][ni], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    barrier();
+  }
+  if (wm == 0) barrier();    // balance group 1's extra barrier
+  const int lr = lane & 31, lc = 4 * (lane >> 5);
+#pragma unroll
+  for (int mi = 0; mi < MB; ++mi) {
+    const int64_t row = m0 + wm * (MB * 32) + mi * 32 + lr;
+    if (row >= g.M) continue;
+#pragma unroll
+    for (int ni = 0; ni < NB; ++ni) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t col = n0 + wn * (NB * 32) + ni * 32 + 8 * j + lc;
+        if (col + 3 < g.N)
+          *(float4*)(g.C + row * g.ldc + col) =
+              make_float4(acc[mi][ni][4 * j] * g.binv, acc[mi][ni][4 * j + 1] * g.binv,
+                          acc[mi][ni][4 * j + 2] * g.binv, acc[mi][ni][4 * j + 3] * g.binv);
+      }
+    }
+  }
+}
+
 // B planes: row n, slot s (8 k): fp16 h[8] = fp16(32 sB b), then l[8] = fp16(32 sB b - h).
 __global__ void split_b_kernel(const float* B, int64_t N, int64_t K, int64_t ldb, float c,
                                uint16_t* Bp, int64_t brow) {
@@ -885,6 +1049,7 @@ extern "C" int lab_gemm_pp(int bk, const float* A_unused, const uint16_t* Ap, co
   const unsigned grid = (unsigned)(((M + 255) / 256) * ((N + 255) / 256));
   if (bk == 5) f16v5_kernel<<<grid, NT, 0, s>>>(g, Ap);
   else if (bk == 7) f16v7_kernel<<<grid, NT, 0, s>>>(g, Ap);
+  else if (bk == 8) f16v8_kernel<false><<<grid, NT, 0, s>>>(g, Ap);
   else if (bk == 32) f16v4_kernel<32><<<grid, NT, 0, s>>>(g, Ap);
   else f16v4_kernel<16><<<grid, NT, 0, s>>>(g, Ap);
   return (int)hipGetLastError();
@@ -897,6 +1062,8 @@ extern "C" int lab_gemm(int bk, int scale, const float* A, int64_t lda, const ui
   const unsigned grid = (unsigned)(((M + 255) / 256) * ((N + 255) / 256));
   if (bk == 6) {   // v6: the ping-pong form of v2 (BK 16, no scaling)
     f16v6_kernel<<<grid, NT, 0, s>>>(g);
+  } else if (bk == 8) {   // v8 with the activation split in the MEM phase
+    f16v8_kernel<true><<<grid, NT, 0, s>>>(g, nullptr);
   } else if (bk == 33) {   // v3: 32-deep K-tiles on 16x16x32 MFMAs
     if (scale) f16v3_kernel<true><<<grid, NT, 0, s>>>(g);
     else f16v3_kernel<false><<<grid, NT, 0, s>>>(g);

@@ -69,18 +69,22 @@ def main():
                  None, 0, -1, None, 0, 0, None, 0, 0, None, 0, None, ptr(ws) if wsb else None,
                  wsb, stream())
 
-        variants = {"lib f16x3": lib_run, "lib f16p (planes, ping-pong)": lib_planes_run}
-        for bk in (16, 5, 7):
-            variants[{5: "v5 glds ring4 bk16", 7: "v7 ping-pong, A+B planes"}.get(bk, f"v4 A+B planes bk{bk}")] = (
-                lambda bk=bk: lab.lab_gemm_pp(bk, None, ptr(Ap), ptr(Bp), M, N, K, 2.0 ** -11 / sB,
-                                              ptr(C), N, stream()))
-        for bk in (16, 32, 33, 6):
-            for sc in (0,):
-                name_ = {33: f"v3 16x16x32 scale{sc}", 6: "v6 ping-pong bk16"}.get(bk, f"v2 bk{bk} scale{sc}")
-                variants[name_] = (
-                    lambda bk=bk, sc=sc: lab.lab_gemm(bk, sc, ptr(A), K, ptr(Bp), M, N, K,
-                                                      2.0 ** -11 / sB, ptr(C), N, ptr(bad),
-                                                      stream()))
+        def pp(bk):
+            return lambda: lab.lab_gemm_pp(bk, None, ptr(Ap), ptr(Bp), M, N, K, 2.0 ** -11 / sB,
+                                           ptr(C), N, stream())
+
+        def v2(bk, sc=0):
+            return lambda: lab.lab_gemm(bk, sc, ptr(A), K, ptr(Bp), M, N, K, 2.0 ** -11 / sB,
+                                        ptr(C), N, ptr(bad), stream())
+
+        variants = {"lib f16x3": lib_run, "lib f16p (planes, ping-pong)": lib_planes_run,
+                    "v4 A+B planes bk16": pp(16), "v5 glds ring4 bk16": pp(5),
+                    "v7 ping-pong, A+B planes": pp(7), "v8 pp + glds ring (row-major), A+B planes": pp(8),
+                    "v2 bk16 scale0": v2(16), "v3 16x16x32 scale0": v2(33),
+                    "v6 ping-pong bk16": v2(6), "v8 pp + glds ring (row-major), A split": v2(8)}
+        only = os.environ.get("LAB_ONLY")
+        if only:
+            variants = {k: f for k, f in variants.items() if any(t in k for t in only.split(","))}
         errs = {}
         for vn, fn in variants.items():
             C.zero_()
