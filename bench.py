@@ -428,7 +428,7 @@ def cpu_baseline(model, cfg, ds, graphs, budget_s=20.0):
                                         cfg["add_skip_connection"])
     best, n = _cpu_timer(run, budget_s)
     e_tot = sum(a.shape[0] for a in res["o"][2])
-    return {"value": e_tot / best, "unit": "layer-edges/s", "cores": cores, "kind": "restatement",
+    return {"value": e_tot / best, "unit": "layer-edges/s", "cores": cores, "kind": "port",
             "sample": f"torch-eager restatement of the reference dataflow (oracle/torch_dataflow.py),"
                       f" {ds} {len(dims)}-layer fwd on {graphs} graph(s) (N={b.num_nodes}, sum "
                       f"E'={e_tot}), {cores} threads, best of {n}: {best:.3f} s; the reference "
@@ -453,7 +453,7 @@ def cpu_baseline_rmat(W, a, NH, F, budget_s=20.0):
             res["o"] = td.layer_forward(x, ei, Wt, at, NH, F, True)
     best, k = _cpu_timer(run, budget_s)
     E2 = res["o"][2].shape[0]
-    return {"value": E2 / best, "unit": "layer-edges/s", "cores": cores, "kind": "restatement",
+    return {"value": E2 / best, "unit": "layer-edges/s", "cores": cores, "kind": "port",
             "sample": f"torch-eager restatement of the reference dataflow, 1 GATLayer fwd on a "
                       f"SCALED RMAT (N={n}, E'={E2}; the full 1e7/1.6e8 graph is infeasible on "
                       f"CPU), {cores} threads, best of {k}: {best:.3f} s"}
