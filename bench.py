@@ -561,7 +561,7 @@ TRAIN_PHASES = {
     # (pre-split f16x3 g_x / the in-loop kernel; the f16x3 weight gradient / its x3 form)
     "bwd_gemm_gx": ("mfma", ("gemm_f16p_kernel<16, 1", "gemm_f16p_kernel<32, 1",
                              "gemm_x3_kernel<true, true, true, 1,")),
-    "bwd_gemm_gw": ("mfma", ("gemm_f16rc_kernel<", "gemm_x3_kernel<false, false, true, 2, 1,")),
+    "bwd_gemm_gw": ("mfma", ("gemm_f16rc_kernel<", "gemm_x3_kernel<false, false, true, 2, 1>")),
     "edge_forward": ("hbm", "edge_forward_kernel"),
     "bwd_edge_dst": ("hbm", "edge_bwd_dst"),
     "bwd_edge_src": ("hbm", "edge_bwd_src"),

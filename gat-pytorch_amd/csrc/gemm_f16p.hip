@@ -372,7 +372,7 @@ __global__ void __launch_bounds__(512, 1) gemm_f16p_kernel(GemmArgs g) {
     if (x3) {
       if (threadIdx.x == 0 && g.fb_counter)
         __hip_atomic_fetch_add(g.fb_counter, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      x3_mainloop<true, true, false, 1, 0>(g, A, g.B, m0, n0, kb, K, ceil_div(K - kb, C::BK),
+      x3_mainloop<true, true, false, 1>(g, A, g.B, m0, n0, kb, K, ceil_div(K - kb, C::BK),
                                            smem, wm, wn, lane, acc);
     }
   }
@@ -628,7 +628,7 @@ __global__ void __launch_bounds__(512, 1) gemm_f16rc_kernel(GemmArgs g) {
       if (threadIdx.x == 0 && g.fb_counter)
         __hip_atomic_fetch_add(g.fb_counter, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __syncthreads();
-      x3_mainloop<false, false, !VEC, 1, 0>(g, g.A, g.B, m0, n0, kb, K, nk, smem, wm, wn, lane,
+      x3_mainloop<false, false, !VEC, 1>(g, g.A, g.B, m0, n0, kb, K, nk, smem, wm, wn, lane,
                                             acc);
     }
   }

@@ -19,7 +19,7 @@ __global__ void fallback_read_kernel(unsigned long long* dst, int reset) {
 }
 
 
-template <bool A_KC, bool B_KC, bool VEC, int TAG, int CFG, int DBG = 0>
+template <bool A_KC, bool B_KC, bool VEC, int TAG, int CFG>
 __global__ void __launch_bounds__(X3Cfg<CFG>::NT, X3Cfg<CFG>::MINB) gemm_x3_kernel(GemmArgs g,
                                                                                    int arith) {
   using C = X3Cfg<CFG>;
@@ -64,7 +64,7 @@ __global__ void __launch_bounds__(X3Cfg<CFG>::NT, X3Cfg<CFG>::MINB) gemm_x3_kern
   const int64_t nk = K > kb ? ceil_div(K - kb, C::BK) : 0;
   if (nk > 0) {
     bool x3 = true;
-    if constexpr (A_KC && B_KC && DBG == 0) if (arith == 2) {
+    if constexpr (A_KC && B_KC) if (arith == 2) {
       // row scaling for the gradient GEMMs (TAG != 0: A = G_aug, rows ~1e-7); the forward
       // projection's activations are in range as they come (a row that is not takes the fallback)
       constexpr bool SCALE = TAG != 0;
@@ -94,14 +94,14 @@ __global__ void __launch_bounds__(X3Cfg<CFG>::NT, X3Cfg<CFG>::MINB) gemm_x3_kern
     }
     if (x3) {
       if (VEC)
-        x3_mainloop<A_KC, B_KC, false, CFG, DBG>(g, A, B, m0, n0, kb, K, nk, smem, wm, wn, lane, acc);
+        x3_mainloop<A_KC, B_KC, false, CFG>(g, A, B, m0, n0, kb, K, nk, smem, wm, wn, lane, acc);
       else
-        x3_mainloop<A_KC, B_KC, true, CFG, DBG>(g, A, B, m0, n0, kb, K, nk, smem, wm, wn, lane, acc);
+        x3_mainloop<A_KC, B_KC, true, CFG>(g, A, B, m0, n0, kb, K, nk, smem, wm, wn, lane, acc);
     }
   }
   write_tile_t<C::MB, C::NB, C::TBM, C::TBN>(g, acc, tail_z, tail_ti, m0, n0, wm, wn, lane);
   // (tail slices are scored by tail_fixup_scores_kernel once summed)
-  if constexpr (TAG == 0 && DBG == 0)
+  if constexpr (TAG == 0)
     if (g.s_part && tail_z < 0)
       scores_tile<C::MB, C::NB, C::TBM, C::TBN, C::WGN>(g, acc, m0, n0, tn, wm, wn, lane, smem);
 }
@@ -115,26 +115,6 @@ int launch_gemm_x3(const gk::GemmArgs& g, bool a_kc, bool b_kc, int batch, int t
   dim3 grid((unsigned)gx, (unsigned)batch, (unsigned)g.splits);
   const int cfg = g.bm == 256 ? 1 : 0;
   const int arith = gatx_get_gemm_mode();   // 1: bf16 split (x3), 2: fp16 split (f16x3)
-  // tuning probes only (wrong results): GATX_X3_DBG=1 conversion without the split arithmetic,
-  // 2 no next-tile LDS stores, 3 no operand loads or stores, 4 MFMAs only (no LDS reads after the
-  // first K-tile, no barriers)
-  static const int dbg = [] {
-    const char* e = getenv("GATX_X3_DBG");
-    return e ? atoi(e) : 0;
-  }();
-  if (dbg && a_kc && b_kc && g.a_vec && g.b_vec) {
-    if (cfg == 1) {
-      if (dbg == 1) gemm_x3_kernel<true, true, true, 0, 1, 1><<<grid, 512, 0, stream>>>(g, 1);
-      else if (dbg == 2) gemm_x3_kernel<true, true, true, 0, 1, 2><<<grid, 512, 0, stream>>>(g, 1);
-      else if (dbg == 3) gemm_x3_kernel<true, true, true, 0, 1, 3><<<grid, 512, 0, stream>>>(g, 1);
-      else gemm_x3_kernel<true, true, true, 0, 1, 4><<<grid, 512, 0, stream>>>(g, 1);
-    } else {
-      if (dbg == 1) gemm_x3_kernel<true, true, true, 0, 0, 1><<<grid, 256, 0, stream>>>(g, 1);
-      else gemm_x3_kernel<true, true, true, 0, 0, 2><<<grid, 256, 0, stream>>>(g, 1);
-    }
-    GATX_LAUNCH_CHECK("gemm_x3 (probe)");
-    return 0;
-  }
 #define GATX_X3_V(AK, BKC, V, TG)                                                             \
   do {                                                                                        \
     if (cfg == 1) gemm_x3_kernel<AK, BKC, V, TG, 1><<<grid, 512, 0, stream>>>(g, arith);         \

@@ -74,7 +74,7 @@ struct PlaneImg {
 };
 
 // Staging of one operand tile: NV float4 per thread, thread idx -> (row, k) as Tile<> maps it.
-template <bool KC, int ROWS, int BK, int NT, int DBG = 0>
+template <bool KC, int ROWS, int BK, int NT>
 struct X3Tile {
   using T = Tile<KC, ROWS, BK, NT>;
   static constexpr int NV = T::NV;
@@ -158,13 +158,8 @@ struct X3Tile {
       const int idx = threadIdx.x + NT * c;
       const int row = row_of(idx), kk = k_of(idx);
       uint32_t h0, m0, l0, h1, m1, l1;
-      if (DBG == 1) {   // tuning probe: conversion only (wrong values), measures the split's cost
-        h0 = m0 = l0 = cvt_pk_bf16(v[c].x, v[c].y);
-        h1 = m1 = l1 = cvt_pk_bf16(v[c].z, v[c].w);
-      } else {
-        split_pair(v[c].x, v[c].y, h0, m0, l0);
-        split_pair(v[c].z, v[c].w, h1, m1, l1);
-      }
+      split_pair(v[c].x, v[c].y, h0, m0, l0);
+      split_pair(v[c].z, v[c].w, h1, m1, l1);
       const int o = Img::off(row, kk);
       *(uint2*)(img + o) = make_uint2(h0, h1);
       *(uint2*)(img + Img::BYTES + o) = make_uint2(m0, m1);
@@ -203,15 +198,15 @@ struct X3Cfg {
 // Main loop over nk K-tiles starting at kb. MASK (unaligned operands): every tile through
 // Tile::load's clamped scalar/vector loads and full masking. Otherwise each thread streams its
 // float4s from fixed per-thread pointers; only a partial last K-tile is masked (k >= K zeroed).
-template <bool A_KC, bool B_KC, bool MASK, int CFG, int DBG>
+template <bool A_KC, bool B_KC, bool MASK, int CFG>
 __device__ inline void x3_mainloop(const GemmArgs& g, const float* __restrict__ A,
                                    const float* __restrict__ B, int64_t m0, int64_t n0,
                                    int64_t kb, int64_t K, int64_t nk, char* smem, int wm, int wn,
                                    int lane, floatx16 (&acc)[X3Cfg<CFG>::MB][X3Cfg<CFG>::NB]) {
   using C = X3Cfg<CFG>;
   constexpr int NT = C::NT, BK = C::BK, MB = C::MB, NB = C::NB;
-  using TA = X3Tile<A_KC, C::TBM, BK, NT, DBG>;
-  using TB = X3Tile<B_KC, C::TBN, BK, NT, DBG>;
+  using TA = X3Tile<A_KC, C::TBM, BK, NT>;
+  using TB = X3Tile<B_KC, C::TBN, BK, NT>;
   constexpr int PA = TA::Img::BYTES, PBy = TB::Img::BYTES;   // bytes per plane
   constexpr int STAGE = 3 * (PA + PBy);                      // A planes h, m, l then B's
   const int64_t M = g.M, N = g.N;
@@ -301,7 +296,7 @@ __device__ inline void x3_mainloop(const GemmArgs& g, const float* __restrict__ 
     TA::template store<false, false>(st, va, m0, M, 0, K);
     TB::template store<false, false>(st + 3 * PA, vb, n0, N, 0, K);
   };
-  if constexpr (!MASK && DBG <= 1 && CFG == 1) {
+  if constexpr (!MASK && CFG == 1) {
     // Steady state (full K-tiles, no branches): operands one K-tile further ahead. Tile kt + 1
     // (loaded during iteration kt - 1) is split into the other stage right after this tile's
     // fragment reads, then tile kt + 2's loads go out, then the MFMAs: the LDS stores drain under
@@ -336,11 +331,11 @@ __device__ inline void x3_mainloop(const GemmArgs& g, const float* __restrict__ 
     char* cur = smem + (kt & 1) * STAGE;
     char* nxt = smem + ((kt & 1) ^ 1) * STAGE;
     const bool more = kt + 1 < nk;
-    if (more && DBG < 3) load(kb + (kt + 1) * BK);
-    if (DBG != 4 || kt == 0) frags(cur);   // probe 4: fragments of the first K-tile reused
+    if (more) load(kb + (kt + 1) * BK);
+    frags(cur);
     mfmas();   // small terms first: (l,h) (h,l) (m,m) (m,h) (h,m) (h,h)
-    if (more && DBG < 2) store(nxt, kb + (kt + 1) * BK);
-    if (DBG != 4) __syncthreads();
+    if (more) store(nxt, kb + (kt + 1) * BK);
+    __syncthreads();
   }
 }
 
