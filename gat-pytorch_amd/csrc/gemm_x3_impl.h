@@ -302,7 +302,7 @@ __device__ inline void x3_mainloop(const GemmArgs& g, const float* __restrict__ 
     // fragment reads, then tile kt + 2's loads go out, then the MFMAs: the LDS stores drain under
     // the MFMAs instead of just ahead of the barrier, and the global loads have a whole
     // iteration to land. -5 to -6% against load-at-top / store-at-bottom on the PPI projection
-    // and 8192 x 4096 x 4096 shapes (tools/gpu_x3_ab.sh); forcing an interleave with
+    // and 8192 x 4096 x 4096 shapes (round-2 interleaved A/B); forcing an interleave with
     // sched_group_barrier was slower than the compiler's schedule. A partial last tile and the
     // unaligned (MASK) path take the generic loop below, and so does CFG 0 (three workgroups per
     // CU: the extra live operands spill under its 168-VGPR cap).
