@@ -604,13 +604,17 @@ __global__ void __launch_bounds__(NT, 1) f16v5_kernel(LabArgs g, const uint16_t*
 // group 0 ends with one extra, so every s_barrier pairs group 0's n-th call with group 1's n-th.
 // Buffer reuse: a wave stores tile i+1 into buffer (i+1)&1 after the barrier that follows every
 // wave's reads of tile i-1 (see the lab notes in DESIGN.md §8).
+// LDSB: the block's LDS allocation in bytes (>= 64 KB; the library kernel's is 99.5 KB, sized
+// for its fused x3 fallback) — a probe of whether the allocation alone costs time.
+template <int LDSB = 65536>
 __global__ void __launch_bounds__(NT, 1) f16v6_kernel(LabArgs g) {
   constexpr int BK = 16;
   using I = Img<BK>;
   constexpr int PB = I::BYTES;
   constexpr int STAGE = 4 * PB;
   constexpr int NVA = BK / 8, NVB = BK / 8, TPR = BK / 4;
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  static_assert(LDSB >= 2 * STAGE, "LDS allocation below the two stages");
+  __shared__ __attribute__((aligned(16))) char smem[LDSB];
   const int64_t T = ((g.M + TBM - 1) / TBM) * ((g.N + TBN - 1) / TBN);
   int64_t tm, tn;
   tile_of(blockIdx.x, T, (g.N + TBN - 1) / TBN, tm, tn);
@@ -1061,7 +1065,9 @@ extern "C" int lab_gemm(int bk, int scale, const float* A, int64_t lda, const ui
   LabArgs g{A, lda, Bp, K * 4, M, N, K, C, ldc, binv, bad};
   const unsigned grid = (unsigned)(((M + 255) / 256) * ((N + 255) / 256));
   if (bk == 6) {   // v6: the ping-pong form of v2 (BK 16, no scaling)
-    f16v6_kernel<<<grid, NT, 0, s>>>(g);
+    f16v6_kernel<><<<grid, NT, 0, s>>>(g);
+  } else if (bk == 60) {   // v6 with the library kernel's 99.5 KB LDS allocation
+    f16v6_kernel<99584><<<grid, NT, 0, s>>>(g);
   } else if (bk == 8) {   // v8 with the activation split in the MEM phase
     f16v8_kernel<true><<<grid, NT, 0, s>>>(g, nullptr);
   } else if (bk == 33) {   // v3: 32-deep K-tiles on 16x16x32 MFMAs

@@ -38,6 +38,9 @@ def timed(fn, reps=10):
 def main():
     shapes = [("L1 44900x1024x1024", 44900, 1024, 1024), ("L2 44900x768x1024", 44900, 768, 1024),
               ("8192^2 x 4096", 8192, 8192, 4096)]
+    if os.environ.get("LAB_SHAPES") == "waves":   # the L1 shape at whole / partial waves of tiles
+        shapes = [(f"M={m} ({(m + 255) // 256 * 4} tiles) x1024x1024", m, 1024, 1024)
+                  for m in (32768, 40960, 44900, 49152)]
     for name, M, N, K in shapes:
         g = torch.Generator(device=dev).manual_seed(1)
         A = torch.randn(M, K, device=dev, generator=g)
@@ -81,7 +84,8 @@ def main():
                     "v4 A+B planes bk16": pp(16), "v5 glds ring4 bk16": pp(5),
                     "v7 ping-pong, A+B planes": pp(7), "v8 pp + glds ring (row-major), A+B planes": pp(8),
                     "v2 bk16 scale0": v2(16), "v3 16x16x32 scale0": v2(33),
-                    "v6 ping-pong bk16": v2(6), "v8 pp + glds ring (row-major), A split": v2(8)}
+                    "v6 ping-pong bk16": v2(6), "v6 + 99.5 KB LDS": v2(60),
+                    "v8 pp + glds ring (row-major), A split": v2(8)}
         only = os.environ.get("LAB_ONLY")
         if only:
             variants = {k: f for k, f in variants.items() if any(t in k for t in only.split(","))}
