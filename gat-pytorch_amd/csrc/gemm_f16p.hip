@@ -24,6 +24,7 @@
 // test_gemm_f16p_accuracy). Loads go through buffer resources bounded to the tile's rows: rows
 // past M or N read as zero.
 #include <cstring>
+#include <type_traits>
 
 #include "gemm_x3_impl.h"
 
@@ -110,8 +111,8 @@ __device__ inline bool f16p_mainloop(const GemmArgs& g, const float* __restrict_
   }
   float4 va[NV];
   uint4 vb[NV];
-  const int64_t nk = ceil_div(K - kb, BK);
-  auto load = [&](int64_t kt) {
+  const int nk = (int)ceil_div(K - kb, BK);
+  auto load = [&](int kt) {
     const int so = (int)((kb + kt * BK) * 4);   // bytes: 4 per k in A and in the planes
 #pragma unroll
     for (int c = 0; c < NV; ++c)
@@ -134,8 +135,8 @@ __device__ inline bool f16p_mainloop(const GemmArgs& g, const float* __restrict_
   };
   // the last K-tile may run past K: A's k >= K would read the next row (B's planes are zero
   // there, but an inf / nan in A would still poison the sums) -> zeroed
-  auto mask_tail = [&](int64_t kt) {
-    const int64_t k0 = kb + kt * BK;
+  auto mask_tail = [&](int kt) {
+    const int64_t k0 = kb + (int64_t)kt * BK;
     if (k0 + BK <= K) return;
 #pragma unroll
     for (int c = 0; c < NV; ++c) {
@@ -201,9 +202,12 @@ __device__ inline bool f16p_mainloop(const GemmArgs& g, const float* __restrict_
     };
     barrier();               // tile 0 staged by every wave
     if (wm == 1) barrier();  // group 1 one barrier behind
-    for (int64_t kt = 0; kt < nk; ++kt) {
-      const char* cur = smem + (kt & 1) * STAGE;
-      char* nxt = smem + ((kt & 1) ^ 1) * STAGE;
+    // one K-tile; the stage is a compile-time constant (the loop below is unrolled by two), so
+    // the fragment reads and stores take immediate LDS offsets instead of per-tile address math
+    auto step = [&](int kt, auto stage) {
+      constexpr int CS = decltype(stage)::value;
+      const char* cur = smem + CS * STAGE;
+      char* nxt = smem + (CS ^ 1) * STAGE;
       f16x8 fa[MB][2], fb[NB][2];
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
@@ -240,11 +244,17 @@ __device__ inline bool f16p_mainloop(const GemmArgs& g, const float* __restrict_
           acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][0], fa[mi][0], acc[mi][ni], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
       barrier();
+    };
+    int kt = 0;
+    for (; kt + 1 < nk; kt += 2) {
+      step(kt, std::integral_constant<int, 0>{});
+      step(kt + 1, std::integral_constant<int, 1>{});
     }
+    if (kt < nk) step(kt, std::integral_constant<int, 0>{});
     if (wm == 0) barrier();  // balances group 1's extra barrier
   } else {
   __syncthreads();
-  for (int64_t kt = 0; kt < nk; ++kt) {
+  for (int kt = 0; kt < nk; ++kt) {
     const char* cur = smem + (kt & 1) * STAGE;
     char* nxt = smem + ((kt & 1) ^ 1) * STAGE;
 #pragma unroll
@@ -334,7 +344,8 @@ __global__ void __launch_bounds__(512, 1) gemm_f16p_kernel(GemmArgs g) {
   }
   const int64_t m0 = tm * 256, n0 = tn * 256;
   const float* __restrict__ A = g.A;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // wave id through readfirstlane: known uniform, so the ping-pong's group branches stay scalar
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave / C::WGN, wn = wave % C::WGN;
   floatx16 acc[C::MB][C::NB];
 #pragma unroll
