@@ -689,7 +689,7 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
   g.elu = elu;
   g.splits = 1; g.k_per_split = K; g.partial = nullptr;
   g.s_a = nullptr; g.s_nh = g.s_f = g.s_fp = g.s_h2 = 0; g.s_part = nullptr;
-  g.b_planes = nullptr; g.b_prow = 0; g.fb_counter = f16_fallback_counter();
+  g.b_planes = nullptr; g.b_prow = 0;
   g.a_rowmax = a_rowmax;
   auto aligned = [](const void* p, int64_t ld, int64_t bs) {
     return ((uintptr_t)p % 16 == 0) && (ld % 4 == 0) && (bs % 4 == 0);
@@ -828,7 +828,9 @@ extern "C" int gatx_gemm_layout_mode(int a_kc, int b_kc) {
 
 extern "C" int gatx_gemm_fallback_read(uint64_t* dst, int reset, gatx_stream_t stream) {
   GATX_REQUIRE(dst != nullptr, "gatx_gemm_fallback_read: dst is NULL");
-  return read_f16_fallbacks((unsigned long long*)dst, reset, (hipStream_t)stream);
+  int rc = read_f16_fallbacks((unsigned long long*)dst, reset, (hipStream_t)stream);
+  if (rc) return rc;
+  return read_f16p_fallbacks((unsigned long long*)dst, reset, (hipStream_t)stream);
 }
 
 extern "C" size_t gatx_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K) {

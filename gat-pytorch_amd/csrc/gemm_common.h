@@ -122,9 +122,8 @@ struct GemmArgs {
   // reference's attention vector s_a (heads s_nh, features s_f, padded s_fp per head of Wh)
   const float* s_a; int s_nh, s_f, s_fp, s_h2; float* s_part;
   // f16p (gemm_f16p.hip): B's pre-split fp16 planes (after their header; nullptr = none) with
-  // b_prow bytes per row, and the f16x3 -> x3 fallback tile counter
+  // b_prow bytes per row
   const void* b_planes; int64_t b_prow;
-  unsigned long long* fb_counter;
   // exact max |A row| per row (gatx_absmax_rows_cols; nullptr = none): the split kernels scale
   // each A row by it instead of by its first K-tile's max
   const float* a_rowmax;
@@ -302,9 +301,10 @@ int absmax_rows_cols(const float* X, int64_t rows, int64_t cols, int64_t ld, flo
 int build_weight_planes(const float* W, int64_t rows, int64_t K, int64_t ld, void* buf,
                         hipStream_t stream);
 // gemm_x3.hip: the device address of the f16x3 -> x3 fallback tile counter
-unsigned long long* f16_fallback_counter();
 // gemm_x3.hip: copy (and optionally zero) the f16x3 -> x3 fallback tile counter
 int read_f16_fallbacks(unsigned long long* dst, int reset, hipStream_t stream);
+// adds gemm_f16p.hip's own count to dst[0] (after read_f16_fallbacks wrote it)
+int read_f16p_fallbacks(unsigned long long* dst, int reset, hipStream_t stream);
 // the x3 kernel instance whose occupancy sizes tail / split-K decisions
 const void* gemm_x3_occupancy_fn(int cfg);   // cfg 0: 128 x 128 tiles, 1: 256 x 256
 

@@ -32,6 +32,21 @@ namespace gatx {
 namespace {
 using namespace gk;
 
+// This file's f16x3 -> x3 fallback workgroups (gemm_x3.hip keeps its own count for the in-loop
+// kernels): a __device__ symbol of this code object, so every launch counts on the device it
+// runs on (a pointer cached from another translation unit would name one device's copy).
+__device__ unsigned long long g_f16p_fallback_tiles = 0;
+
+__global__ void f16p_fallback_add_kernel(unsigned long long* dst, int reset) {
+  if (threadIdx.x == 0) {
+    dst[0] += __hip_atomic_load(&g_f16p_fallback_tiles, __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_AGENT);
+    if (reset)
+      __hip_atomic_store(&g_f16p_fallback_tiles, 0ull, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // h = fp16_rn(x c), l = fp16_rn(x c - h) for an element pair (x in the low halves): v_fma_mix
 // rounds the exact product and then the exact residual (hipcc never selects fma_mix here).
 __device__ inline void split_mix(float x, float y, float c, uint32_t& h, uint32_t& l) {
@@ -61,6 +76,7 @@ struct PImg {
 };
 
 constexpr int kPlanesHeader = 256;   // bytes before the planes: [0] 2^-11 / s_B, [1] s_B, [16..] tile flags
+constexpr int64_t kPlanesMaxRows = 60 * 256;   // one header flag per 256-row tile: 60 fit
 
 template <int BK>
 struct F16pCfg {
@@ -381,8 +397,9 @@ __global__ void __launch_bounds__(512, 1) gemm_f16p_kernel(GemmArgs g) {
       __syncthreads();   // inv read before the fallback or the epilogue reuses the LDS
     }
     if (x3) {
-      if (threadIdx.x == 0 && g.fb_counter)
-        __hip_atomic_fetch_add(g.fb_counter, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (threadIdx.x == 0)
+        __hip_atomic_fetch_add(&g_f16p_fallback_tiles, 1ull, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
       x3_mainloop<true, true, false, 1>(g, A, g.B, m0, n0, kb, K, ceil_div(K - kb, C::BK),
                                            smem, wm, wn, lane, acc);
     }
@@ -636,8 +653,9 @@ __global__ void __launch_bounds__(512, 1) gemm_f16rc_kernel(GemmArgs g) {
         for (int r = 0; r < 16; ++r) acc[i][j][r] = x3 ? 0.f : acc[i][j][r] * f;
     }
     if (x3) {
-      if (threadIdx.x == 0 && g.fb_counter)
-        __hip_atomic_fetch_add(g.fb_counter, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (threadIdx.x == 0)
+        __hip_atomic_fetch_add(&g_f16p_fallback_tiles, 1ull, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
       __syncthreads();
       x3_mainloop<false, false, !VEC, 1>(g, g.A, g.B, m0, n0, kb, K, nk, smem, wm, wn, lane,
                                             acc);
@@ -830,6 +848,12 @@ void launch_absmax(const float* X, int64_t rows, int64_t cols, int64_t ld, float
 
 }  // namespace
 
+int read_f16p_fallbacks(unsigned long long* dst, int reset, hipStream_t stream) {
+  f16p_fallback_add_kernel<<<1, 64, 0, stream>>>(dst, reset);
+  GATX_LAUNCH_CHECK("gatx_gemm_fallback_read");
+  return 0;
+}
+
 int absmax_rows_cols(const float* X, int64_t rows, int64_t cols, int64_t ld, float* rowmax,
                      float* colmax, hipStream_t stream) {
   GATX_REQUIRE(cols <= 2048, "absmax_rows_cols: at most 2048 columns");
@@ -844,13 +868,15 @@ int absmax_rows_cols(const float* X, int64_t rows, int64_t cols, int64_t ld, flo
 }
 
 size_t weight_planes_bytes(int64_t rows, int64_t K) {
+  if (rows <= 0 || rows > kPlanesMaxRows || K <= 0) return 0;   // no planes for this shape
   return (size_t)kPlanesHeader + (size_t)rows * round_up(K, (int64_t)32) * 4 +
          4 * (size_t)(rows + ceil_div(rows, (int64_t)4));
 }
 
 int build_weight_planes(const float* W, int64_t rows, int64_t K, int64_t ld, void* buf,
                         hipStream_t stream) {
-  GATX_REQUIRE(rows <= 60 * 256, "weight planes: at most 15360 rows (tile flags in the header)");
+  GATX_REQUIRE(rows <= kPlanesMaxRows,
+               "weight planes: at most 15360 rows (tile flags in the header)");
   char* planes = (char*)buf + kPlanesHeader;
   float* rowmax = (float*)(planes + rows * round_up(K, (int64_t)32) * 4);
   const int64_t nblk = ceil_div(rows, (int64_t)4);

@@ -142,18 +142,6 @@ int launch_gemm_x3(const gk::GemmArgs& g, bool a_kc, bool b_kc, int batch, int t
   return 0;
 }
 
-unsigned long long* f16_fallback_counter() {
-  static unsigned long long* p = [] {
-    void* a = nullptr;
-    if (hipGetSymbolAddress(&a, HIP_SYMBOL(g_f16_fallback_tiles)) != hipSuccess) {
-      (void)hipGetLastError();
-      a = nullptr;
-    }
-    return (unsigned long long*)a;
-  }();
-  return p;
-}
-
 int read_f16_fallbacks(unsigned long long* dst, int reset, hipStream_t stream) {
   fallback_read_kernel<<<1, 64, 0, stream>>>(dst, reset);
   GATX_LAUNCH_CHECK("gatx_gemm_fallback_read");

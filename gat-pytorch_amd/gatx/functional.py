@@ -205,10 +205,12 @@ def use_weight_planes(rows: int, k: int, m: int) -> bool:
     """Whether a GEMM with this weight operand takes the pre-split f16x3 kernel (gemm_f16p.hip):
     the f16x3 arithmetic, float4-aligned rows, and outputs big enough for its 256 x 256 tiles (the
     library makes the final choice; planes it does not use cost one small build per weight
-    version). GATX_F16P=0: never build them."""
+    version; gatx_weight_planes_bytes is 0 for a weight too tall for the planes' header, which
+    then takes the in-loop split kernel). GATX_F16P=0: never build them."""
     if _env_int("GATX_F16P", 1) == 0 or lib.gatx_get_gemm_mode() != 2:
         return False
-    return k % 4 == 0 and rows >= 256 and m >= 256
+    return (k % 4 == 0 and rows >= 256 and m >= 256
+            and lib.gatx_weight_planes_bytes(rows, k) > 0)
 
 
 def use_wgrad_f16(M: int, N: int, K: int) -> bool:
@@ -511,7 +513,6 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
     # the weight operand pre-split into fp16 planes (gemm_f16p.hip; None: in-loop split)
     planes = projection_planes(W_aug, sh, N)
     pp = ptr(planes) if planes is not None else None
-    saved["planes"] = planes
     if C:   # one launch: [Wh | S | R] = x [W_aug; W_skip_eff]^T into three outputs
         with _span("gemm", (N, sh.K_aug + C, sh.F_in, sh.NH, sh.F)):
             call("gatx_gemm_planes", N, sh.K_aug + C, sh.F_in, ptr(x), sh.F_in, ptr(W_aug),

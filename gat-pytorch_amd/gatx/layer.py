@@ -18,10 +18,16 @@ import torch
 from torch import nn
 
 from . import ops  # noqa: F401  (registers torch.ops.gatx.*)
-from .functional import LazyAlpha, _env_int, gat_layer_lazy
+from .functional import LazyAlpha, gat_layer_lazy
 
 
 class GATLayer(nn.Module):
+    # Opt-in (default off, as the reference writes alpha in every forward, `:106-110`): with
+    # lazy_alpha an inference forward (autograd off, no return_attention_weights) keeps the
+    # softmax state and runs the alpha pass when normalised_attention_coeffs is first read
+    # (functional.LazyAlpha: same kernel, same inputs, bitwise the same values).
+    lazy_alpha = False
+
     def __init__(self, in_features, out_features, num_heads, concat, dropout=0,
                  add_self_loops=False, bias=False, const_attention=False):
         super().__init__()
@@ -65,8 +71,8 @@ class GATLayer(nn.Module):
         """alpha of the last forward (`models/gat_layer.py:110`), (E', NH) in edge_index' order.
         Kept at its allocation bound until read: the exact E' lives on the device, so the slice
         (one host read of E') happens here, not in forward. After an inference forward (autograd
-        off, no return_attention_weights) the alpha pass itself runs on this first read
-        (functional.LazyAlpha: same kernel, same inputs, same values)."""
+        off, no return_attention_weights) of a layer with `lazy_alpha` set, the alpha pass itself
+        runs on this first read (functional.LazyAlpha: same kernel, same inputs, same values)."""
         att = self.__dict__.get("_attention")
         if att is None or isinstance(att, torch.Tensor):
             return att
@@ -106,9 +112,7 @@ class GATLayer(nn.Module):
             self.__dict__["_attention"] = alpha
             return (out, (ei2, alpha)) if return_attention_weights else out
         seed = self._dropout_seed(x.device) if p > 0 else 0
-        # GATX_DEFER_ALPHA=0: every forward writes alpha, as the reference does (bench.py times
-        # the forward both ways)
-        defer = not return_attention_weights and _env_int("GATX_DEFER_ALPHA", 1) != 0
+        defer = self.lazy_alpha and not return_attention_weights
         out, g, alpha = gat_layer_lazy(
             x, edge_index, self.W.weight, None if self.const_attention else self.a.weight,
             self.bias_param if self.bias else None, self.num_heads, self.out_features,

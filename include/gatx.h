@@ -142,7 +142,8 @@ int gatx_get_gemm_mode(void);
  * (the scale and per-256-row-tile range flags) and the build's scratch (row maxima; two launches,
  * no memset). Built once per weight version (the
  * projection's W_aug, the backward's W_aug^T) and passed to gatx_gemm_planes; the buffer
- * (gatx_weight_planes_bytes) must be 256-byte aligned. Replaces nothing in the reference: it is
+ * (gatx_weight_planes_bytes; 0 for a shape that cannot take planes: rows > 15360, the header's
+ * tile flags) must be 256-byte aligned. Replaces nothing in the reference: it is
  * how `self.W(x)` (models/gat_layer.py:64) keeps fp32 accuracy on the fp16 matrix cores. */
 size_t gatx_weight_planes_bytes(int64_t rows, int64_t K);
 int gatx_weight_planes(const float* W, int64_t rows, int64_t K, int64_t ld, void* planes,

@@ -327,3 +327,48 @@ def planetoid_step_grads(x, edge_index, layers, num_heads, out_features, concat,
     _, grads = gat_model_forward_backward(x, edge_index, layers, [], num_heads, out_features,
                                           concat, [False] * L, g_out, g_alphas=g_al)
     return ce + attention_reward * norm, grads
+
+
+def bce_logits_grad(logits, target, pos_weight=None):
+    """torch.nn.BCEWithLogitsLoss(reduction='mean', pos_weight=p) and its gradient
+    (`models/ppi_gat.py:11,19`; PatternGAT's class-balanced form, `models/pattern_gat.py:11-15,
+    23`): l = -(p y log s(x) + (1 - y) log(1 - s(x))), mean over every element;
+    d l / d x = ((p y + 1 - y) s(x) - p y) / n. Returns (loss, grad)."""
+    x = np.asarray(logits, dtype=np.float64)
+    y = np.asarray(target, dtype=np.float64)
+    p = 1.0 if pos_weight is None else float(pos_weight)
+    # log s(x) = -softplus(-x), log(1 - s(x)) = -softplus(x), stably
+    sp_pos = np.logaddexp(0.0, x)
+    sp_neg = np.logaddexp(0.0, -x)
+    n = x.size
+    loss = float((p * y * sp_neg + (1.0 - y) * sp_pos).sum() / n)
+    s = 1.0 / (1.0 + np.exp(-x))
+    return loss, ((p * y + 1.0 - y) * s - p * y) / n
+
+
+def model_step_grads(task, x, edge_index, layers, skips, num_heads, out_features, concat,
+                     add_skip, labels, rows, coef):
+    """One task module's training-step loss and gradients in fp64 (no dropout):
+    * "planetoid": PlanetoidGAT.training_step (`models/planetoid_gat.py:15-30`) = CE(out[rows],
+      y[rows]) + coef * calc_attention_norm;
+    * "ppi": PPI_GAT.training_step (`models/ppi_gat.py:15-33`) = BCEWithLogits(out, y), plus
+      coef * calc_attention_norm only when coef != 0 (`:28-29`);
+    * "pattern": PatternGAT.training_step (`models/pattern_gat.py:18-25`) = BCEWithLogits(
+      squeeze(out), y, pos_weight = 1 / 0.1765).
+    Returns (loss, grads) with grads as gat_model_forward_backward's."""
+    out, ei2, alphas = gat_model_forward(x, edge_index, layers, skips, num_heads, out_features,
+                                         concat, add_skip, dtype=np.float64)
+    if task == "planetoid":
+        loss, g_out = cross_entropy_grad(out, labels, rows)
+    elif task == "ppi":
+        loss, g_out = bce_logits_grad(out, labels)
+    else:
+        loss, g = bce_logits_grad(out[:, 0], labels, pos_weight=1 / 0.1765)
+        g_out = g[:, None]
+    g_al = None
+    if coef != 0.0 and task != "pattern":
+        loss = loss + coef * calc_attention_norm(ei2, alphas)
+        g_al = [coef * g for g in calc_attention_norm_grad(ei2, alphas)]
+    _, grads = gat_model_forward_backward(x, edge_index, layers, skips, num_heads, out_features,
+                                          concat, add_skip, g_out, g_alphas=g_al)
+    return loss, grads

@@ -6,6 +6,7 @@ box; the fixtures it writes are data (inputs that are too big to store are regen
 splitmix64 seeds by gatx.data; expected outputs and gradients are stored).
 
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py
+    (--steps: only the round-5 training-step goldens, step_cases)
 
 For each case: build inputs, run `GATLayer.forward(x, edge_index, return_attention_weights=True)`
 in fp32 (torch CPU), then backprop loss = <out, g_out> + <alpha, g_alpha> with torch autograd and
@@ -375,7 +376,115 @@ def ppi_full_cases():
                        gdata.xavier_uniform(23, NH, NH * 2 * F), gen=g, wgen=[22, 23])
 
 
-if __name__ == "__main__" and "--planetoid" in sys.argv:
+def ref_attention_norm_graph(edge_index, att_list):
+    """GATModel.calc_attention_norm (`models/GATModel.py:189-230`, logging removed) on the
+    reference's own helpers, kept in the autograd graph of the alphas (a training step's loss)."""
+    nb = edge_index[1]
+    first = att_list[0]
+    degrees = sum_over_neighbourhood(torch.ones_like(first[:, 0]), neighbourhood_indices=nb,
+                                     aggregated_shape=first[:, 0].size(), broadcast_back=True)
+    norm = torch.tensor(0.0)
+    for a in att_list:
+        tmp = explicit_broadcast(degrees, a)
+        norm = norm + torch.norm(a * tmp - 1.0, p=1) / nb.size(0)
+    return norm / torch.tensor(len(att_list))
+
+
+def step_labels(task, N, C):
+    """The synthetic labels of the step goldens (regenerated by tests/golden_io.step_labels)."""
+    if task == "planetoid":
+        return (gdata.randint(123, N, 1 << 30) % C).astype(np.int64), np.arange(20 * C)
+    if task == "ppi":
+        return gdata.randint(124, N * C, 2).reshape(N, C).astype(np.float32), None
+    return gdata.randint(125, N, 2).astype(np.float32), None      # PATTERN: one logit per node
+
+
+def step_case(name, base, variants):
+    """Round-5: a whole task-module TRAINING STEP through reference GATLayers
+    under autograd, wired as GATModel.forward_and_return_attention (`models/GATModel.py:153-187`;
+    `forward`, `:120-151`, for PATTERN: the same layers and skips), with the task's loss:
+    * PlanetoidGAT.training_step (`models/planetoid_gat.py:15-30`): CrossEntropy over the train
+      rows + attention_reward x calc_attention_norm;
+    * PPI_GAT.training_step (`models/ppi_gat.py:15-33`): BCEWithLogits (mean) + the norm x
+      attention_penalty, added only when the penalty is non-zero;
+    * PatternGAT.training_step (`models/pattern_gat.py:18-25`): squeeze, BCEWithLogits with
+      pos_weight 1 / 0.1765.
+    Model dropout is 0 (the Planetoid configs' 0.6 draws torch's RNG, which no kernel can
+    reproduce; the layer goldens pin the dropout path with an injected mask). `base` names the
+    model golden whose inputs and weights the step uses; stored per variant (the reward /
+    penalty): the loss and the gradients of every W, a and Linear skip weight."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from golden_io import load_model_case
+    c = load_model_case(base)
+    cfg = c["cfg"]
+    ds = c["meta"]["dataset"]
+    task = {"PPI": "ppi", "PATTERN": "pattern"}.get(ds, "planetoid")
+    heads = [1] + cfg["num_heads_per_layer"]
+    widths = cfg["head_output_features_per_layer"]
+    concat = cfg["heads_concat_per_layer"]
+    add_skip = cfg["add_skip_connection"]
+    L = cfg["num_layers"]
+    N, C = c["x"].shape[0], cfg["num_classes"]
+    y, rows = step_labels(task, N, C)
+    store = {"meta": np.array(json.dumps(dict(kind="step", base=base, task=task,
+                                              variants=list(variants))))}
+    for vi, coef in enumerate(variants):
+        mods = [ref_layer(heads[i] * widths[i], widths[i + 1], heads[i + 1], concat[i], W, a)
+                for i, (W, a) in enumerate(c["layers"])]
+        skips = [None if s is None else torch.from_numpy(s).requires_grad_(True)
+                 for s in c["skips"]]
+        xt = torch.from_numpy(c["x"])
+        edge_index = torch.from_numpy(c["edge_index"])
+        atts, sk = [], 0
+        for i in range(L):
+            layer_input = xt
+            xt, (edge_index, att) = mods[i](xt, edge_index, return_attention_weights=True)
+            atts.append(att)
+            if add_skip[i]:
+                Ws = skips[sk]
+                sk += 1
+                so = layer_input if Ws is None else layer_input @ Ws.T
+                if concat[i]:
+                    xt = xt + so
+                else:
+                    xt = xt + so.view(-1, heads[i + 1], widths[i + 1]).mean(dim=1)
+            if i != L - 1:
+                xt = torch.nn.functional.elu(xt)
+        if task == "planetoid":
+            idx = torch.from_numpy(rows)
+            loss = torch.nn.CrossEntropyLoss(reduction="mean")(
+                xt[idx], torch.from_numpy(y)[idx]) + coef * ref_attention_norm_graph(edge_index,
+                                                                                     atts)
+        elif task == "ppi":
+            loss = torch.nn.BCEWithLogitsLoss(reduction="mean")(xt, torch.from_numpy(y))
+            if coef != 0.0:
+                loss = loss + coef * ref_attention_norm_graph(edge_index, atts)
+        else:
+            loss = torch.nn.BCEWithLogitsLoss(reduction="mean", pos_weight=torch.tensor(
+                [1 / 0.1765]))(torch.squeeze(xt), torch.from_numpy(y))
+        loss.backward()
+        store[f"v{vi}_loss"] = np.array(loss.item(), dtype=np.float64)
+        for i, m in enumerate(mods):
+            put(store, f"v{vi}_grad_W{i}", m.W.weight.grad.numpy())
+            put(store, f"v{vi}_grad_a{i}", m.a.weight.grad.numpy())
+        for j, s in enumerate(skips):
+            if s is not None:
+                put(store, f"v{vi}_grad_skip{j}", s.grad.numpy())
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **store)
+    print(f"{name}: task={task} N={N} variants={variants}")
+
+
+def step_cases():
+    for ds in ("cora", "citeseer", "pubmed"):
+        step_case(f"{ds}_step_trained", f"{ds}_model_trained", [0.0, -0.5])
+    step_case("ppi_step_small", "ppi_model_small", [0.0, 0.5])
+    step_case("pattern_step_trained", "pattern_model_trained", [0.0])
+
+
+if __name__ == "__main__" and "--steps" in sys.argv:
+    torch.set_num_threads(8)
+    step_cases()
+elif __name__ == "__main__" and "--planetoid" in sys.argv:
     torch.set_num_threads(8)
     planetoid_model_cases()
 elif __name__ == "__main__":

@@ -12,7 +12,8 @@ from gatx import data as gdata
 
 GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 LAYER_CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz"))
-                     if "_model_" not in os.path.basename(p))
+                     if "_model_" not in os.path.basename(p)
+                     and "_step_" not in os.path.basename(p))
 MODEL_CASES = ["pattern_model_trained", "ppi_model_small", "cora_model_trained",
                "citeseer_model_trained", "pubmed_model_trained"]
 
@@ -125,3 +126,38 @@ def load_model_case(name):
         exp["attention_norm"] = float(z["attention_norm"])
     return dict(meta=meta, cfg=cfg, x=x, edge_index=ei, layers=layers, skips=skips,
                 expected=exp, edge_index_out=z["edge_index_out"])
+
+
+STEP_CASES = ["cora_step_trained", "citeseer_step_trained", "pubmed_step_trained",
+              "ppi_step_small", "pattern_step_trained"]
+
+
+def step_labels(task, N, C):
+    """The synthetic labels make_goldens.step_labels drew (targets, labelled rows or None)."""
+    if task == "planetoid":
+        return (gdata.randint(123, N, 1 << 30) % C).astype(np.int64), np.arange(20 * C)
+    if task == "ppi":
+        return gdata.randint(124, N * C, 2).reshape(N, C).astype(np.float32), None
+    return gdata.randint(125, N, 2).astype(np.float32), None
+
+
+def load_step_case(name):
+    """A training-step golden (make_goldens.step_case): the base model case's inputs and weights,
+    the task's labels, and per variant (reward / penalty) the reference's loss and gradients."""
+    z = np.load(os.path.join(GOLDEN_DIR, f"{name}.npz"))
+    meta = json.loads(str(z["meta"]))
+    c = load_model_case(meta["base"])
+    cfg = c["cfg"]
+    N = c["x"].shape[0]
+    labels, rows = step_labels(meta["task"], N, cfg["num_classes"])
+    variants = []
+    for vi, coef in enumerate(meta["variants"]):
+        exp = {"loss": float(z[f"v{vi}_loss"])}
+        for i in range(cfg["num_layers"]):
+            exp[f"W{i}"] = Expected(z, f"v{vi}_grad_W{i}")
+            exp[f"a{i}"] = Expected(z, f"v{vi}_grad_a{i}")
+        for j in range(len(c["skips"])):
+            if f"v{vi}_grad_skip{j}" in z or f"v{vi}_grad_skip{j}__rows" in z:
+                exp[f"skip{j}"] = Expected(z, f"v{vi}_grad_skip{j}")
+        variants.append((coef, exp))
+    return dict(c, task=meta["task"], labels=labels, rows=rows, variants=variants)

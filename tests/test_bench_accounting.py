@@ -260,3 +260,43 @@ def test_train_edge_passes_priced_against_the_l2_gather_rate():
     assert abs(g["achieved"] - round(b / (2 * 0.3e-3) / 1e12, 2)) < 0.011
     assert "l2_gather" in objs["edge_forward"]
     assert "l2_gather" not in objs["bwd_gemm_gw"]
+
+
+def test_headline_forward_writes_alpha():
+    """the headline `value` is the reference's forward, which writes alpha in
+    every layer (`models/gat_layer.py:106-110`). gatx's lazy alpha is opt-in (off by default),
+    bench.py times the headline with the default, and the forward's priced dataflow holds one
+    alpha pass per layer. The deferred time is only an extra key."""
+    import inspect
+    import gatx
+    assert gatx.GATLayer.lazy_alpha is False
+    src = inspect.getsource(bench.main)
+    head = src[:src.index("alpha_deferred_ms = None")]
+    assert "lazy_alpha = True" not in head    # nothing before the headline timing turns it on
+    assert "_GL.lazy_alpha = False" in src    # the extra timing turns it off again
+    assert '"value": round(value, 1)' in src and "value = layer_edges * world / step_s" in src
+    for d in bench.layer_dims(gatx.config.data_config["PPI"]):
+        flow = bench.layer_dataflow(N_PPI, E2_PPI, *d, False)
+        assert [k for k, _, _ in flow].count("attention_alpha") == 1
+
+
+def test_bench_dry_run_launches_8_ranks():
+    """the driver's 8-GPU command form (`python bench.py --gpus 8`, one
+    process) rehearsed on the CPU: the parent starts 8 ranks under torch.distributed.run before
+    touching any GPU, each joins the group (gloo here) and times the steps with the barrier +
+    max-over-ranks protocol, and only rank 0 prints the JSON line."""
+    import json
+    import subprocess
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8",
+                        "--dry-run", "--steps", "3", "--warmup", "1"], capture_output=True,
+                       text=True, env=env, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["dry_run"] and d["steps"] == 3
+    assert sorted(r for r, _ in d["ranks"]) == list(range(8))
+    assert sorted(lr for _, lr in d["ranks"]) == list(range(8))

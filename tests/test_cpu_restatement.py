@@ -41,3 +41,27 @@ def test_restatement_matches_oracle(ds, G):
     assert np.abs(out.numpy() - r_out).max() <= 1e-4 * scale
     for a, r in zip(al, r_al):
         assert np.abs(a.numpy() - r).max() <= 1e-5
+
+
+def test_factorised_logits_equal_materialised():
+    """torch_dataflow's factorised logits (s_src[src] + s_dst[dst], used by the full-size
+    gradient parity test to keep autograd's saved tensors small) equal the reference's
+    materialised (E', NH, 2F) . a^T form, forward and gradients, in fp64."""
+    import torch
+    from oracle import torch_dataflow as td
+    g = torch.Generator().manual_seed(4)
+    N, E, fin, NH, F = 40, 300, 7, 3, 5
+    ei = torch.randint(0, N, (2, E), generator=g)
+    outs = []
+    for fact in (False, True):
+        x = torch.randn(N, fin, generator=torch.Generator().manual_seed(1),
+                        dtype=torch.float64).requires_grad_(True)
+        W = torch.randn(NH * F, fin, generator=torch.Generator().manual_seed(2),
+                        dtype=torch.float64).requires_grad_(True)
+        a = torch.randn(NH, NH * 2 * F, generator=torch.Generator().manual_seed(3),
+                        dtype=torch.float64).requires_grad_(True)
+        out, _, al = td.layer_forward(x, ei, W, a, NH, F, True, factorised=fact)
+        (out.sin().sum() + (al * al).sum()).backward()
+        outs.append((out.detach(), al.detach(), x.grad, W.grad, a.grad))
+    for u, v in zip(*outs):
+        assert float((u - v).abs().max()) <= 1e-12 * max(1.0, float(u.abs().max()))

@@ -356,3 +356,102 @@ def test_no_sync_only_gradient_is_reduced_world2():
     ref = torch.cat([p.grad.reshape(-1) for p in model.parameters()])
     for r in range(world):
         assert torch.allclose(out[r], ref, atol=1e-5), (r, (out[r] - ref).abs().max())
+
+
+# ---------------------------------------------------------------------------------------------
+# BASELINE config 4 at 8 ranks: PatternGAT's step (`models/pattern_gat.py:
+# 18-25`, batch sharded over the graph axis, `run_config.py:46`) on the reference dataflow
+# restated in torch (oracle/torch_dataflow.py, CPU; the HIP layer has no CPU path), through the
+# production sharding (shard_graphs / collate_graphs), count_weights and the overlapped
+# GradientAllReducer over gloo: every rank's reduced gradient equals one process's gradient on
+# the union batch.
+
+def _pattern_params():
+    from gatx.config import data_config
+    cfg = data_config["PATTERN"]
+    heads = [1] + cfg["num_heads_per_layer"]
+    widths = cfg["head_output_features_per_layer"]
+    torch.manual_seed(0)
+    params = torch.nn.ParameterList()
+    for i in range(cfg["num_layers"]):
+        fin, F, NH = heads[i] * widths[i], widths[i + 1], heads[i + 1]
+        W = torch.empty(NH * F, fin)
+        a = torch.empty(NH, NH * 2 * F)
+        s = torch.empty(NH * F, fin)
+        for t in (W, a, s):
+            torch.nn.init.xavier_uniform_(t)
+        params.extend([torch.nn.Parameter(W), torch.nn.Parameter(a), torch.nn.Parameter(s)])
+    return cfg, params
+
+
+def _pattern_graphs(num_graphs):
+    from gatx import data as gd
+    b = gd.dataset_batch("PATTERN", num_graphs, graph_seed=271, feature_seed=16)
+    y = (gd.uniform01(28, b.num_nodes) < 0.1765).astype("float32")
+    out = []
+    for g in range(num_graphs):
+        n0, n1 = int(b.node_offsets[g]), int(b.node_offsets[g + 1])
+        m = (b.edge_index[1] >= n0) & (b.edge_index[1] < n1)
+        out.append((torch.from_numpy(b.x[n0:n1]), torch.from_numpy(b.edge_index[:, m] - n0),
+                    torch.from_numpy(y[n0:n1])))
+    return out
+
+
+def _pattern_loss(cfg, params, x, ei, y, w_nodes=1.0, w_edges=1.0):
+    from oracle import torch_dataflow as td
+    L = cfg["num_layers"]
+    layers = [(params[3 * i], params[3 * i + 1]) for i in range(L)]
+    skips = [params[3 * i + 2] for i in range(L)]
+    out, ei2, alphas = td.model_forward(x, ei, layers, skips, cfg["num_heads_per_layer"],
+                                        cfg["head_output_features_per_layer"][1:],
+                                        cfg["heads_concat_per_layer"],
+                                        cfg["add_skip_connection"])
+    bce = torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([1 / 0.1765]))(out.squeeze(-1), y)
+    # + the attention-norm term (PPI_GAT's attention_penalty form, a per-edge mean), weighted by
+    # the rank's share of the union batch's E'
+    return bce * w_nodes + 0.5 * td.attention_norm(ei2, alphas) * w_edges, ei2.size(1)
+
+
+def _pattern_world_worker(rank, world, port, num_graphs, out):
+    from gatx.distributed import GradientAllReducer, collate_graphs, count_weights, shard_graphs
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg, params = _pattern_params()
+    reducer = GradientAllReducer(params, bucket_bytes=16 << 10, average=False)
+    graphs = _pattern_graphs(num_graphs)
+    mine = shard_graphs(num_graphs, rank, world)
+    x, ei, y, _ = collate_graphs([graphs[i] for i in mine])
+    from oracle import torch_dataflow as td
+    e_local = td.self_loop_rewrite(ei).size(1)
+    w_n, w_e = count_weights([x.size(0), e_local])
+    loss, _ = _pattern_loss(cfg, params, x, ei, y, w_n, w_e)
+    loss.backward()
+    reducer.finish()
+    out[rank] = (len(mine), torch.cat([p.grad.reshape(-1) for p in params]).clone())
+    reducer.remove()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("num_graphs", [32, 37])
+def test_pattern_sharded_world8_equals_union_batch(num_graphs):
+    """32 graphs = 4 per rank (the notebook's PATTERN batch, ipynb:690, over 8 GPUs); 37 graphs
+    = uneven 5/5/5/5/5/4/4/4 shards."""
+    world = 8
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_pattern_world_worker, args=(world, _free_port(), num_graphs, out), nprocs=world,
+             join=True)
+    from gatx.distributed import collate_graphs
+    cfg, params = _pattern_params()
+    x, ei, y, _ = collate_graphs(_pattern_graphs(num_graphs))
+    loss, _ = _pattern_loss(cfg, params, x, ei, y)
+    loss.backward()
+    ref = torch.cat([p.grad.reshape(-1) for p in params])
+    sizes = sorted(out[r][0] for r in range(world))
+    assert sum(sizes) == num_graphs and sizes[-1] - sizes[0] <= 1
+    for r in range(world):
+        got = out[r][1]
+        assert torch.allclose(got, ref, rtol=1e-4, atol=1e-6), (r, (got - ref).abs().max())

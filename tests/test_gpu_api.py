@@ -79,13 +79,15 @@ def test_weight_update_through_data_is_seen(device):
 
 @pytest.mark.parametrize("shape", [(4, 8, 24, True), (4, 8, 24, False), (4, 16, 8, True)])
 def test_inference_alpha_on_read(shape, device):
-    """An inference forward without return_attention_weights defers the alpha pass until
+    """With `lazy_alpha` set, an inference forward without return_attention_weights defers the
+    alpha pass until
     `normalised_attention_coeffs` is read (`models/gat_layer.py:110` stores alpha in every
     forward): the value read is bitwise the eager forward's alpha and matches the oracle, for
     the plain and the reassociated (narrow input) dataflows; a later forward replaces it."""
     NH, F, fin, concat = shape
     b, W, a, _, _ = _small_case(seed=5, fin=fin, NH=NH, F=F)
     layer = _layer(device, W, a, NH, F, concat).eval()
+    layer.lazy_alpha = True
     x = torch.from_numpy(b.x).to(device)
     ei = torch.from_numpy(b.edge_index).to(device)
     _, r_ei, r_alpha, _ = orc.gat_layer_forward(b.x, b.edge_index, W, a, NH, F, concat)
@@ -110,6 +112,7 @@ def test_inference_alpha_read_on_another_stream(device):
     NH, F, fin = 4, 8, 24
     b, W, a, _, _ = _small_case(seed=6, fin=fin, NH=NH, F=F)
     layer = _layer(device, W, a, NH, F, True).eval()
+    layer.lazy_alpha = True
     x = torch.from_numpy(b.x).to(device)
     ei = torch.from_numpy(b.edge_index).to(device)
     with torch.no_grad():

@@ -3,7 +3,8 @@ produced by importing /root/reference/models/gat_layer.py — see tests/golden/m
 import numpy as np
 import pytest
 
-from golden_io import LAYER_CASES, MODEL_CASES, grad_seeds, load_layer_case, load_model_case
+from golden_io import (LAYER_CASES, MODEL_CASES, STEP_CASES, grad_seeds, load_layer_case,
+                       load_model_case, load_step_case)
 from oracle import gat_oracle as orc
 
 OUT_TOL = 1e-4          # outputs / alpha: absolute (north_star: within 1e-4 fp32)
@@ -186,3 +187,27 @@ def test_oracle_planetoid_step_finite_differences():
                 arr[idx] = old
                 fd = (lp - lm) / (2 * eps)
                 assert abs(fd - grads[k][li][idx]) <= 1e-5 * max(1.0, abs(fd)), (li, k, idx, fd)
+
+
+@pytest.mark.parametrize("name", STEP_CASES)
+def test_oracle_step_matches_reference(name):
+    """the oracle's whole training step (model_step_grads: the task module's
+    loss through the GATModel wiring and every layer's backward, in fp64) against the reference's
+    own autograd (tests/golden/*_step_*.npz: reference GATLayers wired as GATModel, the task
+    module's loss, `loss.backward()`), for every variant (attention reward / penalty). Model-level
+    tolerance: 2e-4 of the gradient's scale (the reference's fp32 noise grows with depth)."""
+    c = load_step_case(name)
+    cfg = c["cfg"]
+    for coef, exp in c["variants"]:
+        loss, grads = orc.model_step_grads(
+            c["task"], c["x"], c["edge_index"], c["layers"], c["skips"],
+            cfg["num_heads_per_layer"], cfg["head_output_features_per_layer"][1:],
+            cfg["heads_concat_per_layer"], cfg["add_skip_connection"], c["labels"], c["rows"],
+            coef)
+        assert abs(loss - exp["loss"]) <= 1e-5 * max(1.0, abs(exp["loss"])), (coef, loss)
+        for i in range(cfg["num_layers"]):
+            exp[f"W{i}"].check(grads["W"][i], 2e-4, rtol_scale=True, what=f"{coef} ")
+            exp[f"a{i}"].check(grads["a"][i], 2e-4, rtol_scale=True, what=f"{coef} ")
+        for j, g in enumerate(grads["skip"]):
+            if f"skip{j}" in exp:
+                exp[f"skip{j}"].check(g, 2e-4, rtol_scale=True, what=f"{coef} ")
