@@ -74,7 +74,8 @@ def gemm_roof():
     from gatx import _lib
     mode = _lib.lib.gatx_get_gemm_mode()
     if mode == 2:
-        f16p = os.environ.get("GATX_F16P", "1") != "0"
+        from gatx import tuning
+        f16p = tuning.get("f16p") != 0
         return dict(mode="f16x3", peak=BF16_MFMA_PEAK_TFS / F16X3_PRODUCTS,
                     prefix=("gemm_f16p_kernel<16, 0", "gemm_f16p_kernel<32, 0",
                             "gemm_x3_kernel<true, true, true, 0,"),
@@ -204,7 +205,8 @@ def layer_dataflow(N, E2, F_in, NH, F, concat, resid, alpha=True, gather_rows=No
     it does not run it. gather_rows: the gathered-row count beyond the MALL when known
     (distinct_sources_per_chunk: a source's row is read once per node chunk that gathers it, not
     once per edge). Returns [(kernel, bytes, flops)]."""
-    from gatx.functional import LayerShape, _env_int, fold_scores_into_gemm, use_reassociation
+    from gatx import tuning
+    from gatx.functional import LayerShape, fold_scores_into_gemm, use_reassociation
     sh = LayerShape(NH, F, F_in, concat, False)
     H2, Fp, Dp = 2 * NH, sh.Fp, sh.Dp
     oc = sh.out_cols
@@ -227,7 +229,7 @@ def layer_dataflow(N, E2, F_in, NH, F, concat, resid, alpha=True, gather_rows=No
     if fold_scores_into_gemm(sh):
         out.append(("gemm", 4 * (N * F_in + (Dp + H2) * F_in + N * Dp + N * H2),
                     2 * N * F_in * (NH * F + H2)))
-    elif _env_int("GATX_FUSED_SCORES", 1):
+    elif tuning.get("fused_scores"):
         # S reduced from the accumulators in the GEMM epilogue (gatx_projection_gemm_scores): no
         # second read of Wh; flops counted as the 2NH extra columns of x W_aug^T
         out.append(("gemm", 4 * (N * F_in + (Dp + H2) * F_in + N * Dp + N * H2),
@@ -720,8 +722,8 @@ def run_rmat(args, world, rank, dev):
     # gathered Wh rows (20 GB of them, far beyond the MALL): a source's row comes from HBM once
     # per destination chunk that gathers it (R-MAT hubs are gathered by almost every chunk, but
     # re-read within one only from L2), not once per edge
-    from gatx.functional import _env_int
-    chunk = _env_int("GATX_EDGE_CHUNK", 2048)
+    from gatx import tuning
+    chunk = tuning.get("edge_chunk")
     g_rows = distinct_sources_per_chunk(graph_cache.get(ei, N, True), chunk)
     flow = layer_dataflow(N, E2, FIN, NH, F, True, False, gather_rows=g_rows)
     uniq = sum(b for _, b, _ in flow) + graph_build_bytes(E, E2, N)
@@ -747,7 +749,7 @@ def run_rmat(args, world, rank, dev):
                    "gathered_rows_per_layer": g_rows,
                    "gather_model": f"a source row once per {chunk}-destination chunk that "
                                    "gathers it (distinct_sources_per_chunk), not once per edge",
-                   "hub_split_backward": train and os.environ.get("GATX_BWD_HUBS") != "0",
+                   "hub_split_backward": train and tuning.get("bwd_hubs") != 0,
                    "nodes": N, "edges_in": int(ei.size(1)), "edges_per_layer": E2,
                    "parallelism": "replicas" if world > 1 else "single GPU"},
         "unique_GBps": round(uniq / step_s / 1e9, 1),
@@ -761,6 +763,7 @@ def run_rmat(args, world, rank, dev):
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not train:
         result["cpu_baseline"] = cpu_baseline_rmat(layer.W.weight.detach().cpu().numpy(),
                                                    layer.a.weight.detach().cpu().numpy(), NH, F)
+    result["config"]["tuning"] = tuning_changes()
     if rank == 0:
         print(json.dumps(result), flush=True)
 
@@ -790,6 +793,13 @@ def launch_ranks(nproc: int, argv) -> int:
         print(f"bench.py: {nproc}-rank run failed with exit status {proc.returncode}",
               file=sys.stderr)
     return proc.returncode
+
+
+def tuning_changes() -> dict:
+    """The gatx.tuning switches this run set away from their defaults (--tune)."""
+    from gatx import tuning
+    cur = tuning.current()
+    return {k: v for k, v in cur.items() if v != tuning.DEFAULTS[k]}
 
 
 def dry_run(args, world: int, rank: int, local: int) -> int:
@@ -854,6 +864,9 @@ def main():
                     help="gatx: skip / ELU / dropout fused into the layers; reference: the "
                          "reference GATModel.forward op for op around gatx GATLayers (the "
                          "INTEGRATION.md drop-in)")
+    ap.add_argument("--tune", action="append", default=[], metavar="SWITCH=VALUE",
+                    help="set a gatx.tuning switch for this run (A/B measurements; repeatable); "
+                         "the line's config.tuning lists every switch that differs from default")
     ap.add_argument("--dry-run", action="store_true",
                     help="exercise the launch path only: --gpus N starts N ranks, each joins a "
                          "gloo group and runs the barrier / max-over-ranks timing around an empty "
@@ -872,6 +885,8 @@ def main():
     # one-GPU box): GATX_BENCH_BACKEND=gloo, GATX_BENCH_ONE_DEVICE=1 (every rank on cuda:0).
     if args.dry_run:
         sys.exit(dry_run(args, world, rank, local))
+    from gatx import tuning
+    tuning.set(**tuning.parse(args.tune))
     one_device = os.environ.get("GATX_BENCH_ONE_DEVICE") == "1"
     dev_idx = 0 if one_device else local
     backend = os.environ.get("GATX_BENCH_BACKEND", "nccl")
@@ -1125,6 +1140,7 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.mode == "fwd":
         result["cpu_baseline"] = cpu_baseline(model, cfg, ds, 8 if ds == "PATTERN" else 1)
+    result["config"]["tuning"] = tuning_changes()
     if rank == 0:
         print(json.dumps(result), flush=True)
     if reducer is not None:

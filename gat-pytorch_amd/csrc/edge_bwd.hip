@@ -1185,13 +1185,9 @@ extern "C" int gatx_edge_backward_src_hubs(const float* S, const uint32_t* M_ord
   a.chunk = kChunk;
   GATX_REQUIRE(set_hubs(a, hub_edges, hubs, hub_count, hub_bound, hub_part),
                "edge_backward_src: hub splitting needs its plan and partial buffer");
-  static const bool per_head = [] {   // A/B switch: GATX_SRC_MEAN=0 keeps per-head items
-    const char* e = getenv("GATX_SRC_MEAN");
-    return e && e[0] == '0';
-  }();
   // head-mean: one item per source, all heads (hub-split graphs take the per-head items, which
   // also serve head-mean layers: go_head4 = 0)
-  if (!concat && NH <= 8 && !per_head && a.hub_T == 0) {
+  if (!concat && NH <= 8 && a.hub_T == 0) {
     const unsigned grid = (unsigned)ceil_div(N, 4);
     GATX_DISPATCH_HEAD(gm, edge_bwd_src_mean_kernel, grid, a);
     GATX_LAUNCH_CHECK("edge_bwd_src_mean");

@@ -1484,11 +1484,7 @@ extern "C" int gatx_edge_forward_skip(
   GATX_REQUIRE(blocks < (1ll << 31), "edge_forward: too many work items");
   const unsigned grid = (unsigned)blocks;
   // rows shared by every head (the reassociated first layer): one lane per chunk for all heads
-  static const bool shared_on = [] {   // A/B switch: GATX_SHARED_ROWS=0 keeps the generic kernel
-    const char* e = getenv("GATX_SHARED_ROWS");
-    return !(e && e[0] == '0');
-  }();
-  if (shared_on && head_stride == 0 && concat && !resid && !elu && !bias && out_p == 0.f &&
+  if (head_stride == 0 && concat && !resid && !elu && !bias && out_p == 0.f &&
       Fp / 4 <= 64 && (HS == 1 || HS == 2 || HS == 4 || HS == 8)) {
     int lpe = 1;
     while (lpe < Fp / 4) lpe <<= 1;

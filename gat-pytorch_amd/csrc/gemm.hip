@@ -410,41 +410,17 @@ __global__ void __launch_bounds__(64 * WGM * WGN, MINB) gemm_f32_kernel(GemmArgs
   write_tile<MB, NB, BM, BN, false>(g, acc, tail_z, tail_ti, m0, n0, wm, wn, lane);
 }
 
-// GEMM arithmetic, env GATX_GEMM (or gatx_set_gemm_mode): "f16x3" (default) = the split-fp16
+// GEMM arithmetic, gatx_set_gemm_mode (never the environment): 2 "f16x3" (default) = the split-fp16
 // kernel of gemm_x3.hip (3 fp16 MFMA products; tiles outside its operand range fall back to the
-// bf16 split in-kernel), "x3" = the split-bf16 kernel (6 bf16 products), "f32" =
+// bf16 split in-kernel), 1 "x3" = the split-bf16 kernel (6 bf16 products), 0 "f32" =
 // v_mfma_f32_32x32x2_f32.
-int g_gemm_mode = -1;   // -1: read the environment on first use; 0: f32; 1: x3; 2: f16x3
-int gemm_mode() {
-  if (g_gemm_mode < 0) {
-    const char* e = getenv("GATX_GEMM");
-    g_gemm_mode = !e ? 2 : strcmp(e, "f32") == 0 ? 0 : strcmp(e, "x3") == 0 ? 1 : 2;
-  }
-  return g_gemm_mode;
-}
+int g_gemm_mode = 2;
+int gemm_mode() { return g_gemm_mode; }
 
-// K-tile depth / occupancy of the GEMM kernel, env GATX_GEMM_BK (tuning only): 17 (default) =
-// BK 16 at 4 workgroups per CU (LDS 4 x 40 KB, <= 128 VGPRs), 16 = BK 16 at 3, 32 = BK 32 at 2,
-// 64 = BK 64 at 1. Measured on the PPI shapes: 118 / 115 / 111 / 93 TF (occupancy hides the
-// barrier and LDS latency that one K-tile of MFMAs cannot). 8-wave workgroups with 32 x 64 wave
-// tiles (84 VGPRs, 2 workgroups per CU) measured 113 TF, no better; the template keeps WGM x WGN.
-int gemm_variant() {
-  static const int v = [] {
-    const char* e = getenv("GATX_GEMM_BK");
-    const int x = e ? atoi(e) : 17;
-    return (x == 16 || x == 32 || x == 64) ? x : 17;
-  }();
-  return v;
-}
-
-// GATX_F16P=0 (A/B tests): the in-loop split kernel even when pre-split weight planes are given
-bool f16p_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("GATX_F16P");
-    return !(e && strcmp(e, "0") == 0);
-  }();
-  return on;
-}
+// The f32-MFMA kernel's K-tile depth / occupancy: BK 16 at 4 workgroups per CU (LDS 4 x 40 KB,
+// <= 128 VGPRs). Measured on the PPI shapes (round 1): BK 64 / 1 WG 93 TF, BK 32 / 2 WG 111, BK 16
+// / 3 WG 115, BK 16 / 4 WG 118 (occupancy hides the barrier and LDS latency that one K-tile of
+// MFMAs cannot); 8-wave workgroups with 32 x 64 wave tiles 113 TF. Only the last is built.
 
 // The pre-split kernel, then the tail fix-up of its partial last wave (as launch_gemm).
 int launch_f16p_and_fixups(const GemmArgs& g, int tag, hipStream_t stream) {
@@ -477,17 +453,10 @@ int launch_gemm(const GemmArgs& g0, bool a_kc, bool b_kc, int batch, hipStream_t
   GATX_REQUIRE(tiles < (1ll << 31) && batch < 65536, "gemm: too many tiles");
   const int64_t gx = g.tail_s > 1 ? g.dp_blocks + g.tail_rem * g.tail_s : tiles;
   dim3 grid((unsigned)gx, (unsigned)batch, (unsigned)g.splits);
-  const int var = gemm_variant();
   if (gemm_mode() >= 1) {
     GATX_CALL(launch_gemm_x3(g, a_kc, b_kc, batch, TAG, stream));
   } else {
-#define GATX_GEMM_V(AK, BKC, V)                                                                 \
-  do {                                                                                         \
-    if (var == 16) gemm_f32_kernel<AK, BKC, V, TAG, 16, 3, 2, 2><<<grid, 256, 0, stream>>>(g);  \
-    else if (var == 17) gemm_f32_kernel<AK, BKC, V, TAG, 16, 4, 2, 2><<<grid, 256, 0, stream>>>(g); \
-    else if (var == 64) gemm_f32_kernel<AK, BKC, V, TAG, 64, 1, 2, 2><<<grid, 256, 0, stream>>>(g); \
-    else gemm_f32_kernel<AK, BKC, V, TAG, 32, 2, 2, 2><<<grid, 256, 0, stream>>>(g);            \
-  } while (0)
+#define GATX_GEMM_V(AK, BKC, V) gemm_f32_kernel<AK, BKC, V, TAG, 16, 4, 2, 2><<<grid, 256, 0, stream>>>(g)
 #define GATX_GEMM_GO(AK, BKC)                                                                  \
   do {                                                                                        \
     if (g.a_vec && g.b_vec) GATX_GEMM_V(AK, BKC, true);                                       \
@@ -525,19 +494,9 @@ struct Kind {
 };
 Kind choose_kind(int64_t M, int64_t N) {
   if (gemm_mode() == 0) return {0, 128, 128};
-  static const int force = [] {   // tuning only: GATX_X3_TILE=128|256
-    const char* e = getenv("GATX_X3_TILE");
-    return e ? atoi(e) : 0;
-  }();
-  if (force == 128) return {1, 128, 128};
   const int64_t small_area = round_up(M, 128) * round_up(N, 128);
   const int64_t big_area = round_up(M, 256) * round_up(N, 256);
-  static const int tol = [] {   // tuning only: GATX_X3_BIGTOL=percent padding accepted
-    const char* e = getenv("GATX_X3_BIGTOL");
-    return e ? atoi(e) : 115;
-  }();
-  if (force == 256 || (M >= 256 && N >= 256 && big_area * 100 <= small_area * tol))
-    return {2, 256, 256};
+  if (M >= 256 && N >= 256 && big_area * 100 <= small_area * 115) return {2, 256, 256};
   return {1, 128, 128};
 }
 
@@ -546,12 +505,8 @@ int64_t resident_blocks(const Kind& kd) {
   static int64_t cached[3] = {0, 0, 0};
   if (cached[kd.id]) return cached[kd.id];
   int dev = 0, cus = 0, per_cu = 0;
-  const int var = gemm_variant();
   int nt = kd.id == 2 ? 512 : 256;
-  const void* fn = reinterpret_cast<const void*>(&gemm_f32_kernel<true, true, true, 0, 32, 2, 2, 2>);
-  if (var == 16) fn = reinterpret_cast<const void*>(&gemm_f32_kernel<true, true, true, 0, 16, 3, 2, 2>);
-  if (var == 17) fn = reinterpret_cast<const void*>(&gemm_f32_kernel<true, true, true, 0, 16, 4, 2, 2>);
-  if (var == 64) fn = reinterpret_cast<const void*>(&gemm_f32_kernel<true, true, true, 0, 64, 1, 2, 2>);
+  const void* fn = reinterpret_cast<const void*>(&gemm_f32_kernel<true, true, true, 0, 16, 4, 2, 2>);
   if (kd.id >= 1) fn = gemm_x3_occupancy_fn(kd.id == 2 ? 1 : 0);
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
@@ -587,11 +542,6 @@ int choose_splits(int64_t tiles, int64_t K, int64_t slots) {
 int choose_tail_split(int64_t tiles, int64_t K, int64_t slots, const Kind& kd, int64_t& rem) {
   rem = tiles % slots;
   if (rem == 0 || tiles < 1) return 1;
-  static const int forced = [] {   // tuning only: GATX_TAIL_SPLIT=s forces s slices
-    const char* e = getenv("GATX_TAIL_SPLIT");
-    return e ? atoi(e) : 0;
-  }();
-  if (forced > 0) return (int)std::min<int64_t>(std::min(forced, 16), ceil_div(K, 2 * KSTEP));
   const double peak = kd.id == 0 ? 120e12 : 200e12;   // sustained rates, f32 vs x3
   const double wave_s = 2.0 * kd.bm * kd.bn * (double)K / (peak / (double)slots);
   int best = 1;
@@ -696,23 +646,15 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
   };
   g.a_vec = aligned(A, g.lda, a_bs);
   g.b_vec = aligned(B, g.ldb, b_bs);
-  static const bool tiny_on = [] {   // A/B switch: GATX_TINY_GEMM=0 keeps the MFMA kernels
-    const char* e = getenv("GATX_TINY_GEMM");
-    return !(e && strcmp(e, "0") == 0);
-  }();
   // (only short K and few rows: every output re-reads its A row and B column, so the VALU
   // kernel turns TA-bound — PATTERN's K = 952-node weight gradients ran 28 us vs 12 us tiled,
   // PPI's 44900 x 8 x 50 score product 26 us vs 11 us on the small-K MFMA kernel)
-  if (tiny_on && K <= 64 && M <= 16384 && M * N * K * batch <= (int64_t(1) << 25)) {
+  if (K <= 64 && M <= 16384 && M * N * K * batch <= (int64_t(1) << 25)) {
     g.splits = 1; g.tail_s = 1; g.tiles_m = g.tiles_n = 1; g.dp_blocks = g.tail_rem = 0;
     g.bm = g.bn = 32; g.tail_partial = nullptr;
     return launch_gemm_tiny(g, batch, a_kc, b_kc, stream);
   }
-  static const bool smallk_on = [] {   // A/B switch: GATX_SMALLK=0 keeps the tiled kernel
-    const char* e = getenv("GATX_SMALLK");
-    return !(e && strcmp(e, "0") == 0);
-  }();
-  if (smallk_on && gemm_mode() >= 1 && n_split >= N &&
+  if (gemm_mode() >= 1 && n_split >= N &&
       gemm_smallk_fits(M, N, K, a_kc, b_kc, accumulate, resid != nullptr)) {
     g.splits = 1; g.tail_s = 1; g.tiles_m = g.tiles_n = 1; g.dp_blocks = g.tail_rem = 0;
     g.bm = g.bn = 32; g.tail_partial = nullptr;
@@ -725,7 +667,7 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
   g.tail_partial = nullptr;
   // the weight gradient G_aug^T x with G_aug's exact column maxima: the row-contiguous f16x3
   // kernel (gemm_f16p.hip), its 256-row tiles all full (a few rows past them: the thin kernel)
-  const bool wgrad_f16 = a_rowmax && tag == 2 && gemm_mode() == 2 && f16p_enabled() &&
+  const bool wgrad_f16 = a_rowmax && tag == 2 && gemm_mode() == 2 &&
                          kd.id == 2 && batch == 1 && !a_kc && !b_kc && !accumulate;
   if (wgrad_f16 && wgrad_thin_rows(M) && g.a_vec && g.b_vec && N % 4 == 0) g.tiles_m = M / kd.bm;
   const int64_t tiles = g.tiles_m * g.tiles_n * batch;
@@ -789,7 +731,7 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
     g.s_a = sc->a; g.s_nh = sc->nh; g.s_f = sc->f; g.s_fp = (int)round_up(sc->f, 4);
     g.s_h2 = 2 * sc->nh; g.s_part = s_part;
   }
-  if (b_planes && gemm_mode() == 2 && f16p_enabled() && kd.id == 2 && batch == 1 && a_kc &&
+  if (b_planes && gemm_mode() == 2 && kd.id == 2 && batch == 1 && a_kc &&
       b_kc && g.a_vec && g.b_vec && g.splits == 1 && tag != 2 && g.lda < (1 << 20) &&
       N <= 60 * 256) {   // (the planes' header holds 60 tile flags)
     g.b_planes = (const char*)b_planes + 256;   // past the planes' header (gemm_f16p.hip)
@@ -823,7 +765,7 @@ extern "C" int gatx_gemm_layout_mode(int a_kc, int b_kc) {
   const int m = gemm_mode();
   if (m != 2) return m;
   if (a_kc && b_kc) return 2;
-  return !a_kc && !b_kc && f16p_enabled() ? 2 : 1;
+  return !a_kc && !b_kc ? 2 : 1;
 }
 
 extern "C" int gatx_gemm_fallback_read(uint64_t* dst, int reset, gatx_stream_t stream) {

@@ -89,7 +89,7 @@ struct F16pCfg {
 // Main loop over the K-tiles [kb, K) of one 256 x 256 tile. Returns true when a row of A left the
 // fp16 range (the caller recomputes the tile as x3). inv[256] (LDS, after the stages) receives
 // 1 / s_r per tile row.
-// PP (ping-pong, 16-deep K-tiles): the block's two wave groups (waves 0-3: tile rows 0-127, waves
+// Ping-pong (16-deep K-tiles; the single-phase loop measured 2-3% slower in situ): the block's two wave groups (waves 0-3: tile rows 0-127, waves
 // 4-7: rows 128-255; one wave of each per SIMD) run the loop one barrier apart, each K-tile as
 // MEM (this tile's fragments, the next tile's split + LDS stores, the loads of the one after) |
 // raw barrier | MATH (the 24 MFMAs, raised priority) | raw barrier, so one group's MFMAs overlap
@@ -99,7 +99,7 @@ struct F16pCfg {
 // wave's stores of tile i + 1 (buffer (i + 1) & 1) come after the barrier that follows every
 // wave's reads of tile i - 1; reads of tile i + 1 come after both groups' stores (each wave waits
 // for its LDS stores before every barrier). Global loads stay in flight across the barriers.
-template <int BK, int SCALE, bool PP = false>
+template <int BK, int SCALE>
 __device__ inline bool f16p_mainloop(const GemmArgs& g, const float* __restrict__ A, int64_t m0,
                                      int64_t n0, int64_t kb, int64_t K, char* smem, int wm,
                                      int wn, int lane, floatx16 (&acc)[4][2]) {
@@ -209,113 +209,64 @@ __device__ inline bool f16p_mainloop(const GemmArgs& g, const float* __restrict_
     load(1);
     mask_tail(1);
   }
-  if constexpr (PP) {
-    static_assert(BK == 16, "the ping-pong loop takes one 16-deep MFMA step per K-tile");
-    auto barrier = [] {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    };
-    barrier();               // tile 0 staged by every wave
-    if (wm == 1) barrier();  // group 1 one barrier behind
-    // one K-tile; the stage is a compile-time constant (the loop below is unrolled by two), so
-    // the fragment reads and stores take immediate LDS offsets instead of per-tile address math
-    auto step = [&](int kt, auto stage) {
-      constexpr int CS = decltype(stage)::value;
-      const char* cur = smem + CS * STAGE;
-      char* nxt = smem + (CS ^ 1) * STAGE;
-      f16x8 fa[MB][2], fb[NB][2];
+  static_assert(BK == 16, "the ping-pong loop takes one 16-deep MFMA step per K-tile");
+  auto barrier = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  barrier();               // tile 0 staged by every wave
+  if (wm == 1) barrier();  // group 1 one barrier behind
+  // one K-tile; the stage is a compile-time constant (the loop below is unrolled by two), so
+  // the fragment reads and stores take immediate LDS offsets instead of per-tile address math
+  auto step = [&](int kt, auto stage) {
+    constexpr int CS = decltype(stage)::value;
+    const char* cur = smem + CS * STAGE;
+    char* nxt = smem + (CS ^ 1) * STAGE;
+    f16x8 fa[MB][2], fb[NB][2];
 #pragma unroll
-      for (int p = 0; p < 2; ++p) {
+    for (int p = 0; p < 2; ++p) {
 #pragma unroll
-        for (int x = 0; x < MB; ++x)
-          fa[x][p] = *(const f16x8*)(cur + p * PB +
-                                     I::off(wm * (MB * 32) + x * 32 + (lane & 31), 8 * (lane >> 5)));
+      for (int x = 0; x < MB; ++x)
+        fa[x][p] = *(const f16x8*)(cur + p * PB +
+                                   I::off(wm * (MB * 32) + x * 32 + (lane & 31), 8 * (lane >> 5)));
 #pragma unroll
-        for (int x = 0; x < NB; ++x)
-          fb[x][p] = *(const f16x8*)(cur + (2 + p) * PB +
-                                     I::off(wn * (NB * 32) + x * 32 + (lane & 31), 8 * (lane >> 5)));
-      }
-      if (kt + 1 < nk) store(nxt);
-      if (kt + 2 < nk) {
-        load(kt + 2);
-        mask_tail(kt + 2);
-      }
-      barrier();
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int mi = 0; mi < MB; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < NB; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][1], fa[mi][0], acc[mi][ni], 0, 0, 0);
-#pragma unroll
-      for (int mi = 0; mi < MB; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < NB; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][0], fa[mi][1], acc[mi][ni], 0, 0, 0);
-#pragma unroll
-      for (int mi = 0; mi < MB; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < NB; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][0], fa[mi][0], acc[mi][ni], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-      barrier();
-    };
-    int kt = 0;
-    for (; kt + 1 < nk; kt += 2) {
-      step(kt, std::integral_constant<int, 0>{});
-      step(kt + 1, std::integral_constant<int, 1>{});
+      for (int x = 0; x < NB; ++x)
+        fb[x][p] = *(const f16x8*)(cur + (2 + p) * PB +
+                                   I::off(wn * (NB * 32) + x * 32 + (lane & 31), 8 * (lane >> 5)));
     }
-    if (kt < nk) step(kt, std::integral_constant<int, 0>{});
-    if (wm == 0) barrier();  // balances group 1's extra barrier
-  } else {
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const char* cur = smem + (kt & 1) * STAGE;
-    char* nxt = smem + ((kt & 1) ^ 1) * STAGE;
-#pragma unroll
-    for (int q = 0; q < BK / 16; ++q) {
-      f16x8 fa[MB][2], fb[NB][2];
-#pragma unroll
-      for (int p = 0; p < 2; ++p) {
-#pragma unroll
-        for (int x = 0; x < MB; ++x)
-          fa[x][p] = *(const f16x8*)(cur + p * PB +
-                                     I::off(wm * (MB * 32) + x * 32 + (lane & 31), 16 * q + 8 * (lane >> 5)));
-#pragma unroll
-        for (int x = 0; x < NB; ++x)
-          fb[x][p] = *(const f16x8*)(cur + (2 + p) * PB +
-                                     I::off(wn * (NB * 32) + x * 32 + (lane & 31), 16 * q + 8 * (lane >> 5)));
-      }
-      if (q == 0) {
-        // tile kt + 1 (loaded during iteration kt - 1) into the other stage, then tile kt + 2's
-        // loads, then this tile's MFMAs
-        if (kt + 1 < nk) store(nxt);
-        if (kt + 2 < nk) {
-          load(kt + 2);
-          mask_tail(kt + 2);
-        }
-      }
-      // C^T = B^T A^T (lane = output row, see write_tile_t); small terms first
-#pragma unroll
-      for (int mi = 0; mi < MB; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < NB; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][1], fa[mi][0], acc[mi][ni], 0, 0, 0);
-#pragma unroll
-      for (int mi = 0; mi < MB; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < NB; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][0], fa[mi][1], acc[mi][ni], 0, 0, 0);
-#pragma unroll
-      for (int mi = 0; mi < MB; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < NB; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][0], fa[mi][0], acc[mi][ni], 0, 0, 0);
+    if (kt + 1 < nk) store(nxt);
+    if (kt + 2 < nk) {
+      load(kt + 2);
+      mask_tail(kt + 2);
     }
-    __syncthreads();
+    barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int mi = 0; mi < MB; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NB; ++ni)
+        acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][1], fa[mi][0], acc[mi][ni], 0, 0, 0);
+#pragma unroll
+    for (int mi = 0; mi < MB; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NB; ++ni)
+        acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][0], fa[mi][1], acc[mi][ni], 0, 0, 0);
+#pragma unroll
+    for (int mi = 0; mi < MB; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NB; ++ni)
+        acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[ni][0], fa[mi][0], acc[mi][ni], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    barrier();
+  };
+  int kt = 0;
+  for (; kt + 1 < nk; kt += 2) {
+    step(kt, std::integral_constant<int, 0>{});
+    step(kt + 1, std::integral_constant<int, 1>{});
   }
-  }
+  if (kt < nk) step(kt, std::integral_constant<int, 0>{});
+  if (wm == 0) barrier();  // balances group 1's extra barrier
   // a row is out of range when its largest |Ah| = |fp16(64 s a)| is inf / nan (64 s |a| past the
   // fp16 range: |s a| > 1023) or, unless the row is zero, below 2^-3 (s |a| < 2^-9: the residual
   // plane would go subnormal)
@@ -331,7 +282,7 @@ __device__ inline bool f16p_mainloop(const GemmArgs& g, const float* __restrict_
   return bad;
 }
 
-template <int BK, int TAG, bool PP = false>
+template <int BK, int TAG>
 __global__ void __launch_bounds__(512, 1) gemm_f16p_kernel(GemmArgs g) {
   using Cf = F16pCfg<BK>;
   using C = X3Cfg<1>;
@@ -379,9 +330,9 @@ __global__ void __launch_bounds__(512, 1) gemm_f16p_kernel(GemmArgs g) {
       // gradients (TAG 1, rows ~1e-7): scaled by their exact row max when given, else by the
       // first K-tile's; activations (TAG 0) as they come
       const bool bad =
-          TAG == 0 ? f16p_mainloop<BK, 0, PP>(g, A, m0, n0, kb, K, smem, wm, wn, lane, acc)
-          : g.a_rowmax ? f16p_mainloop<BK, 2, PP>(g, A, m0, n0, kb, K, smem, wm, wn, lane, acc)
-                       : f16p_mainloop<BK, 1, PP>(g, A, m0, n0, kb, K, smem, wm, wn, lane, acc);
+          TAG == 0 ? f16p_mainloop<BK, 0>(g, A, m0, n0, kb, K, smem, wm, wn, lane, acc)
+          : g.a_rowmax ? f16p_mainloop<BK, 2>(g, A, m0, n0, kb, K, smem, wm, wn, lane, acc)
+                       : f16p_mainloop<BK, 1>(g, A, m0, n0, kb, K, smem, wm, wn, lane, acc);
       x3 = __syncthreads_or(bad);
       const float* inv = (const float*)(smem + 2 * Cf::STAGE);
       const float binv = ((const float*)hdr)[0];
@@ -994,17 +945,8 @@ int launch_gemm_f16p(const gk::GemmArgs& g, int tag, hipStream_t stream) {
   dim3 grid((unsigned)gx, 1u, (unsigned)g.splits);
   // (32-deep K-tiles measured slower in the library: they spill beside the x3 fallback, bench
   // 1.43 -> 1.61 ms, gpurun_out/r05h; lab numbers in DESIGN.md §8)
-  static const bool pp = [] {   // A/B: GATX_F16P_PP=0 keeps the single-phase loop
-    const char* e = getenv("GATX_F16P_PP");
-    return !(e && strcmp(e, "0") == 0);
-  }();
-  if (pp) {
-    if (tag == 0) gemm_f16p_kernel<16, 0, true><<<grid, 512, 0, stream>>>(g);
-    else gemm_f16p_kernel<16, 1, true><<<grid, 512, 0, stream>>>(g);
-  } else {
-    if (tag == 0) gemm_f16p_kernel<16, 0><<<grid, 512, 0, stream>>>(g);
-    else gemm_f16p_kernel<16, 1><<<grid, 512, 0, stream>>>(g);
-  }
+  if (tag == 0) gemm_f16p_kernel<16, 0><<<grid, 512, 0, stream>>>(g);
+  else gemm_f16p_kernel<16, 1><<<grid, 512, 0, stream>>>(g);
   GATX_LAUNCH_CHECK("gemm_f16p");
   return 0;
 }

@@ -702,28 +702,17 @@ int sort_pairs(const int32_t* keys_in, const int32_t* vals_in, int32_t* keys_out
     int32_t* ov = to_out ? vals_out : w.tv;
     int32_t* ov2 = v2 ? (to_out ? vals2_out : w.tv2) : nullptr;
     const int shift = ps * kRadixBits;
-    // 16-wave tiles for the 8-bit passes (A/B: GATX_RADIX_WAVES=4 keeps 4-wave tiles)
-    static const bool w16 = [] {
-      const char* e = getenv("GATX_RADIX_WAVES");
-      return !(e && strcmp(e, "4") == 0);
-    }();
-    const bool big = !wide && w16 && items >= 4;
+    // 16-wave tiles for the 8-bit passes of sorts of at least 4 items per thread
+    const bool big = !wide && items >= 4;
     if (wide) radix_hist_kernel<kWideBits><<<(unsigned)nb, 256, 0, stream>>>(ck, n, 0, items, nb, w.hist);
     else if (big) radix_hist16_kernel<<<(unsigned)nb, 1024, 0, stream>>>(ck, n, shift, items, nb, w.hist);
     else radix_hist_kernel<kRadixBits><<<(unsigned)nb, 256, 0, stream>>>(ck, n, shift, items, nb, w.hist);
     GATX_LAUNCH_CHECK("radix_hist");
-    static const bool lds_tiles = [] {   // A/B: GATX_RADIX_LDS=0 keeps the direct scatter
-      const char* e = getenv("GATX_RADIX_LDS");
-      return !(e && strcmp(e, "0") == 0);
-    }();
-    static const bool dscan_on = [] {   // A/B: GATX_RADIX_DSCAN=0 keeps rocPRIM's scan
-      const char* e = getenv("GATX_RADIX_DSCAN");
-      return !(e && strcmp(e, "0") == 0);
-    }();
-    const bool dscan = big && lds_tiles && dscan_on && nb <= 4096;
+    // per-digit scans of the block counts (one launch) up to 4096 tiles; rocPRIM's scan beyond
+    const bool dscan = big && nb <= 4096;
     // the one-pass sort: per-digit scans (4096 digits) + the digit-total scan in the scatter,
     // which also writes rowptr — three launches for the whole sort instead of five
-    const bool wscan = wide && v2 && dscan_on && nb <= 4096 && num_rows < (1 << kWideBits);
+    const bool wscan = wide && v2 && nb <= 4096 && num_rows < (1 << kWideBits);
     if (dscan || wscan) {
       radix_digit_scan_kernel<<<wscan ? (1u << kWideBits) : (unsigned)kRadix, 256, 0, stream>>>(
           w.hist, nb, w.offs, w.offs + m);
@@ -743,7 +732,7 @@ int sort_pairs(const int32_t* keys_in, const int32_t* vals_in, int32_t* keys_out
       else
         radix_scatter_lds16_kernel<false, true><<<(unsigned)nb, 1024, 0, stream>>>(
             ck, cv, n, shift, items, nb, w.offs, w.hist, ok, ov, nullptr, nullptr, w.offs + m);
-    } else if (big && lds_tiles) {
+    } else if (big) {
       if (v2)
         radix_scatter_lds16_kernel<true><<<(unsigned)nb, 1024, 0, stream>>>(
             ck, cv, n, shift, items, nb, w.offs, w.hist, ok, ov, cv2, ov2);
@@ -757,24 +746,15 @@ int sort_pairs(const int32_t* keys_in, const int32_t* vals_in, int32_t* keys_out
     } else if (v2 && wide)   // (the wide LDS tile has no room for a second value)
       radix_scatter_kernel<kWideBits, true><<<(unsigned)nb, 256, 0, stream>>>(
           ck, cv, n, 0, items, nb, w.offs, ok, ov, cv2, ov2);
-    else if (v2 && lds_tiles)
+    else if (v2)
       radix_scatter_lds_kernel<kRadixBits, true><<<(unsigned)nb, 256, 0, stream>>>(
           ck, cv, n, shift, items, nb, w.offs, w.hist, ok, ov, cv2, ov2);
-    else if (v2)
-      radix_scatter_kernel<kRadixBits, true><<<(unsigned)nb, 256, 0, stream>>>(
-          ck, cv, n, shift, items, nb, w.offs, ok, ov, cv2, ov2);
-    else if (lds_tiles && wide)
+    else if (wide)
       radix_scatter_lds_kernel<kWideBits><<<(unsigned)nb, 256, 0, stream>>>(
           ck, cv, n, 0, items, nb, w.offs, w.hist, ok, ov);
-    else if (lds_tiles)
+    else
       radix_scatter_lds_kernel<kRadixBits><<<(unsigned)nb, 256, 0, stream>>>(
           ck, cv, n, shift, items, nb, w.offs, w.hist, ok, ov);
-    else if (wide)
-      radix_scatter_kernel<kWideBits><<<(unsigned)nb, 256, 0, stream>>>(ck, cv, n, 0, items, nb,
-                                                                        w.offs, ok, ov);
-    else
-      radix_scatter_kernel<kRadixBits><<<(unsigned)nb, 256, 0, stream>>>(ck, cv, n, shift, items,
-                                                                         nb, w.offs, ok, ov);
     GATX_LAUNCH_CHECK("radix_scatter");
     ck = ok;
     cv = ov;

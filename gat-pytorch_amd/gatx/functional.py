@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import torch
 
+from . import tuning
 from ._lib import ARGMAX_CAP, call, lib, ptr, stream, version
 from .graph import Graph
 
@@ -206,8 +207,8 @@ def use_weight_planes(rows: int, k: int, m: int) -> bool:
     the f16x3 arithmetic, float4-aligned rows, and outputs big enough for its 256 x 256 tiles (the
     library makes the final choice; planes it does not use cost one small build per weight
     version; gatx_weight_planes_bytes is 0 for a weight too tall for the planes' header, which
-    then takes the in-loop split kernel). GATX_F16P=0: never build them."""
-    if _env_int("GATX_F16P", 1) == 0 or lib.gatx_get_gemm_mode() != 2:
+    then takes the in-loop split kernel). tuning f16p=0: never build them."""
+    if tuning.get("f16p") == 0 or lib.gatx_get_gemm_mode() != 2:
         return False
     return (k % 4 == 0 and rows >= 256 and m >= 256
             and lib.gatx_weight_planes_bytes(rows, k) > 0)
@@ -217,8 +218,8 @@ def use_wgrad_f16(M: int, N: int, K: int) -> bool:
     """Whether the weight gradient G_aug^T x (M = K_aug rows, N = F_in, K = nodes) takes the
     row-contiguous f16x3 kernel (gemm_f16p.hip, scales from G_aug's exact column maxima): the
     f16x3 arithmetic and an output its 256 x 256 tiles cover (the library decides finally; the
-    statistics pass is then only wasted work). GATX_F16P=0: never."""
-    if _env_int("GATX_F16P", 1) == 0 or lib.gatx_get_gemm_mode() != 2:
+    statistics pass is then only wasted work). tuning f16p=0: never."""
+    if tuning.get("f16p") == 0 or lib.gatx_get_gemm_mode() != 2:
         return False
     return M >= 256 and N >= 256 and M <= 2048 and N % 4 == 0
 
@@ -261,24 +262,6 @@ def _attention_alpha(graph: Graph, S, M_ord, den, sh: "LayerShape", alpha, argma
          ptr(alpha), ptr(argmax), s)
 
 
-_TUNE: dict = {}
-
-
-def _env_int(name: str, default: int) -> int:
-    """Tuning switches (GATX_*), read from the environment once per process (the forward's
-    per-call path stays free of os.environ lookups); reset_tuning() re-reads them."""
-    v = _TUNE.get(name)
-    if v is None:
-        import os
-        e = os.environ.get(name)
-        v = _TUNE[name] = int(e) if e not in (None, "") else None
-    return default if v is None else v
-
-
-def reset_tuning():
-    _TUNE.clear()
-
-
 def edge_heads_per_item(sh: LayerShape) -> int:
     """Heads per edge work item: ~256+ floats of gathered row per item, so one XCD's L2 holds
     the sweep's slice of the rows (measured inside the PPI forward: 1 head of 256 per item beats
@@ -286,11 +269,11 @@ def edge_heads_per_item(sh: LayerShape) -> int:
     registers). Head-mean layers use the same rule: a head group smaller than NH runs as one
     launch per group, accumulating into the output in stream order (PPI L2: 6 heads x 124
     floats -> 3 groups of 2, each group's per-graph slice ~2.2 MB instead of 6.7 MB)."""
-    hs = _env_int("GATX_HEADS_PER_ITEM", 0)
+    hs = tuning.get("heads_per_item")
     if hs > 0 and sh.NH % hs == 0 and hs <= 8:
         return hs
     if not sh.concat:
-        hm = _env_int("GATX_MEAN_HEADS", 0)
+        hm = tuning.get("mean_heads")
         if hm > 0 and sh.NH % hm == 0 and hm <= 8:
             return hm
         # measured at PPI L2 (6 x 124 floats), edge pass per step: groups of 6 / 3 / 2 / 1
@@ -302,12 +285,12 @@ def edge_heads_per_item(sh: LayerShape) -> int:
 
 def hub_args(graph: Graph, sh: LayerShape, hs: int, group_count: int, dev):
     """The trailing hub-splitting arguments of gatx_edge_forward_hubs: (hub_edges, hubs, count,
-    bound, partials). Segments longer than GATX_HUB_EDGES (8192) edges are aggregated in pieces
+    bound, partials). Segments longer than tuning hub_edges (8192) edges are aggregated in pieces
     by parallel waves (degree skew). Engaged for graphs of more than
-    GATX_HUB_MIN_EDGES (2^22) input edges: there the plan and the combine launch cost nothing
+    tuning hub_min_edges (2^22) input edges: there the plan and the combine launch cost nothing
     next to the edge pass; a smaller graph's longest segment costs one wave at most 2^22 edges."""
-    T = _env_int("GATX_HUB_EDGES", 8192)
-    if T <= 0 or graph.num_input_edges <= _env_int("GATX_HUB_MIN_EDGES", 1 << 22):
+    T = tuning.get("hub_edges")
+    if T <= 0 or graph.num_input_edges <= tuning.get("hub_min_edges"):
         return (0, None, None, 0, None)
     hubs, count, bound = graph.hub_plan(T)
     nb = lib.gatx_edge_forward_hub_part_bytes(bound, sh.NH, sh.F, hs, group_count)
@@ -321,11 +304,11 @@ def bwd_hub_args(graph: Graph, NH: int, F: int, dev, source: bool):
     2^22-edge threshold. The backward's items are one head each (the forward's carry up to 8), so
     a segment costs one wave 8x less there: on R-MAT 1e7 / 1.6e8 splitting at 8192 edges gained
     nothing (dst pass 19.06 ms unsplit vs 17.84 + 1.18 split; profiles/r03m), so the backward
-    splits only segments past GATX_BWD_HUB_EDGES = 65536 edges — the guard against extreme skew
-    (a star graph's hub would otherwise be one wave's walk). GATX_BWD_HUBS=0: never split."""
-    T = _env_int("GATX_BWD_HUB_EDGES", 65536)
-    if (T <= 0 or _env_int("GATX_BWD_HUBS", 1) == 0
-            or graph.num_input_edges <= _env_int("GATX_HUB_MIN_EDGES", 1 << 22)):
+    splits only segments past tuning bwd_hub_edges = 65536 edges — the guard against extreme skew
+    (a star graph's hub would otherwise be one wave's walk). tuning bwd_hubs=0: never split."""
+    T = tuning.get("bwd_hub_edges")
+    if (T <= 0 or tuning.get("bwd_hubs") == 0
+            or graph.num_input_edges <= tuning.get("hub_min_edges")):
         return (0, None, None, 0, None)
     hubs, count, bound = graph.hub_plan(T, source)
     nb = lib.gatx_edge_backward_hub_part_bytes(bound, NH, F, int(source))
@@ -373,7 +356,7 @@ def fold_scores_into_gemm(sh: LayerShape) -> bool:
 def use_reassociation(sh: LayerShape) -> bool:
     """Aggregate x rows instead of Wh rows when x is much narrower (PPI layer 0: 50 vs 1024):
     out_h = (sum alpha~ x[src]) W_h^T == sum alpha~ (x[src] W_h^T)."""
-    if _env_int("GATX_REASSOC", 1) == 0:
+    if tuning.get("reassoc") == 0:
         return False
     return sh.concat and 2 * _round4(sh.F_in) <= sh.Dp and reassoc_heads_per_item(sh) > 0
 
@@ -447,7 +430,7 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
     s = stream()
     E2 = graph.edge_bound   # allocation bound; kernels read |edge_index'| on the device
     f32 = dict(dtype=torch.float32, device=dev)
-    chunk = _env_int("GATX_EDGE_CHUNK", 2048)
+    chunk = tuning.get("edge_chunk")
     out = torch.empty((N, sh.out_cols), **f32)
     alpha = torch.empty((max(E2, 1), sh.NH), **f32) if want_alpha else None
     den = torch.empty((N, sh.NH), **f32)
@@ -523,7 +506,7 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
             call("gatx_gemm_planes", N, sh.K_aug, sh.F_in, ptr(x), sh.F_in, ptr(W_aug), sh.F_in,
                  pp, ptr(Wh), sh.Dp, sh.Dp, ptr(S), max(sh.H2, 1), -1, None, 0, 0, None, 0, 0,
                  None, 0, None, *gemm_workspace(N, sh.K_aug, sh.F_in, dev), s)
-    elif _env_int("GATX_FUSED_SCORES", 1):
+    elif tuning.get("fused_scores"):
         # S reduced from the projection's accumulators in its epilogue (no second read of Wh)
         with _span("gemm", (N, sh.Dp, sh.F_in, sh.NH, sh.F)):
             nb = lib.gatx_projection_scores_workspace_bytes(N, sh.Dp, sh.F_in, sh.NH)
@@ -531,7 +514,7 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
             call("gatx_gemm_planes", N, sh.Dp, sh.F_in, ptr(x), sh.F_in, ptr(W_aug), sh.F_in, pp,
                  ptr(Wh), sh.Dp, sh.Dp, None, 0, -1, None, 0, 0, ptr(a), sh.NH, sh.F, ptr(S), 0,
                  None, ptr(ws), nb, s)
-    else:   # (GATX_FUSED_SCORES=0: the projection alone, then the score pass over Wh)
+    else:   # (tuning fused_scores=0: the projection alone, then the score pass over Wh)
         with _span("gemm", (N, sh.Dp, sh.F_in, sh.NH, sh.F)):
             call("gatx_gemm_planes", N, sh.Dp, sh.F_in, ptr(x), sh.F_in, ptr(W_aug), sh.F_in, pp,
                  ptr(Wh), sh.Dp, sh.Dp, None, 0, -1, None, 0, 0, None, 0, 0, None, 0, None,

@@ -26,16 +26,16 @@ SKIP_GEMM_MIN_MACS = 1 << 26
 
 
 def _dropout_fuse_enabled() -> bool:
-    """GATX_DROPOUT_FUSE=0 applies every input dropout with the standalone gatx kernel instead
+    """tuning dropout_fuse=0 applies every input dropout with the standalone gatx kernel instead
     of the producing layer's epilogue (A/B tests)."""
-    from .functional import _env_int
-    return _env_int("GATX_DROPOUT_FUSE", 1) != 0
+    from . import tuning
+    return tuning.get("dropout_fuse") != 0
 
 
 def _skip_fold_enabled() -> bool:
-    """GATX_SKIP_FOLD=0 turns the folded skip projection off (A/B tests and measurements)."""
-    from .functional import _env_int
-    return _env_int("GATX_SKIP_FOLD", 1) != 0
+    """tuning skip_fold=0 turns the folded skip projection off (A/B tests and measurements)."""
+    from . import tuning
+    return tuning.get("skip_fold") != 0
 
 
 class GATModel(nn.Module):

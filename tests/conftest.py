@@ -24,13 +24,9 @@ def device():
 
 @pytest.fixture(autouse=True)
 def _fresh_tuning():
-    """gatx reads its GATX_* tuning switches once per process; tests that monkeypatch them get a
-    fresh read."""
-    try:
-        from gatx import functional
-    except Exception:   # library not built: the tests that need it fail on their own
-        yield
-        return
-    functional.reset_tuning()
+    """Every test starts and ends with gatx's default tuning switches (gatx.tuning; tests that
+    exercise an alternative path set it explicitly)."""
+    from gatx import tuning
+    tuning.reset()
     yield
-    functional.reset_tuning()
+    tuning.reset()

@@ -2,7 +2,7 @@
 (gatx_dropout) against the oracle's restatement of the counter-based mask, the same dropout fused
 into the producing layer's edge-pass epilogue (out_dropout=) against layer-then-kernel, and a
 PlanetoidGAT-shaped model in train mode (dropout 0.6: input, inter-layer and attention dropout)
-fused vs unfused (GATX_DROPOUT_FUSE=0) under the same seeds. torch's own RNG stream cannot be
+fused vs unfused (gatx.tuning dropout_fuse=0) under the same seeds. torch's own RNG stream cannot be
 reproduced bit for bit, so the mask is gatx's (restated in oracle.dropout_keep)."""
 import numpy as np
 import pytest
@@ -74,8 +74,7 @@ def test_planetoid_model_dropout_fused_vs_unfused(name, device, monkeypatch):
     b = gd.uniform_graph_batch(1, 700, 5000, cfg["num_input_node_features"], feature_seed=61)
     res = {}
     for fuse in ("1", "0"):
-        monkeypatch.setenv("GATX_DROPOUT_FUSE", fuse)
-        functional.reset_tuning()
+        gatx.tuning.set(dropout_fuse=int(fuse))
         torch.manual_seed(3)
         model = gatx.GATModel(**cfg).to(device).train()
         x = torch.from_numpy(b.x).to(device)

@@ -1,6 +1,6 @@
 """Hub splitting of the edge passes (gatx_graph_hub_plan + gatx_edge_forward_hubs, and in the
 backward gatx_edge_backward_dst_hubs / gatx_edge_backward_src_hubs): destination segments (and,
-in the backward's source pass, source segments) longer than GATX_HUB_EDGES are processed in
+in the backward's source pass, source segments) longer than gatx.tuning hub_edges are processed in
 pieces by parallel waves and combined in piece order. Checked against the oracle (the reference's
 dataflow, whose scatter_add_ backward `models/utils.py:17-20` has no per-degree cliff) on graphs
 with destination AND source hubs of a few to many pieces, every epilogue kind (concat, one-pass
@@ -66,11 +66,11 @@ def _run(device, x, ei, W, a, NH, F, concat, dropout=0.0, grads=True, x_grad=Tru
     return r
 
 
-CASES = {   # name: (fin, NH, F, concat, env)
+CASES = {   # name: (fin, NH, F, concat, gatx.tuning switches)
     "concat": (16, 4, 16, True, {}),
     "concat_wide": (16, 2, 256, True, {}),
     "mean_one_pass": (16, 6, 12, False, {}),
-    "mean_multi_pass": (16, 6, 12, False, {"GATX_MEAN_HEADS": "2"}),
+    "mean_multi_pass": (16, 6, 12, False, {"mean_heads": 2}),
     "reassociated": (8, 4, 64, True, {}),
     "reassociated_input": (8, 4, 64, True, {}),   # x needs no gradient: _reassoc_backward
     "dropout": (16, 4, 16, True, {}),
@@ -82,11 +82,9 @@ CASES = {   # name: (fin, NH, F, concat, env)
 def test_hub_split_vs_oracle(name, T, device, monkeypatch):
     fin, NH, F, concat, env = CASES[name]
     dropout = 0.5 if name == "dropout" else 0.0
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
-    monkeypatch.setenv("GATX_HUB_EDGES", T)
-    monkeypatch.setenv("GATX_BWD_HUB_EDGES", T)
-    monkeypatch.setenv("GATX_HUB_MIN_EDGES", "0")
+    from gatx import tuning
+    tuning.set(**env)
+    tuning.set(hub_edges=int(T), bwd_hub_edges=int(T), hub_min_edges=0)
     from gatx import data as gd
     x, ei = _hub_graph(fin=fin)
     W = gd.xavier_uniform(6, NH * F, fin)
@@ -110,10 +108,7 @@ def test_hub_split_vs_oracle(name, T, device, monkeypatch):
     for k in ("out", "alpha") + tuple(f"grad_{k}" for k in keys):
         np.testing.assert_array_equal(r[k], r1[k], err_msg=k)
     # the same layer without splitting: same result to fp32 summation-order noise
-    monkeypatch.setenv("GATX_HUB_EDGES", "0")
-    monkeypatch.setenv("GATX_BWD_HUB_EDGES", "0")
-    from gatx import functional
-    functional.reset_tuning()
+    tuning.set(hub_edges=0, bwd_hub_edges=0)
     r0 = _run(device, x, ei, W, a, NH, F, concat, dropout, x_grad=x_grad)
     assert np.abs(r["out"] - r0["out"]).max() <= 1e-5
     assert np.abs(r["alpha"] - r0["alpha"]).max() <= 1e-5
@@ -188,12 +183,11 @@ def test_rmat_scaled_backward_hub_split(device, monkeypatch):
     x0 = torch.randn(N, FIN, device=device, generator=g)
     gout = torch.randn(N, NH * F, device=device, generator=g)
 
-    monkeypatch.setenv("GATX_BWD_HUB_EDGES", "8192")   # split at the forward's threshold
+    from gatx import tuning
+    tuning.set(bwd_hub_edges=8192)   # split at the forward's threshold
 
     def run(split):
-        monkeypatch.setenv("GATX_BWD_HUBS", "1" if split else "0")
-        from gatx import functional
-        functional.reset_tuning()
+        tuning.set(bwd_hubs=1 if split else 0)
         gatx.clear_graph_cache()
         layer.zero_grad(set_to_none=True)
         x = x0.clone().requires_grad_(True)

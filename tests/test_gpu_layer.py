@@ -223,7 +223,7 @@ def test_gemm_x3_split_accuracy(split_mode, device):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["cora_l0_trained", "ppi_small_l1"])
 def test_layer_goldens_f32_gemm(name, device):
-    """The f32-MFMA GEMM kernels (GATX_GEMM=f32) stay parity-green on the reference goldens."""
+    """The f32-MFMA GEMM kernels (gatx_set_gemm_mode(0)) stay parity-green on the reference goldens."""
     from gatx._lib import lib
     lib.gatx_set_gemm_mode(0)
     try:
@@ -235,7 +235,7 @@ def test_layer_goldens_f32_gemm(name, device):
 @pytest.mark.gpu
 def test_gemm_smallk(device):
     """The small-K path (K <= 64, N <= 256: csrc/gemm_smallk.hip, B split once into LDS) against
-    float64 and beside the tiled kernel (GATX_SMALLK is read once, so the tiled result comes from
+    float64 and beside the tiled kernel (the library always takes the small-K kernel for these shapes, so the tiled result comes from
     the f32 kernel): fused bias / residual / ELU epilogue, batched with strided heads, ragged M,
     N and K, unaligned lda (scalar loads); error relative to sum|a||b| at the fp32 GEMM's level;
     bitwise repeatable."""
@@ -448,7 +448,8 @@ def test_reassociation_paths(reassoc, fin, NH, F, x_grad, device, monkeypatch):
     """First-layer reassociation (aggregate x rows, then project per head) vs the direct path;
     both against the oracle, forward and backward. Without an input gradient the reassociated
     backward runs (g_Z = go W_h, dst pass over x rows, no Wh)."""
-    monkeypatch.setenv("GATX_REASSOC", reassoc)
+    from gatx import tuning
+    tuning.set(reassoc=int(reassoc))
     _layer_vs_oracle(device, 2, 150, 2500, fin, NH, F, True, x_grad=x_grad)
 
 
@@ -461,8 +462,8 @@ def test_reassociated_backward_ppi_l0_dropout(device):
 @pytest.mark.parametrize("hs", ["1", "2", "4"])
 @pytest.mark.parametrize("chunk", ["0", "7"])
 def test_heads_per_item_and_chunking(hs, chunk, device, monkeypatch):
-    monkeypatch.setenv("GATX_HEADS_PER_ITEM", hs)
-    monkeypatch.setenv("GATX_EDGE_CHUNK", chunk)
+    from gatx import tuning
+    tuning.set(heads_per_item=int(hs), edge_chunk=int(chunk))
     _layer_vs_oracle(device, 3, 100, 2000, 300, 4, 64, True)
 
 

@@ -5,7 +5,7 @@ by the edge-pass / output-projection epilogue) against the fp64 oracle: the laye
 W, a and W_s. Covers both first-layer dataflows (reassociated: the skip rides on the score GEMM;
 direct: gatx_projection_gemm3), head mean, const attention and an input without gradient.
 Model level: a PATTERN-shaped GATModel (every layer a Linear skip) with the fold matches the
-oracle's model forward/backward and the unfolded path (GATX_SKIP_FOLD=0)."""
+oracle's model forward/backward and the unfolded path (gatx.tuning skip_fold=0)."""
 import numpy as np
 import pytest
 
@@ -94,9 +94,8 @@ def test_folded_skip_pattern_model(device, monkeypatch):
     ei = torch.from_numpy(b.edge_index).to(device)
     results = {}
     for fold in ("1", "0"):
-        monkeypatch.setenv("GATX_SKIP_FOLD", fold)
-        from gatx import functional
-        functional.reset_tuning()
+        from gatx import tuning
+        tuning.set(skip_fold=int(fold))
         model = _pattern_model(device, 5)
         x = torch.from_numpy(b.x).to(device)
         out = model(x, ei)

@@ -38,9 +38,8 @@ def test_next_layer_dropout_fusion_decisions(name, expected):
 
 
 def test_dropout_fuse_switch(monkeypatch):
-    from gatx import functional
-    monkeypatch.setenv("GATX_DROPOUT_FUSE", "0")
-    functional.reset_tuning()
+    from gatx import tuning
+    tuning.set(dropout_fuse=0)
     m = _model("Cora")
     assert not any(m._fuse_next_dropout(i) for i in range(m.num_layers))
 
@@ -63,12 +62,11 @@ def test_reference_wiring_flag_defaults_to_fused():
 def test_split_gemm_kernel_choices(monkeypatch):
     """Which GEMMs take the pre-split weight planes (gemm_f16p) and the f16x3 weight gradient
     (gemm_f16rc): PPI's projection / g_x shapes do, small or unaligned weights and wide weight
-    gradients do not, and GATX_F16P=0 turns both off (no GPU call: the library only reports its
+    gradients do not, and tuning f16p=0 turns both off (no GPU call: the library only reports its
     arithmetic mode)."""
     from gatx import functional as gf
     from gatx._lib import lib
-    monkeypatch.delenv("GATX_F16P", raising=False)
-    gf.reset_tuning()
+    from gatx import tuning
     lib.gatx_set_gemm_mode(2)
     try:
         assert gf.use_weight_planes(1032, 1024, 44900)        # PPI L1 projection
@@ -81,15 +79,13 @@ def test_split_gemm_kernel_choices(monkeypatch):
         assert not gf.use_wgrad_f16(1032, 50, 44900)
         assert lib.gatx_gemm_layout_mode(1, 1) == 2 and lib.gatx_gemm_layout_mode(0, 0) == 2
         assert lib.gatx_gemm_layout_mode(1, 0) == 1
-        monkeypatch.setenv("GATX_F16P", "0")
-        gf.reset_tuning()
+        tuning.set(f16p=0)
         assert not gf.use_weight_planes(1032, 1024, 44900)
         assert not gf.use_wgrad_f16(1032, 1024, 44900)
         lib.gatx_set_gemm_mode(1)
-        monkeypatch.delenv("GATX_F16P")
-        gf.reset_tuning()
+        tuning.reset()
         assert not gf.use_weight_planes(1032, 1024, 44900)    # x3 arithmetic: no planes
         assert lib.gatx_gemm_layout_mode(1, 1) == 1
     finally:
         lib.gatx_set_gemm_mode(2)
-        gf.reset_tuning()
+        tuning.reset()
