@@ -873,7 +873,7 @@ def main():
                          "step, no GPU touched (CPU rehearsal of the driver's N-GPU command)")
     ap.add_argument("--hipgraph", choices=["auto", "on", "off"], default="auto",
                     help="replay each step as one captured hipGraph (gatx.capture). auto: forward "
-                         "steps, and PATTERN training on one GPU")
+                         "steps, and every training step on one GPU")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -947,8 +947,13 @@ def main():
         from gatx.graph import graph_cache as _gc
         _ = _gc.get(ei, b.num_nodes, True).num_edges   # built and validated before any capture
     use_graph = args.hipgraph == "on" or (
-        args.hipgraph == "auto" and (args.mode == "fwd"
-                                     or (world == 1 and (ds == "PATTERN" or planetoid))))
+        args.hipgraph == "auto" and (args.mode == "fwd" or world == 1))
+    if use_graph and args.mode == "train" and not args.cached_graph and ds != "PATTERN":
+        # PPI_GAT's step returns the attention (forward_and_return_attention) while its CSR is
+        # rebuilt every step: promise |edge_index'| (known from one eager build of this batch)
+        # so the captured step needs no device read (gatx.graph.expect_num_edges)
+        from gatx.graph import expect_num_edges, graph_cache as _gc
+        expect_num_edges(ei, b.num_nodes, True, _gc.get(ei, b.num_nodes, True).num_edges)
     # a captured training step needs the optimizer's step counter on the device
     # torch's fused Adam (one launch for all parameters; same update rule as the reference's
     # Adam, models/*_gat.py configure_optimizers); a captured step needs capturable state
@@ -1033,7 +1038,7 @@ def main():
     fb = torch.zeros(1, dtype=torch.int64, device=dev)
     _lib.call("gatx_gemm_fallback_read", _lib.ptr(fb), 1, _lib.stream())   # reset the counter
     # (small batches are launch-bound: their instrumented eager steps run after the clock)
-    instr_outside = use_graph and ds != "PPI"
+    instr_outside = use_graph and (ds != "PPI" or args.graphs < 20)
     elapsed, summ, n_instr = run_timed(step, args.steps, world, dev,
                                        step.eager if use_graph else None, instr_outside)
     _lib.call("gatx_gemm_fallback_read", _lib.ptr(fb), 1, _lib.stream())

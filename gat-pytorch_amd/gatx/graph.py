@@ -107,6 +107,10 @@ class Graph:
         self.srowptr = self.scol = self.seid = None
         self._hub_plans = {}
         self._E2 = None
+        # |edge_index'| promised by the caller (expect_num_edges): answers num_edges without a
+        # device read (so a captured step may return edge_index' / alpha); checked against the
+        # device count whenever that is read
+        self._E2_hint = _HINTS.get(_hint_key(edge_index, N, add_self_loops))
         self._error = None
         self._edge_index = None
         # non-blocking validation: the meta lands in pinned memory behind an event
@@ -141,6 +145,11 @@ class Graph:
             self._error = err   # every later use of this graph raises it again
             raise err
         self._E2 = int(m[0])
+        if self._E2_hint is not None and self._E2 != self._E2_hint:
+            self._error = RuntimeError(
+                f"gatx: edge_index' has {self._E2} edges, but expect_num_edges promised "
+                f"{self._E2_hint} for this edge_index (its contents changed?)")
+            raise self._error
 
     def poll(self):
         """Validate without blocking if the device has produced the meta (raises on bad ids)."""
@@ -156,13 +165,20 @@ class Graph:
         """|edge_index'| (reads the device meta once: a sync if it is not there yet)."""
         if self._error is not None:
             raise self._error
+        if self._E2 is None and self._E2_hint is not None:
+            # trust the promise now; the device count is compared when it lands (poll /
+            # check_pending), or never inside a captured step
+            return self._E2_hint
         if self._E2 is None:
-            if self._event is not None:
-                self._event.synchronize()
-                self._validate(self._meta_host)
-            else:
-                self._validate(self.meta.cpu())
+            self._read_meta()
         return self._E2
+
+    def _read_meta(self):
+        if self._event is not None:
+            self._event.synchronize()
+            self._validate(self._meta_host)
+        else:
+            self._validate(self.meta.cpu())
 
     @property
     def edge_index(self) -> torch.Tensor:
@@ -215,6 +231,28 @@ class Graph:
 
 _META_WS = {}
 _PENDING: list = []
+_HINTS: dict = {}
+
+
+def _hint_key(edge_index: torch.Tensor, num_nodes, add_self_loops: bool):
+    return (edge_index.data_ptr(), tuple(edge_index.shape), edge_index.dtype, edge_index.device,
+            num_nodes, add_self_loops)
+
+
+def expect_num_edges(edge_index: torch.Tensor, num_nodes: int, add_self_loops: bool,
+                     num_edges: int | None) -> None:
+    """Promise |edge_index'| for this edge_index tensor (same storage, shape and node count) for
+    every later graph build from it, cached or rebuilt, so returning edge_index' / the attention
+    weights needs no device read: what lets a step that rebuilds its CSR every time (the
+    reference rewrites self-loops in every layer call) and returns the attention (PPI_GAT /
+    PlanetoidGAT's forward_and_return_attention) be captured as a hipGraph. The device count is
+    still compared with the promise whenever it is read outside a capture (a mismatch raises, as
+    a device assert would). None withdraws the promise. Survives clear_graph_cache()."""
+    k = _hint_key(edge_index, num_nodes, add_self_loops)
+    if num_edges is None:
+        _HINTS.pop(k, None)
+    else:
+        _HINTS[k] = int(num_edges)
 
 
 def _meta_ws(dev):
@@ -237,7 +275,7 @@ def check_pending(block: bool = True):
             continue   # gone, validated, or its error already raised
         try:
             if block:
-                _ = g.num_edges
+                g._read_meta()
             else:
                 g.poll()
         except Exception:

@@ -93,3 +93,65 @@ def test_captured_pattern_train_step_equals_eager(device):
     assert abs(float(last) - losses[-1]) <= 1e-6 * max(1.0, abs(losses[-1]))
     for p1, p2 in zip(m1.parameters(), m2.parameters()):
         assert torch.equal(p1, p2)
+
+
+def test_captured_ppi_train_step_equals_eager(device):
+    """PPI_GAT.training_step (`models/ppi_gat.py:15-33`) at the reference batch of 2 graphs
+    (`run_config.py:30`) captured as one hipGraph: the step rebuilds its CSR
+    every time (clear_graph_cache) AND returns the attention (forward_and_return_attention, the
+    attention norm with a non-zero penalty), which needs |edge_index'| on the host — promised by
+    gatx.graph.expect_num_edges, so nothing reads the device inside the capture. Replays give
+    the eager step's parameters bit for bit; a broken promise raises when the count is read."""
+    import gatx
+    from gatx.capture import CapturedStep
+    from gatx.config import data_config
+    from gatx.graph import expect_num_edges, graph_cache
+    from gatx.losses import BCEWithLogitsLoss
+    cfg = data_config["PPI"]
+    x, ei, b = _batch("PPI", 2, device)
+    y = (torch.from_numpy(np.arange(b.num_nodes * 121) % 7 == 0).float()).to(device).view(-1, 121)
+    loss_fn = BCEWithLogitsLoss()
+
+    def make():
+        torch.manual_seed(0)
+        m = gatx.GATModel(**cfg).to(device).train()
+        o = torch.optim.Adam(m.parameters(), lr=cfg["learning_rate"], capturable=True)
+        return m, o
+
+    def make_step(m, o):
+        def step():
+            gatx.clear_graph_cache()
+            o.zero_grad(set_to_none=True)
+            out, ei2, atts = m.forward_and_return_attention(x, ei)
+            loss = loss_fn(out, y) + 0.1 * m.calc_attention_norm(ei2, atts)
+            loss.backward()
+            o.step()
+            return loss.detach()
+        return step
+
+    gatx.clear_graph_cache()
+    E2 = graph_cache.get(ei, b.num_nodes, True).num_edges
+    m1, o1 = make()
+    s1 = make_step(m1, o1)
+    losses = [float(s1()) for _ in range(2 + 5)]
+    expect_num_edges(ei, b.num_nodes, True, E2)
+    try:
+        m2, o2 = make()
+        cap = CapturedStep(make_step(m2, o2), warmup=2)
+        for _ in range(5):
+            last = cap()
+        torch.cuda.synchronize()
+        assert abs(float(last) - losses[-1]) <= 1e-6 * max(1.0, abs(losses[-1]))
+        for p1, p2 in zip(m1.parameters(), m2.parameters()):
+            assert torch.equal(p1, p2)
+        # a promise that does not match the device count raises at its first host read
+        expect_num_edges(ei, b.num_nodes, True, E2 + 1)
+        gatx.clear_graph_cache()
+        g = graph_cache.get(ei, b.num_nodes, True)
+        assert g.num_edges == E2 + 1          # the promise answers without a device read
+        with pytest.raises(RuntimeError, match="expect_num_edges"):
+            from gatx.graph import check_pending
+            check_pending(block=True)
+    finally:
+        expect_num_edges(ei, b.num_nodes, True, None)
+        gatx.clear_graph_cache()
