@@ -7,4 +7,5 @@ python -c "
 import json
 for f in ('ppi2_train','ppi2_train_eager'):
     d=json.load(open('$OUT/'+f+'.json')); print(f, d['ms_per_step'], d['config']['launch'])"
-bash tools/gpu_ab.sh r06c 3 "" "-" "--tune edge_chunk=2245" "--tune edge_chunk=1122"
+bash tools/gpu_ab.sh r06c 3 "" "-" "--tune edge_chunk=2245" "--tune edge_chunk=1122" || exit 1
+cd tools/edge_lab && timeout -k 10 120 ./edge_lab > $OUT/edge_lab.txt 2>&1; rc=$?; cat $OUT/edge_lab.txt; exit $rc
