@@ -1,0 +1,294 @@
+// LDS-staged edge forward (round 5) for graphs that split into node blocks of <= kLdsRows nodes
+// with no edge between blocks (a PyG-style batch of graphs: gatx_graph_segments). Replaces the
+// L2-gather aggregation of edge_fwd.hip (one wave per (node, head), one 1 KB row gathered per
+// edge, bound by the L2 -> CU gather rate, ~15 TB/s) with two passes:
+//
+//   records   one wave per destination n, all NH heads: raw = s_src[src] + s_dst[n] (the
+//             factorised logits), ex = exp(0.01 (raw - M)), den = sum ex (the same per-lane
+//             partials and butterfly as edge_forward_kernel, so den and alpha are bitwise the
+//             L2-gather pass's), alpha = ex / (den + 1e-8) written in edge_index' order (the
+//             reference's returned attention, models/gat_layer.py:106-110, one NH-float row per
+//             edge), max()'s tied argmax entries recorded as attention_alpha_ei does, and per
+//             (head, CSR slot) the record {4 * src, alpha~} (the source row's float4 index in a
+//             whole-graph image) (alpha~ = dropout(alpha), :112-115).
+//   aggregate one 1024-thread workgroup per (node block, head, 16-float chunk of the head's row):
+//             the chunk of every row of the block is staged in LDS (<= 2304 x 64 B = 144 KB), then
+//             each wave takes 16 destinations at a time, a quad of lanes per destination walking
+//             its CSR segment: per edge one 8-byte record load, one ds_read_b128 of the source's
+//             16 B piece per lane, one float4 FMA — out[n, h, chunk] = sum_e alpha~ Wh[src, h,
+//             chunk] (:117-127), then bias, the fused skip add, ELU and the next layer's input
+//             dropout as edge_forward_kernel's epilogue.
+// The staged bytes are read from LDS at up to 256 B/clk/CU (MI355X_MICROARCH.md §LDS) instead of
+// from L2 at ~64 B/clk/CU.
+#include "gatx_common.h"
+
+namespace gatx {
+namespace {
+
+constexpr int kLdsRows = 2304;         // rows of one staged chunk image (2304 x 64 B = 144 KB)
+constexpr int kChunk = 16;             // floats per chunk (64 B rows: 4 lanes x float4)
+
+__device__ inline int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ inline int64_t xcd_contiguous(int64_t b, int64_t nb) {
+  const int64_t q = nb / 8, r = nb % 8, xcd = b % 8, j = b / 8;
+  return (xcd < r) ? xcd * (q + 1) + j : r * (q + 1) + (xcd - r) * q + j;
+}
+
+struct RecArgs {
+  const float* S;            // [N][2NH] = (s_src | s_dst)
+  const uint32_t* M_ord;
+  const int32_t* rowptr;
+  const int32_t* col;
+  const int32_t* perm;       // CSR slot -> edge_index' position
+  int64_t N, E_bound;
+  int NH, const_att;
+  float p_drop;
+  const uint64_t* seed;
+  int2* rec;                 // [NH][E_bound]
+  float* den;                // [N][NH]
+  float* alpha;              // [E'][NH], edge_index' order (nullable)
+  long long* argmax;         // tie records (nullable)
+};
+
+// one wave per destination; lane j <-> CSR slot beg + j of each 64-edge batch
+template <int NHC>
+__global__ void __launch_bounds__(256) edge_records_kernel(RecArgs g) {
+  const int lane = threadIdx.x & 63;
+  const int64_t n = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (n >= g.N) return;
+  const int NH = NHC, S2 = 2 * NHC;
+  const int beg = uni(g.rowptr[n]), end = uni(g.rowptr[n + 1]);
+  const float M = g.const_att ? 0.f : ord_to_float(*g.M_ord);
+  float sdst[NHC], dn[NHC];
+#pragma unroll
+  for (int h = 0; h < NHC; ++h) {
+    sdst[h] = g.const_att ? 0.f : g.S[n * S2 + NH + h];
+    dn[h] = 0.f;
+  }
+  // sweep 1: denominators (per-lane partials over the batches, then the butterfly, exactly as
+  // edge_forward_kernel sums them)
+  for (int base = beg; base < end; base += 64) {
+    const int e = base + lane;
+    if (e < end) {
+      const int64_t src = g.col[e];
+#pragma unroll
+      for (int h = 0; h < NHC; ++h)
+        dn[h] += g.const_att ? 1.f : att_exp(g.S[src * S2 + h] + sdst[h], M);
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < NHC; ++h) {
+    float t = dn[h];
+    for (int off = 1; off < 64; off <<= 1) t += __shfl_xor(t, off);
+    dn[h] = t;
+  }
+  if (lane < NHC) {
+    float d = 0.f;
+#pragma unroll
+    for (int h = 0; h < NHC; ++h)
+      if (h == lane) d = dn[h];
+    g.den[n * NH + lane] = d;
+  }
+  const bool drop = g.p_drop > 0.f;
+  const float drop_scale = drop ? 1.f / (1.f - g.p_drop) : 1.f;
+  const uint64_t seed = drop ? *g.seed : 0ull;
+  // sweep 2: alpha, its records, ties
+  for (int base = beg; base < end; base += 64) {
+    const int e = base + lane;
+    if (e >= end) continue;
+    const int src = g.col[e];
+    const int64_t p = g.perm[e];
+    float a[NHC];
+#pragma unroll
+    for (int h = 0; h < NHC; ++h) {
+      const float raw = g.const_att ? 0.f : g.S[(int64_t)src * S2 + h] + sdst[h];
+      a[h] = (g.const_att ? 1.f : att_exp(raw, M)) / (dn[h] + kSoftmaxEps);
+      if (!g.const_att && raw == M && g.argmax) {   // rare: every tied argmax (slot, head)
+        unsigned long long k = atomicAdd((unsigned long long*)g.argmax, 1ull);
+        if (k < GATX_ARGMAX_CAP) g.argmax[1 + k] = (long long)e * NH + h;
+      }
+      float w = a[h];
+      if (drop) w = dropout_keep(seed, p * NH + h, g.p_drop) ? w * drop_scale : 0.f;
+      g.rec[(int64_t)h * g.E_bound + e] = make_int2(src * 4, __float_as_int(w));
+    }
+    if (g.alpha) {
+      float* o = g.alpha + p * NH;
+      if constexpr (NHC % 4 == 0) {
+#pragma unroll
+        for (int h = 0; h < NHC; h += 4) *(float4*)(o + h) = make_float4(a[h], a[h + 1], a[h + 2], a[h + 3]);
+      } else if constexpr (NHC % 2 == 0) {
+#pragma unroll
+        for (int h = 0; h < NHC; h += 2) *(float2*)(o + h) = make_float2(a[h], a[h + 1]);
+      } else {
+#pragma unroll
+        for (int h = 0; h < NHC; ++h) o[h] = a[h];
+      }
+    }
+  }
+}
+
+struct LdsArgs {
+  const float* rows;         // Wh: row r, head h, feature f at rows[r * row_stride + h * Fp + f]
+  int64_t row_stride;
+  const int32_t* rowptr;
+  const int2* rec;           // [NH][E_bound]
+  int64_t E_bound;
+  const int32_t* segs;       // block b = nodes [segs[b], segs[b + 1])
+  const int32_t* seg_count;
+  int64_t seg_bound;         // grid's block dimension (>= *seg_count)
+  int NH, F, Fp, nchunks;
+  const float* bias;         // [NH * F] or nullptr
+  float* out;
+  int64_t out_ld;
+  const float* resid;
+  int64_t resid_ld;
+  int elu;
+  float out_p;
+  const uint64_t* out_seed;
+  int vec_out;               // F % 4 == 0 and 16-byte aligned rows of out / resid
+};
+
+__device__ inline float lds_epilogue(float v, const LdsArgs& g, int64_t n, int64_t col) {
+  if (g.bias) v += g.bias[col];
+  if (g.resid) v += g.resid[n * g.resid_ld + col];
+  if (g.elu) v = elu_act(v);
+  if (g.out_p > 0.f)
+    v = dropout_keep(*g.out_seed, n * (int64_t)(g.NH * g.F) + col, g.out_p) ? v * (1.f / (1.f - g.out_p))
+                                                                          : 0.f;
+  return v;
+}
+
+template <int U>
+__global__ void __launch_bounds__(1024) edge_lds_kernel(LdsArgs g) {
+  __shared__ __attribute__((aligned(16))) float4 img[kLdsRows * 4];
+  const int64_t b = xcd_contiguous(blockIdx.x, gridDim.x);   // the chunks of one (block, head)
+  const int c = (int)(b % g.nchunks);                           // run on one XCD: its records
+  const int h = (int)((b / g.nchunks) % g.NH);                  // stay in that L2
+  const int64_t k = b / ((int64_t)g.nchunks * g.NH);
+  if (k >= (int64_t)*g.seg_count) return;
+  const int n0 = g.segs[k], R = g.segs[k + 1] - n0;
+  const int tid = threadIdx.x;
+  const int F4 = g.Fp / 4;
+  // stage: 4 lanes per row (64 B); pieces past the head's padded row end stage zeros
+  {
+    const int q = tid & 3;
+    const int f4 = c * 4 + q;
+    const float4* src = (const float4*)(g.rows + (int64_t)h * g.Fp) + f4;
+    const int64_t rs4 = g.row_stride / 4;
+    for (int r = tid >> 2; r < R; r += 256)
+      img[r * 4 + q] = f4 < F4 ? src[(int64_t)(n0 + r) * rs4] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  __syncthreads();
+  const int lane = tid & 63, wave = tid >> 6, q = lane & 3, j = lane >> 2;
+  const int2* rh = g.rec + (int64_t)h * g.E_bound;
+  // image float4 of (source s, piece q) = 4 s + q - 4 n0: records hold 4 s
+  const int qoff = q - 4 * n0;
+  const int f0 = c * kChunk + q * 4;   // this lane's first feature in the head's row
+  for (int d0 = wave * 16; d0 < R; d0 += 256) {
+    const int dl = d0 + j;
+    const bool live = dl < R;
+    const int64_t n = n0 + dl;
+    int e = live ? g.rowptr[n] : 0;
+    const int end = live ? g.rowptr[n + 1] : 0;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    while (__builtin_amdgcn_readfirstlane((int)__any(e < end))) {   // wave-uniform trip count
+      int2 r[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) r[u] = (e + u < end) ? rh[e + u] : make_int2(4 * n0, 0);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const float4 v = img[r[u].x + qoff];
+        acc = fma4(__int_as_float(r[u].y), v, acc);
+      }
+      e += U;
+    }
+    if (!live || f0 >= g.F) continue;
+    const int64_t cb = (int64_t)h * g.F + f0;
+    float* orow = g.out + n * g.out_ld;
+    if (g.vec_out) {
+      float4 o = acc;
+      if (g.bias) o = add4(o, *(const float4*)(g.bias + cb));
+      if (g.resid) o = add4(o, *(const float4*)(g.resid + n * g.resid_ld + cb));
+      if (g.elu) {
+        o.x = elu_act(o.x); o.y = elu_act(o.y); o.z = elu_act(o.z); o.w = elu_act(o.w);
+      }
+      if (g.out_p > 0.f) {
+        const float sc = 1.f / (1.f - g.out_p);
+        const int64_t base = n * (int64_t)(g.NH * g.F) + cb;
+        const uint64_t sd = *g.out_seed;
+        o.x = dropout_keep(sd, base, g.out_p) ? o.x * sc : 0.f;
+        o.y = dropout_keep(sd, base + 1, g.out_p) ? o.y * sc : 0.f;
+        o.z = dropout_keep(sd, base + 2, g.out_p) ? o.z * sc : 0.f;
+        o.w = dropout_keep(sd, base + 3, g.out_p) ? o.w * sc : 0.f;
+      }
+      *(float4*)(orow + cb) = o;
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        if (f0 + t < g.F) orow[cb + t] = lds_epilogue(get4(acc, t), g, n, cb + t);
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int gatx_edge_lds_rows(void) { return kLdsRows; }
+
+extern "C" int gatx_edge_records(const float* S, const uint32_t* M_ord, const int32_t* rowptr,
+                                 const int32_t* col, const int32_t* perm, int64_t N,
+                                 int64_t E_bound, int NH, int const_att, float dropout_p,
+                                 const uint64_t* seed, void* rec, float* den, float* alpha,
+                                 long long* argmax, gatx_stream_t s) {
+  GATX_REQUIRE(N >= 0 && E_bound >= 0 && NH >= 1 && NH <= 8, "edge_records: bad arguments");
+  GATX_REQUIRE(dropout_p == 0.f || seed != nullptr, "edge_records: dropout needs its seed");
+  if (N == 0) return 0;
+  RecArgs g;
+  g.S = S; g.M_ord = M_ord; g.rowptr = rowptr; g.col = col; g.perm = perm;
+  g.N = N; g.E_bound = E_bound; g.NH = NH; g.const_att = const_att;
+  g.p_drop = dropout_p; g.seed = seed; g.rec = (int2*)rec; g.den = den; g.alpha = alpha;
+  g.argmax = argmax;
+  const unsigned grid = (unsigned)ceil_div(N, (int64_t)4);
+  hipStream_t st = (hipStream_t)s;
+  switch (NH) {
+    case 1: edge_records_kernel<1><<<grid, 256, 0, st>>>(g); break;
+    case 2: edge_records_kernel<2><<<grid, 256, 0, st>>>(g); break;
+    case 3: edge_records_kernel<3><<<grid, 256, 0, st>>>(g); break;
+    case 4: edge_records_kernel<4><<<grid, 256, 0, st>>>(g); break;
+    case 5: edge_records_kernel<5><<<grid, 256, 0, st>>>(g); break;
+    case 6: edge_records_kernel<6><<<grid, 256, 0, st>>>(g); break;
+    case 7: edge_records_kernel<7><<<grid, 256, 0, st>>>(g); break;
+    default: edge_records_kernel<8><<<grid, 256, 0, st>>>(g); break;
+  }
+  GATX_LAUNCH_CHECK("edge_records");
+  return 0;
+}
+
+extern "C" int gatx_edge_lds_forward(const float* rows, int64_t row_stride,
+                                     const int32_t* rowptr, const void* rec,
+                                     int64_t E_bound, const int32_t* segs,
+                                     const int32_t* seg_count, int64_t seg_bound, int NH, int F,
+                                     const float* bias, float* out, int64_t out_ld,
+                                     const float* resid, int64_t resid_ld, int elu,
+                                     float out_p, const uint64_t* out_seed, gatx_stream_t s) {
+  const int Fp = (int)round_up(F, 4);
+  GATX_REQUIRE(NH >= 1 && F >= 1 && seg_bound >= 0 && row_stride >= (int64_t)NH * Fp &&
+                   row_stride % 4 == 0 && (uintptr_t)rows % 16 == 0,
+               "edge_lds_forward: bad arguments");
+  GATX_REQUIRE(out_p == 0.f || out_seed != nullptr, "edge_lds_forward: dropout needs its seed");
+  if (seg_bound == 0) return 0;
+  LdsArgs g;
+  g.rows = rows; g.row_stride = row_stride; g.rowptr = rowptr; g.rec = (const int2*)rec;
+  g.E_bound = E_bound; g.segs = segs; g.seg_count = seg_count; g.seg_bound = seg_bound;
+  g.NH = NH; g.F = F; g.Fp = Fp; g.nchunks = (int)ceil_div(Fp, kChunk);
+  g.bias = bias; g.out = out; g.out_ld = out_ld; g.resid = resid; g.resid_ld = resid_ld;
+  g.elu = elu; g.out_p = out_p; g.out_seed = out_seed;
+  auto al = [](const void* p, int64_t ld) { return p == nullptr || ((uintptr_t)p % 16 == 0 && ld % 4 == 0); };
+  g.vec_out = (F % 4 == 0) && al(out, out_ld) && al(resid, resid_ld) && al(bias, 0);
+  const int64_t blocks = seg_bound * NH * g.nchunks;
+  GATX_REQUIRE(blocks < (1ll << 31), "edge_lds_forward: too many workgroups");
+  edge_lds_kernel<4><<<(unsigned)blocks, 1024, 0, (hipStream_t)s>>>(g);
+  GATX_LAUNCH_CHECK("edge_lds_forward");
+  return 0;
+}
+
+}  // namespace gatx

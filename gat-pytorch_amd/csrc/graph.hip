@@ -896,6 +896,173 @@ extern "C" int gatx_graph_transpose(const int32_t* col, const int32_t* rowidx, i
   return 0;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Node blocks (round 5): the node range cut into contiguous blocks that no edge crosses, each at
+// most max_rows nodes — the graphs of a PyG-style batch, packed greedily — found from the CSR
+// alone. A boundary b (0 < b < N) is free when max_{d<b} hi[d] < b and min_{d>=b} lo[d] >= b,
+// with lo / hi[d] the smallest / largest node among d and its in-neighbours (an edge s -> d
+// covers every boundary in (min(s,d), max(s,d)]). The LDS-staged edge passes stage one block's
+// rows per workgroup; the count is -1 when some gap-free run exceeds max_rows, when there are more
+// than kSegMax runs, or N > kSegMaxNodes (those graphs keep the L2-gather passes).
+constexpr int kSegMax = 4096;
+constexpr int64_t kSegMaxNodes = int64_t(1) << 17;
+
+// one wave per destination: lo / hi over its in-neighbours (lanes stride the segment)
+__global__ void __launch_bounds__(256) seg_hilo_kernel(const int32_t* __restrict__ rowptr,
+                                                       const int32_t* __restrict__ col, int64_t N,
+                                                       int32_t* __restrict__ lo,
+                                                       int32_t* __restrict__ hi) {
+  const int lane = threadIdx.x & 63;
+  const int64_t d = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (d >= N) return;
+  const int beg = rowptr[d], end = rowptr[d + 1];
+  int mn = (int)d, mx = (int)d;
+  for (int e = beg + lane; e < end; e += 64) {
+    const int s = col[e];
+    mn = min(mn, s);
+    mx = max(mx, s);
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    mn = min(mn, __shfl_xor(mn, off));
+    mx = max(mx, __shfl_xor(mx, off));
+  }
+  if (lane == 0) {
+    lo[d] = mn;
+    hi[d] = mx;
+  }
+}
+
+// one 1024-thread workgroup: thread t owns nodes [t c, t c + c); pm[] (global scratch) holds the
+// prefix max of hi within the thread's range between its two sweeps
+__global__ void __launch_bounds__(1024) seg_build_kernel(const int32_t* __restrict__ lo,
+                                                         const int32_t* __restrict__ hi,
+                                                         int32_t* __restrict__ pm, int64_t N,
+                                                         int max_rows, int32_t* __restrict__ segs,
+                                                         int32_t* __restrict__ seg_count) {
+  __shared__ int sh_a[1024], sh_b[1024];
+  __shared__ int bnd[kSegMax + 2];
+  __shared__ int total;
+  const int t = threadIdx.x;
+  const int n = (int)N;
+  const int c = (n + 1023) / 1024;
+  const int r0 = min(n, t * c), r1 = min(n, r0 + c);
+  int tmax = -1, tmin = n;
+  for (int d = r0; d < r1; ++d) {
+    tmax = max(tmax, hi[d]);
+    pm[d] = tmax;   // max of hi over [r0, d]
+    tmin = min(tmin, lo[d]);
+  }
+  sh_a[t] = tmax;
+  sh_b[t] = tmin;
+  __syncthreads();
+  // exclusive prefix max of tmax, exclusive suffix min of tmin (Hillis-Steele in LDS)
+  for (int off = 1; off < 1024; off <<= 1) {
+    const int a = t >= off ? sh_a[t - off] : -1;
+    const int b = t + off < 1024 ? sh_b[t + off] : n;
+    __syncthreads();
+    sh_a[t] = max(sh_a[t], a);
+    sh_b[t] = min(sh_b[t], b);
+    __syncthreads();
+  }
+  const int pmax_before = t > 0 ? sh_a[t - 1] : -1;   // max hi over d < r0
+  const int smin_after = t < 1023 ? sh_b[t + 1] : n;  // min lo over d >= r1
+  __syncthreads();
+  // boundaries b in (r0, r1] with 0 < b < n, swept backwards (suffix min of lo within range)
+  int cnt = 0, sm = smin_after;
+  for (int b = r1; b > r0; --b) {
+    if (b < n) {
+      const int before = max(pmax_before, pm[b - 1]);
+      if (before < b && sm >= b) ++cnt;
+    }
+    sm = min(sm, lo[b - 1]);
+  }
+  sh_a[t] = cnt;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {   // inclusive prefix sum of the counts
+    const int a = t >= off ? sh_a[t - off] : 0;
+    __syncthreads();
+    sh_a[t] += a;
+    __syncthreads();
+  }
+  if (t == 1023) total = sh_a[1023];
+  __syncthreads();
+  const int nb = total;   // free boundaries strictly inside (0, n)
+  if (nb <= kSegMax) {
+    int k = sh_a[t] - cnt;   // this thread's first slot (ascending order within the thread)
+    // forward order: recompute validity forwards is not possible for the suffix min, so write
+    // the backward sweep's hits from the top of the thread's slot range down
+    int slot = k + cnt - 1;
+    sm = smin_after;
+    for (int b = r1; b > r0; --b) {
+      if (b < n) {
+        const int before = max(pmax_before, pm[b - 1]);
+        if (before < b && sm >= b) bnd[1 + slot--] = b;
+      }
+      sm = min(sm, lo[b - 1]);
+    }
+  }
+  __syncthreads();
+  if (t == 0) {
+    int count = 0;
+    if (n == 0) {
+      segs[0] = 0;
+    } else if (nb > kSegMax) {
+      count = -1;
+    } else {
+      bnd[0] = 0;
+      bnd[nb + 1] = n;
+      // greedy packing of the gap-free runs [bnd[i], bnd[i+1]) into blocks of <= max_rows nodes
+      int start = 0;
+      segs[0] = 0;
+      for (int i = 1; i <= nb + 1 && count >= 0; ++i) {
+        const int b = bnd[i], prev = bnd[i - 1];
+        if (b - prev > max_rows) {
+          count = -1;
+        } else if (b - start > max_rows) {
+          segs[++count] = prev;
+          start = prev;
+        }
+      }
+      if (count >= 0) segs[++count] = n;
+    }
+    *seg_count = count;
+  }
+}
+
+__global__ void seg_none_kernel(int32_t* seg_count) {
+  if (threadIdx.x == 0) *seg_count = -1;
+}
+
+extern "C" size_t gatx_graph_segments_workspace_bytes(int64_t N) {
+  return 3 * align256(sizeof(int32_t) * (size_t)(N > 0 ? N : 1));
+}
+
+extern "C" int gatx_graph_segments(const int32_t* rowptr, const int32_t* col, int64_t N,
+                                   int max_rows, int32_t* segs, int32_t* seg_count, void* ws,
+                                   size_t ws_bytes, gatx_stream_t s) {
+  GATX_REQUIRE(N >= 0 && max_rows > 0, "graph_segments: bad arguments");
+  hipStream_t st = (hipStream_t)s;
+  if (N > kSegMaxNodes) {   // no blocks: the caller keeps the L2-gather passes
+    seg_none_kernel<<<1, 64, 0, st>>>(seg_count);
+    GATX_LAUNCH_CHECK("graph_segments none");
+    return 0;
+  }
+  GATX_REQUIRE(ws_bytes >= gatx_graph_segments_workspace_bytes(N), "graph_segments: workspace");
+  char* p = (char*)ws;
+  int32_t* lo = (int32_t*)p; p += align256(sizeof(int32_t) * (size_t)(N > 0 ? N : 1));
+  int32_t* hi = (int32_t*)p; p += align256(sizeof(int32_t) * (size_t)(N > 0 ? N : 1));
+  int32_t* pm = (int32_t*)p;
+  if (N > 0) {
+    seg_hilo_kernel<<<(unsigned)ceil_div(N, (int64_t)4), 256, 0, st>>>(rowptr, col, N, lo, hi);
+    GATX_LAUNCH_CHECK("graph_segments hilo");
+  }
+  seg_build_kernel<<<1, 1024, 0, st>>>(lo, hi, pm, N, max_rows, segs, seg_count);
+  GATX_LAUNCH_CHECK("graph_segments build");
+  return 0;
+}
+
+extern "C" int gatx_graph_segments_max(void) { return kSegMax; }
+
 extern "C" int64_t gatx_graph_hub_bound(int64_t E_bound, int hub_edges) {
   // sum over hubs of ceil(deg / T) <= E'/T + #hubs <= 2 E'/T
   return hub_edges > 0 ? 2 * ceil_div(E_bound, hub_edges) + 1 : 0;

@@ -223,6 +223,24 @@ class Graph:
             plan = self._hub_plans[key] = (hubs, count, bound)
         return plan
 
+    def node_blocks(self, max_rows: int):
+        """(segs, count) of gatx_graph_segments for this CSR (device tensors, built once per graph
+        and max_rows): contiguous node blocks no edge crosses, each <= max_rows nodes; count -1
+        when the graph has none (a gap-free run longer than max_rows)."""
+        key = ("blocks", max_rows)
+        hit = self._hub_plans.get(key)
+        if hit is None:
+            dev = self.device
+            segs = torch.empty(_lib.lib.gatx_graph_segments_max() + 2, dtype=torch.int32,
+                               device=dev)
+            count = torch.empty(1, dtype=torch.int32, device=dev)
+            wb = _lib.lib.gatx_graph_segments_workspace_bytes(self.num_nodes)
+            ws = torch.empty(max(wb, 1), dtype=torch.uint8, device=dev)
+            call("gatx_graph_segments", ptr(self.rowptr), ptr(self.col), self.num_nodes,
+                 int(max_rows), ptr(segs), ptr(count), ptr(ws), wb, stream())
+            hit = self._hub_plans[key] = (segs, count)
+        return hit
+
     def csr_host(self):
         """(rowptr, col, perm) as CPU tensors — for tests."""
         E2 = self.num_edges

@@ -261,6 +261,20 @@ int64_t gatx_graph_hub_bound(int64_t E_bound, int hub_edges);
 int gatx_graph_hub_plan(const int32_t* rowptr, int64_t num_nodes, int hub_edges, int32_t* hubs,
                         int64_t hub_bound, int32_t* hub_count, gatx_stream_t stream);
 
+/* Node blocks (round 5): cut [0, N) into contiguous blocks [segs[k], segs[k+1]), k <
+ * *seg_count, that no edge crosses (an edge s -> d covers the boundaries in (min, max]), each at
+ * most max_rows nodes, packing the gap-free runs greedily — the graphs of a PyG-style batch
+ * (models/GATModel.py's data.x / data.edge_index of a collated batch), found from the CSR alone.
+ * *seg_count = -1 (device) when a gap-free run exceeds max_rows, there are more than
+ * gatx_graph_segments_max() runs, or N > 2^17. segs: gatx_graph_segments_max() + 2 entries. Two
+ * launches, no host sync. Replaces nothing in the reference (it never batches beyond PyG's
+ * disjoint union); the LDS-staged edge passes stage one block per workgroup. */
+size_t gatx_graph_segments_workspace_bytes(int64_t num_nodes);
+int gatx_graph_segments(const int32_t* rowptr, const int32_t* col, int64_t num_nodes,
+                        int max_rows, int32_t* segs, int32_t* seg_count, void* workspace,
+                        size_t workspace_bytes, gatx_stream_t stream);
+int gatx_graph_segments_max(void);
+
 /* ---------------------------------------------------------------- attention + aggregation */
 
 /* Global max M = max_{e,h} s_src[col[e],h] + s_dst[rowidx[e],h]  (gat_layer.py:85), written as an
@@ -394,6 +408,31 @@ void gatx_set_debug(int flags);
  * cols..ld_dst-1 (float4-aligned source rows for the gathers). */
 int gatx_pad_rows(const float* src, int64_t rows, int64_t cols, int64_t ld_src, float* dst,
                   int64_t ld_dst, gatx_stream_t stream);
+
+/* LDS-staged edge forward (round 5; csrc/edge_lds.hip) for graphs cut into node blocks by
+ * gatx_graph_segments(max_rows = gatx_edge_lds_rows()). Two passes replace gatx_edge_forward_*
+ * + gatx_attention_alpha_ei on such graphs (models/gat_layer.py:84-135):
+ * gatx_edge_records — one wave per destination, all heads: den (bitwise the L2-gather pass's),
+ *   alpha in edge_index' order (nullable), max()'s tied argmax entries (nullable; counter reset by
+ *   gatx_attention_max), and per (head, CSR slot) an 8-byte record {4 * src, alpha~} in rec
+ *   ([NH][E_bound] x 8 B; alpha~ = alpha after the attention dropout). NH <= 8.
+ * gatx_edge_lds_forward — concat layers: one workgroup per (node block, head, 16-float chunk)
+ *   stages that chunk of every row of its block in LDS and sums alpha~ x row over each
+ *   destination's segment, then bias / resid / ELU / the next layer's input dropout as
+ *   gatx_edge_forward_drop. rows: Wh with row_stride >= NH * round4(F) floats, 16-byte aligned.
+ *   seg_bound: the grid's block bound (>= *seg_count; blocks past the count exit). */
+int gatx_edge_lds_rows(void);
+int gatx_edge_records(const float* S, const uint32_t* M_ord, const int32_t* rowptr,
+                      const int32_t* col, const int32_t* perm, int64_t num_nodes,
+                      int64_t E_bound, int num_heads, int const_attention, float dropout_p,
+                      const uint64_t* seed, void* rec, float* den, float* alpha,
+                      long long* argmax, gatx_stream_t stream);
+int gatx_edge_lds_forward(const float* rows, int64_t row_stride, const int32_t* rowptr,
+                          const void* rec, int64_t E_bound, const int32_t* segs,
+                          const int32_t* seg_count, int64_t seg_bound, int num_heads,
+                          int out_features, const float* bias, float* out, int64_t out_ld,
+                          const float* resid, int64_t resid_ld, int elu, float out_p,
+                          const uint64_t* out_seed, gatx_stream_t stream);
 
 /* ---------------------------------------------------------------- backward (autograd of above) */
 

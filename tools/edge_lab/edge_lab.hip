@@ -117,6 +117,87 @@ __global__ void __launch_bounds__(1024) lds_kernel(const float* __restrict__ Wh,
   }
 }
 
+
+// ---- LDS-staged, v2: each lane of a quad loads its own record (RPL consecutive records per
+// lane: 4 * RPL per quad per load), the next group is prefetched while the current one is
+// consumed through quad broadcasts (DPP quad_perm)
+template <int T>
+__device__ inline int qbcast(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, T | (T << 2) | (T << 4) | (T << 6), 0xf, 0xf, false);
+}
+template <int RPL>
+__global__ void __launch_bounds__(1024) lds2_kernel(const float* __restrict__ Wh,
+                                                    const int* __restrict__ rowptr,
+                                                    const int2* __restrict__ rec,
+                                                    const int* __restrict__ seg,
+                                                    int E, float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) float4 rows[MAXR * 4];
+  const int64_t b = xcd_contiguous(blockIdx.x, gridDim.x);
+  const int c = (int)(b % NCH);
+  const int h = (int)((b / NCH) % NH);
+  const int gi = (int)(b / (NCH * NH));
+  const int n0 = seg[gi], R = seg[gi + 1] - n0;
+  const int tid = threadIdx.x;
+  const float4* src4 = (const float4*)Wh;
+  for (int r = tid >> 2; r < R; r += 256)
+    rows[r * 4 + (tid & 3)] = src4[(int64_t)(n0 + r) * (NH * F / 4) + h * (F / 4) + c * 4 + (tid & 3)];
+  __syncthreads();
+  const int lane = tid & 63, wave = tid >> 6, q = lane & 3, j = lane >> 2;
+  const int2* rh = rec + (int64_t)h * E;
+  const int qoff = q - 4 * n0;   // records hold 4 * src (float4 index of the row)
+  constexpr int G = 4 * RPL;     // records per quad per group
+  for (int d0 = wave * 16; d0 < R; d0 += 256) {
+    const int dl = d0 + j;
+    const bool live = dl < R;
+    int e = live ? rowptr[n0 + dl] : 0;
+    const int end = live ? rowptr[n0 + dl + 1] : 0;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    int2 ra[RPL], rb[RPL];
+    bool va[RPL], vb[RPL];
+    const int last = end > 0 ? end - 1 : 0;
+    // unconditional loads (clamped index; out-of-range records masked when consumed), so the
+    // compiler can count them with vmcnt and keep the prefetch in flight
+    auto load = [&](int2 (&r)[RPL], bool (&ok)[RPL], int e0) {
+#pragma unroll
+      for (int u = 0; u < RPL; ++u) {
+        const int ee = e0 + q * RPL + u;
+        ok[u] = ee < end;
+        r[u] = rh[min(ee, last)];
+      }
+    };
+    auto consume = [&](const int2 (&cur0)[RPL], const bool (&ok)[RPL]) {
+#pragma unroll
+      for (int u = 0; u < RPL; ++u) {
+        const int cx = ok[u] ? cur0[u].x : 4 * n0;
+        const int cy = ok[u] ? cur0[u].y : 0;
+#define STEP(T)                                                                              \
+        {                                                                                    \
+          const int x = qbcast<T>(cx);                                                       \
+          const float w = __int_as_float(qbcast<T>(cy));                                     \
+          const float4 v = rows[x + qoff];                                                   \
+          acc.x += w * v.x; acc.y += w * v.y; acc.z += w * v.z; acc.w += w * v.w;            \
+        }
+        STEP(0) STEP(1) STEP(2) STEP(3)
+#undef STEP
+      }
+    };
+    // wave-uniform trip count: groups of G edges, rounded up to pairs (ping-pong)
+    int need = (end - e + G - 1) / G;
+    for (int off = 4; off < 64; off <<= 1) need = max(need, __shfl_xor(need, off));
+    const int trips = __builtin_amdgcn_readfirstlane(need);
+    load(ra, va, e);
+    for (int it = 0; it < trips; it += 2) {
+      load(rb, vb, e + G);
+      consume(ra, va);
+      load(ra, va, e + 2 * G);
+      consume(rb, vb);
+      e += 2 * G;
+    }
+    if (live)
+      ((float4*)out)[(int64_t)(n0 + dl) * (NH * F / 4) + h * (F / 4) + c * 4 + q] = acc;
+  }
+}
+
 __global__ void clobber(float4* p, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     p[i] = make_float4(1.f, (float)i, 0.f, 0.f);
@@ -140,7 +221,7 @@ int main() {
   const int E = rowptr[N];
   std::vector<float> wt((size_t)NH * E);
   for (auto& x : wt) x = (rnd() % 1000) / 1000.f;
-  std::vector<int2> rec((size_t)NH * E);
+  std::vector<int2> rec((size_t)NH * E), rec2((size_t)NH * E);
   std::vector<int> seg(G + 1);
   for (int g = 0; g <= G; ++g) seg[g] = g * NPG;
   for (int h = 0; h < NH; ++h)
@@ -149,22 +230,24 @@ int main() {
         const int n0 = (d / NPG) * NPG;
         float w = wt[(size_t)h * E + e];
         rec[(size_t)h * E + e] = make_int2((col[e] - n0) * 64, *(int*)&w);
+        rec2[(size_t)h * E + e] = make_int2(col[e] * 4, *(int*)&w);
       }
   std::vector<float> Wh((size_t)N * NH * F);
   for (auto& x : Wh) x = ((int)(rnd() % 2001) - 1000) / 1000.f;
   printf("N=%d E'=%d\n", N, E);
 
-  float *dWh, *dwt, *dout, *dout2; int *drp, *dcol, *dseg; int2* drec; float4* junk;
+  float *dWh, *dwt, *dout, *dout2; int *drp, *dcol, *dseg; int2* drec; int2* drec2; float4* junk;
   const int64_t JN = 320ll << 20 >> 4;
   CK(hipMalloc(&dWh, Wh.size() * 4)); CK(hipMalloc(&dwt, wt.size() * 4));
   CK(hipMalloc(&dout, (size_t)N * NH * F * 4)); CK(hipMalloc(&dout2, (size_t)N * NH * F * 4));
   CK(hipMalloc(&drp, rowptr.size() * 4)); CK(hipMalloc(&dcol, col.size() * 4));
-  CK(hipMalloc(&drec, rec.size() * 8)); CK(hipMalloc(&dseg, seg.size() * 4)); CK(hipMalloc(&junk, JN * 16));
+  CK(hipMalloc(&drec, rec.size() * 8)); CK(hipMalloc(&drec2, rec2.size() * 8)); CK(hipMalloc(&dseg, seg.size() * 4)); CK(hipMalloc(&junk, JN * 16));
   CK(hipMemcpy(dWh, Wh.data(), Wh.size() * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(dwt, wt.data(), wt.size() * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(drp, rowptr.data(), rowptr.size() * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(dcol, col.data(), col.size() * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(drec, rec.data(), rec.size() * 8, hipMemcpyHostToDevice));
+  CK(hipMemcpy(drec2, rec2.data(), rec2.size() * 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(dseg, seg.data(), seg.size() * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(dout2, Wh.data(), Wh.size() * 4, hipMemcpyHostToDevice));   // pristine copy of Wh
   hipEvent_t a, bb; CK(hipEventCreate(&a)); CK(hipEventCreate(&bb));
@@ -201,12 +284,16 @@ int main() {
   auto g1 = [&] { gather_kernel<<<gblocks, 256>>>(dWh, drp, dcol, dwt, E, dout); };
   auto l2 = [&] { lds_kernel<2><<<G * NH * NCH, 1024>>>(dWh, drp, drec, dseg, E, dout); };
   auto l4 = [&] { lds_kernel<4><<<G * NH * NCH, 1024>>>(dWh, drp, drec, dseg, E, dout); };
+  auto m1 = [&] { lds2_kernel<1><<<G * NH * NCH, 1024>>>(dWh, drp, drec2, dseg, E, dout); };
+  auto m2 = [&] { lds2_kernel<2><<<G * NH * NCH, 1024>>>(dWh, drp, drec2, dseg, E, dout); };
+  auto m4 = [&] { lds2_kernel<4><<<G * NH * NCH, 1024>>>(dWh, drp, drec2, dseg, E, dout); };
+  (void)l2;
   for (int rep = 0; rep < 2; ++rep) {
     run("gather (library-like)", g1, dout, true);
-    run("lds U=2", l2, dout, true);
-    run("lds U=4", l4, dout, true);
-    run("gather warm", g1, dout, false);
-    run("lds U=4 warm", l4, dout, false);
+    run("lds2 RPL=1", m1, dout, true);
+    run("lds2 RPL=2", m2, dout, true);
+    run("lds2 RPL=4", m4, dout, true);
+    run("lds2 RPL=2 warm", m2, dout, false);
   }
   return 0;
 }
