@@ -867,6 +867,9 @@ def main():
     ap.add_argument("--tune", action="append", default=[], metavar="SWITCH=VALUE",
                     help="set a gatx.tuning switch for this run (A/B measurements; repeatable); "
                          "the line's config.tuning lists every switch that differs from default")
+    ap.add_argument("--verify", action="store_true",
+                    help="after timing, compare one more timed-path step's output with an eager "
+                         "step's (stderr; diagnostic)")
     ap.add_argument("--dry-run", action="store_true",
                     help="exercise the launch path only: --gpus N starts N ranks, each joins a "
                          "gloo group and runs the barrier / max-over-ranks timing around an empty "
@@ -1043,6 +1046,17 @@ def main():
                                        step.eager if use_graph else None, instr_outside)
     _lib.call("gatx_gemm_fallback_read", _lib.ptr(fb), 1, _lib.stream())
     fallback_tiles = int(fb.item())
+    if args.verify and args.mode == "fwd":
+        from gatx.graph import graph_cache as _gcv
+        o1 = step().clone()
+        torch.cuda.synchronize()
+        _g = _gcv.get(ei, b.num_nodes, True)   # the captured step's graph (no eager step since)
+        _h = _g._hub_plans.get(("blocks", 2304))
+        print(f"bench.py --verify: node blocks after a timed-path step: "
+              f"{int(_h[1].item()) if _h is not None else None}", file=sys.stderr)
+        o2 = (step.eager if use_graph else eager_step)().clone()
+        print(f"bench.py --verify: max|timed-path step - eager step| = "
+              f"{float((o1 - o2).abs().max()):.3e}", file=sys.stderr)
     step_s = elapsed / args.steps
     ms = step_s * 1e3
 

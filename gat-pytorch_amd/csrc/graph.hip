@@ -932,101 +932,108 @@ __global__ void __launch_bounds__(256) seg_hilo_kernel(const int32_t* __restrict
   }
 }
 
-// one 1024-thread workgroup: thread t owns nodes [t c, t c + c); pm[] (global scratch) holds the
-// prefix max of hi within the thread's range between its two sweeps
-__global__ void __launch_bounds__(1024) seg_build_kernel(const int32_t* __restrict__ lo,
-                                                         const int32_t* __restrict__ hi,
-                                                         int32_t* __restrict__ pm, int64_t N,
-                                                         int max_rows, int32_t* __restrict__ segs,
-                                                         int32_t* __restrict__ seg_count) {
-  __shared__ int sh_a[1024], sh_b[1024];
-  __shared__ int bnd[kSegMax + 2];
-  __shared__ int total;
+// scan pass 1 (one 1024-node tile per workgroup): within-tile inclusive prefix max of hi and
+// suffix min of lo per node, and the tile's aggregates
+__global__ void __launch_bounds__(1024) seg_tile_kernel(const int32_t* __restrict__ lo,
+                                                        const int32_t* __restrict__ hi, int64_t N,
+                                                        int32_t* __restrict__ phi,
+                                                        int32_t* __restrict__ slo,
+                                                        int32_t* __restrict__ agg) {
+  __shared__ int sa[1024], sb[1024];
   const int t = threadIdx.x;
+  const int64_t d = (int64_t)blockIdx.x * 1024 + t;
   const int n = (int)N;
-  const int c = (n + 1023) / 1024;
-  const int r0 = min(n, t * c), r1 = min(n, r0 + c);
-  int tmax = -1, tmin = n;
-  for (int d = r0; d < r1; ++d) {
-    tmax = max(tmax, hi[d]);
-    pm[d] = tmax;   // max of hi over [r0, d]
-    tmin = min(tmin, lo[d]);
-  }
-  sh_a[t] = tmax;
-  sh_b[t] = tmin;
+  sa[t] = d < N ? hi[d] : -1;
+  sb[t] = d < N ? lo[d] : n;
   __syncthreads();
-  // exclusive prefix max of tmax, exclusive suffix min of tmin (Hillis-Steele in LDS)
   for (int off = 1; off < 1024; off <<= 1) {
-    const int a = t >= off ? sh_a[t - off] : -1;
-    const int b = t + off < 1024 ? sh_b[t + off] : n;
+    const int a = t >= off ? sa[t - off] : -1;
+    const int b = t + off < 1024 ? sb[t + off] : n;
     __syncthreads();
-    sh_a[t] = max(sh_a[t], a);
-    sh_b[t] = min(sh_b[t], b);
-    __syncthreads();
-  }
-  const int pmax_before = t > 0 ? sh_a[t - 1] : -1;   // max hi over d < r0
-  const int smin_after = t < 1023 ? sh_b[t + 1] : n;  // min lo over d >= r1
-  __syncthreads();
-  // boundaries b in (r0, r1] with 0 < b < n, swept backwards (suffix min of lo within range)
-  int cnt = 0, sm = smin_after;
-  for (int b = r1; b > r0; --b) {
-    if (b < n) {
-      const int before = max(pmax_before, pm[b - 1]);
-      if (before < b && sm >= b) ++cnt;
-    }
-    sm = min(sm, lo[b - 1]);
-  }
-  sh_a[t] = cnt;
-  __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {   // inclusive prefix sum of the counts
-    const int a = t >= off ? sh_a[t - off] : 0;
-    __syncthreads();
-    sh_a[t] += a;
+    sa[t] = max(sa[t], a);
+    sb[t] = min(sb[t], b);
     __syncthreads();
   }
-  if (t == 1023) total = sh_a[1023];
-  __syncthreads();
-  const int nb = total;   // free boundaries strictly inside (0, n)
-  if (nb <= kSegMax) {
-    int k = sh_a[t] - cnt;   // this thread's first slot (ascending order within the thread)
-    // forward order: recompute validity forwards is not possible for the suffix min, so write
-    // the backward sweep's hits from the top of the thread's slot range down
-    int slot = k + cnt - 1;
-    sm = smin_after;
-    for (int b = r1; b > r0; --b) {
-      if (b < n) {
-        const int before = max(pmax_before, pm[b - 1]);
-        if (before < b && sm >= b) bnd[1 + slot--] = b;
-      }
-      sm = min(sm, lo[b - 1]);
-    }
+  if (d < N) {
+    phi[d] = sa[t];
+    slo[d] = sb[t];
   }
-  __syncthreads();
   if (t == 0) {
-    int count = 0;
-    if (n == 0) {
-      segs[0] = 0;
-    } else if (nb > kSegMax) {
-      count = -1;
-    } else {
-      bnd[0] = 0;
-      bnd[nb + 1] = n;
-      // greedy packing of the gap-free runs [bnd[i], bnd[i+1]) into blocks of <= max_rows nodes
-      int start = 0;
-      segs[0] = 0;
-      for (int i = 1; i <= nb + 1 && count >= 0; ++i) {
-        const int b = bnd[i], prev = bnd[i - 1];
-        if (b - prev > max_rows) {
-          count = -1;
-        } else if (b - start > max_rows) {
-          segs[++count] = prev;
-          start = prev;
-        }
-      }
-      if (count >= 0) segs[++count] = n;
-    }
-    *seg_count = count;
+    agg[2 * blockIdx.x] = sa[1023];
+    agg[2 * blockIdx.x + 1] = sb[0];
   }
+}
+
+// scan pass 2: every free boundary b (0 < b < N: max_{d<b} hi[d] < b and min_{d>=b} lo[d] >= b)
+// appended to list[] (unordered; at most kSegMax kept, the count is exact)
+__global__ void __launch_bounds__(1024) seg_free_kernel(const int32_t* __restrict__ phi,
+                                                        const int32_t* __restrict__ slo,
+                                                        const int32_t* __restrict__ agg,
+                                                        int64_t N, int ntiles,
+                                                        int32_t* __restrict__ list,
+                                                        int32_t* __restrict__ count) {
+  __shared__ int pre_hi, suf_lo;
+  const int t = threadIdx.x, k = blockIdx.x;
+  const int n = (int)N;
+  if (t == 0) {   // aggregates of the tiles before / after this one (<= 128 tiles)
+    int a = -1, b = n;
+    for (int i = 0; i < k; ++i) a = max(a, agg[2 * i]);
+    for (int i = k + 1; i < ntiles; ++i) b = min(b, agg[2 * i + 1]);
+    pre_hi = a;
+    suf_lo = b;
+  }
+  __syncthreads();
+  const int64_t bd = (int64_t)k * 1024 + t;   // boundary between nodes bd - 1 and bd
+  if (bd <= 0 || bd >= N) return;
+  const int before = t > 0 ? max(pre_hi, phi[bd - 1]) : pre_hi;   // max hi over d < bd
+  const int after = min(suf_lo, slo[bd]);                           // min lo over d >= bd
+  if (before < (int)bd && after >= (int)bd) {
+    const int slot = atomicAdd(count, 1);
+    if (slot < kSegMax) list[slot] = (int)bd;
+  }
+}
+
+// pack: sort the free boundaries (rank by counting, in LDS) and pack the gap-free runs greedily
+// into blocks of <= max_rows nodes (thread 0)
+__global__ void __launch_bounds__(1024) seg_pack_kernel(const int32_t* __restrict__ list,
+                                                        const int32_t* __restrict__ count_in,
+                                                        int64_t N, int max_rows,
+                                                        int32_t* __restrict__ segs,
+                                                        int32_t* __restrict__ seg_count) {
+  __shared__ int in[kSegMax], bnd[kSegMax + 2];
+  const int t = threadIdx.x, n = (int)N;
+  const int nb = *count_in;
+  if (nb > kSegMax) {
+    if (t == 0) *seg_count = -1;
+    return;
+  }
+  for (int i = t; i < nb; i += 1024) in[i] = list[i];
+  __syncthreads();
+  for (int i = t; i < nb; i += 1024) {   // boundaries are distinct: rank = # smaller
+    const int v = in[i];
+    int r = 0;
+    for (int j = 0; j < nb; ++j) r += in[j] < v;
+    bnd[1 + r] = v;
+  }
+  __syncthreads();
+  if (t != 0) return;
+  bnd[0] = 0;
+  bnd[nb + 1] = n;
+  int count = 0, start = 0;
+  segs[0] = 0;
+  if (n > 0) {
+    for (int i = 1; i <= nb + 1 && count >= 0; ++i) {
+      const int b = bnd[i], prev = bnd[i - 1];
+      if (b - prev > max_rows) {
+        count = -1;
+      } else if (b - start > max_rows) {
+        segs[++count] = prev;
+        start = prev;
+      }
+    }
+    if (count >= 0) segs[++count] = n;
+  }
+  *seg_count = count;
 }
 
 __global__ void seg_none_kernel(int32_t* seg_count) {
@@ -1034,7 +1041,9 @@ __global__ void seg_none_kernel(int32_t* seg_count) {
 }
 
 extern "C" size_t gatx_graph_segments_workspace_bytes(int64_t N) {
-  return 3 * align256(sizeof(int32_t) * (size_t)(N > 0 ? N : 1));
+  const size_t nn = align256(sizeof(int32_t) * (size_t)(N > 0 ? N : 1));
+  return 4 * nn + align256(sizeof(int32_t) * (2 * (size_t)ceil_div(N > 0 ? N : 1, 1024) + 1)) +
+         align256(sizeof(int32_t) * kSegMax);
 }
 
 extern "C" int gatx_graph_segments(const int32_t* rowptr, const int32_t* col, int64_t N,
@@ -1048,16 +1057,31 @@ extern "C" int gatx_graph_segments(const int32_t* rowptr, const int32_t* col, in
     return 0;
   }
   GATX_REQUIRE(ws_bytes >= gatx_graph_segments_workspace_bytes(N), "graph_segments: workspace");
+  const size_t nn = align256(sizeof(int32_t) * (size_t)(N > 0 ? N : 1));
+  const int ntiles = (int)ceil_div(N > 0 ? N : 1, (int64_t)1024);
   char* p = (char*)ws;
-  int32_t* lo = (int32_t*)p; p += align256(sizeof(int32_t) * (size_t)(N > 0 ? N : 1));
-  int32_t* hi = (int32_t*)p; p += align256(sizeof(int32_t) * (size_t)(N > 0 ? N : 1));
-  int32_t* pm = (int32_t*)p;
+  int32_t* lo = (int32_t*)p; p += nn;
+  int32_t* hi = (int32_t*)p; p += nn;
+  int32_t* phi = (int32_t*)p; p += nn;
+  int32_t* slo = (int32_t*)p; p += nn;
+  int32_t* agg = (int32_t*)p; p += align256(sizeof(int32_t) * (2 * (size_t)ntiles + 1));
+  int32_t* list = (int32_t*)p;
+  int32_t* cnt = agg + 2 * ntiles;
+  const hipError_t me = hipMemsetAsync(cnt, 0, sizeof(int32_t), st);
+  if (me != hipSuccess) {
+    set_error("graph_segments: %s", hipGetErrorString(me));
+    return (int)me;
+  }
   if (N > 0) {
     seg_hilo_kernel<<<(unsigned)ceil_div(N, (int64_t)4), 256, 0, st>>>(rowptr, col, N, lo, hi);
     GATX_LAUNCH_CHECK("graph_segments hilo");
+    seg_tile_kernel<<<(unsigned)ntiles, 1024, 0, st>>>(lo, hi, N, phi, slo, agg);
+    GATX_LAUNCH_CHECK("graph_segments tile");
+    seg_free_kernel<<<(unsigned)ntiles, 1024, 0, st>>>(phi, slo, agg, N, ntiles, list, cnt);
+    GATX_LAUNCH_CHECK("graph_segments free");
   }
-  seg_build_kernel<<<1, 1024, 0, st>>>(lo, hi, pm, N, max_rows, segs, seg_count);
-  GATX_LAUNCH_CHECK("graph_segments build");
+  seg_pack_kernel<<<1, 1024, 0, st>>>(list, cnt, N, max_rows, segs, seg_count);
+  GATX_LAUNCH_CHECK("graph_segments pack");
   return 0;
 }
 

@@ -342,6 +342,15 @@ def _edge_pass(rows, row_stride, S, M_ord, graph, sh, bias, p, seed, out, resid_
                  *(drop_args if last else (0.0, None)), None, s)
 
 
+def lds_blocks(graph: Graph, sh: LayerShape):
+    """(segs, count, n_blocks) when this layer's edge pass takes the LDS-staged kernels
+    (csrc/edge_lds.hip; tuning edge_lds): a concat layer of <= 8 heads on a graph whose node
+    blocks (gatx_graph_segments) fit the LDS image; else None."""
+    if not tuning.get("edge_lds") or not sh.concat or sh.NH > 8:
+        return None
+    return graph.lds_blocks(lib.gatx_edge_lds_rows())
+
+
 def fold_scores_into_gemm(sh: LayerShape) -> bool:
     """Compute S as 2NH extra GEMM columns only when they fit the last column tile for free;
     otherwise (e.g. Dp = 1024: a whole extra 128-wide tile, +12% GEMM time) project Wh alone and
@@ -525,6 +534,25 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
         with _span("attention_max", (E2, sh.NH)):
             call("gatx_attention_max", ptr(graph.col), ptr(graph.rowidx), E2, graph.e2_ptr,
                  ptr(S), sh.NH, ptr(M_ord), ptr(argmax), ptr(_max_ws(dev)), s)
+    blocks = lds_blocks(graph, sh)
+    if blocks is not None:
+        # LDS-staged edge pass (csrc/edge_lds.hip): records (den, alpha, ties, {4 src, alpha~}
+        # per head and CSR slot), then one workgroup per (node block, head, 16-float chunk)
+        segs, count, nblocks = blocks
+        rec = torch.empty((sh.NH, max(E2, 1)), dtype=torch.int64, device=dev)
+        with _span("edge_records", (E2, sh.NH)):
+            call("gatx_edge_records", ptr(S), ptr(M_ord), ptr(graph.rowptr), ptr(graph.col),
+                 ptr(graph.perm), N, E2, sh.NH, int(sh.const), float(p), ptr(seed), ptr(rec),
+                 ptr(den), ptr(alpha) if want_alpha else None,
+                 ptr(argmax) if want_alpha else None, s)
+        with _span("edge_forward", (N, E2, sh.NH, sh.F, sh.concat)):
+            call("gatx_edge_lds_forward", ptr(Wh), sh.Dp, ptr(graph.rowptr), ptr(rec), E2,
+                 ptr(segs), ptr(count), nblocks, sh.NH, sh.F, ptr(bias), ptr(out), sh.out_cols,
+                 resid_p, sh.out_cols, int(elu), *drop_args, s)
+        if not want_alpha:
+            alpha = LazyAlpha(graph, S, M_ord, den, sh, argmax)
+        saved.update(Wh=Wh, S=S, reassoc=False)
+        return out, alpha, saved
     with _span("edge_forward", (N, E2, sh.NH, sh.F, sh.concat)):   # local + generic: one record
         _edge_pass(Wh, sh.Dp, S, M_ord, graph, sh, bias, p, seed, out, resid_p, elu, den, chunk,
                    drop_args, dev, s)

@@ -226,7 +226,9 @@ class Graph:
     def node_blocks(self, max_rows: int):
         """(segs, count) of gatx_graph_segments for this CSR (device tensors, built once per graph
         and max_rows): contiguous node blocks no edge crosses, each <= max_rows nodes; count -1
-        when the graph has none (a gap-free run longer than max_rows)."""
+        when the graph has none (a gap-free run longer than max_rows). The workspace is a
+        per-device scratch that lives as long as the process (stream-ordered reuse), so no
+        buffer a captured step reads is ever freed and handed to another allocation."""
         key = ("blocks", max_rows)
         hit = self._hub_plans.get(key)
         if hit is None:
@@ -235,11 +237,32 @@ class Graph:
                                device=dev)
             count = torch.empty(1, dtype=torch.int32, device=dev)
             wb = _lib.lib.gatx_graph_segments_workspace_bytes(self.num_nodes)
-            ws = torch.empty(max(wb, 1), dtype=torch.uint8, device=dev)
+            ws = _seg_ws(dev, wb)
             call("gatx_graph_segments", ptr(self.rowptr), ptr(self.col), self.num_nodes,
                  int(max_rows), ptr(segs), ptr(count), ptr(ws), wb, stream())
             hit = self._hub_plans[key] = (segs, count)
         return hit
+
+    def lds_blocks(self, max_rows: int):
+        """(segs, count, n_blocks) of node_blocks(max_rows) when this edge_index is known to cut
+        into such blocks, else None. Known: decided once per edge_index tensor (storage, version,
+        shape, node count) by one read of the device count (outside a capture), cached across
+        graph rebuilds (clear_graph_cache) — the same identity the graph cache keys on; inside a
+        capture an undecided graph takes the L2-gather pass."""
+        key = _hint_key(self.source, self.num_nodes, self.add_self_loops) + (
+            version(self.source), max_rows)
+        known = _BLOCKS.get(key)
+        if known is None:
+            if torch.cuda.is_current_stream_capturing():
+                return None
+            segs, count = self.node_blocks(max_rows)
+            known = _BLOCKS[key] = int(count.item())
+            while len(_BLOCKS) > 64:
+                _BLOCKS.pop(next(iter(_BLOCKS)))
+        if known <= 0:
+            return None
+        segs, count = self.node_blocks(max_rows)
+        return segs, count, known
 
     def csr_host(self):
         """(rowptr, col, perm) as CPU tensors — for tests."""
@@ -250,6 +273,7 @@ class Graph:
 _META_WS = {}
 _PENDING: list = []
 _HINTS: dict = {}
+_BLOCKS: dict = {}   # edge_index identity -> node-block count (<= 0: no LDS-staged passes)
 
 
 def _hint_key(edge_index: torch.Tensor, num_nodes, add_self_loops: bool):
@@ -271,6 +295,24 @@ def expect_num_edges(edge_index: torch.Tensor, num_nodes: int, add_self_loops: b
         _HINTS.pop(k, None)
     else:
         _HINTS[k] = int(num_edges)
+
+
+_SEG_WS: dict = {}
+_SEG_WS_RETIRED: list = []
+
+
+def _seg_ws(dev, nbytes: int):
+    """Per-device scratch of gatx_graph_segments, grown to the largest graph seen and never
+    freed (a captured step's launches keep its address)."""
+    t = _SEG_WS.get(dev)
+    if t is None or t.numel() < nbytes:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("gatx: node-block scratch must be sized before a capture (run "
+                               "the step once eagerly)")
+        if t is not None:
+            _SEG_WS_RETIRED.append(t)   # a captured graph may still launch on the old one
+        t = _SEG_WS[dev] = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
+    return t
 
 
 def _meta_ws(dev):

@@ -414,7 +414,7 @@ int gatx_pad_rows(const float* src, int64_t rows, int64_t cols, int64_t ld_src, 
  * + gatx_attention_alpha_ei on such graphs (models/gat_layer.py:84-135):
  * gatx_edge_records — one wave per destination, all heads: den (bitwise the L2-gather pass's),
  *   alpha in edge_index' order (nullable), max()'s tied argmax entries (nullable; counter reset by
- *   gatx_attention_max), and per (head, CSR slot) an 8-byte record {4 * src, alpha~} in rec
+ *   gatx_attention_max), and per (head, CSR slot) an 8-byte record {64 * src, alpha~} in rec
  *   ([NH][E_bound] x 8 B; alpha~ = alpha after the attention dropout). NH <= 8.
  * gatx_edge_lds_forward — concat layers: one workgroup per (node block, head, 16-float chunk)
  *   stages that chunk of every row of its block in LDS and sums alpha~ x row over each

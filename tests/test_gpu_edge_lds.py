@@ -1,0 +1,126 @@
+"""The LDS-staged edge forward (csrc/edge_lds.hip, gatx.tuning edge_lds=1): concat layers on
+graphs that cut into node blocks of <= 2304 nodes stage one 16-float chunk of every row of a
+block in LDS and aggregate from there (records pass: den, alpha, max() ties and per-edge
+{row, alpha~} records). Parity: every reference golden (layers, models, task steps' gradients
+through the unchanged backward) as test_gpu_layer.py checks them, and the L2-gather pass's results
+to fp32 summation order on the headline batch."""
+import numpy as np
+import pytest
+import torch
+
+from golden_io import LAYER_CASES, MODEL_CASES
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def lds_on():
+    from gatx import tuning
+    tuning.set(edge_lds=1)
+    yield
+    tuning.reset()
+
+
+def _took_lds(c, device):
+    """Whether this golden's layer takes the LDS-staged pass (concat, <= 8 heads, blocks fit)."""
+    import gatx
+    from gatx import functional as gf
+    from gatx.graph import graph_cache
+    m = c["meta"]
+    ei = torch.from_numpy(np.ascontiguousarray(c["edge_index"])).to(device)
+    gatx.clear_graph_cache()
+    g = graph_cache.get(ei, c["x"].shape[0], m["add_self_loops"])
+    sh = gf.LayerShape(m["num_heads"], m["out_features"], m["in_features"], m["concat"],
+                       m["const_attention"])
+    return gf.lds_blocks(g, sh) is not None and not gf.use_reassociation(sh)
+
+
+@pytest.mark.parametrize("name", LAYER_CASES)
+def test_layer_goldens_lds(name, device, lds_on):
+    from test_gpu_layer import test_layer_matches_reference_goldens
+    test_layer_matches_reference_goldens(name, device)
+
+
+def test_lds_path_is_taken(device, lds_on):
+    from golden_io import load_layer_case
+    took = {n: _took_lds(load_layer_case(n), device) for n in
+            ("ppi_small_l1", "ppi_full_l1", "edge_dropout", "edge_bias", "edge_odd_widths",
+             "edge_trailing_isolated", "cora_l0_trained", "ppi_small_l2")}
+    assert took["ppi_small_l1"] and took["ppi_full_l1"]
+    assert not took["cora_l0_trained"]    # one 2708-node component: no block fits the image
+    assert not took["ppi_small_l2"]       # head mean: the L2-gather pass
+    assert not took["edge_dropout"]       # narrow input: the reassociated first-layer pass
+
+
+@pytest.mark.parametrize("G,n,e,fin,NH,F,dropout", [
+    (3, 300, 4000, 64, 2, 16, 0.0),       # several blocks
+    (3, 300, 4000, 64, 2, 16, 0.6),       # attention dropout through the records
+    (2, 200, 3000, 16, 3, 7, 0.0),        # F % 4 != 0: scalar epilogue, padded chunk
+    (1, 2245, 61318, 512, 8, 64, 0.0),    # one full PPI-size graph, 8 heads
+    (1, 2300, 20000, 64, 4, 20, 0.0),     # a block near the 2304-row image
+    (2, 2000, 9000, 96, 4, 40, 0.3),      # blocks packed over two graphs
+])
+def test_lds_vs_oracle(G, n, e, fin, NH, F, dropout, device, lds_on):
+    from test_gpu_layer import _layer_vs_oracle
+    _layer_vs_oracle(device, G, n, e, fin, NH, F, True, dropout=dropout)
+
+
+@pytest.mark.parametrize("name", MODEL_CASES)
+def test_model_goldens_lds(name, device, lds_on):
+    from test_gpu_layer import test_model_matches_reference_goldens
+    test_model_matches_reference_goldens(name, device)
+
+
+def test_headline_batch_lds_equals_gather(device):
+    """The 20-graph PPI batch: the LDS-staged forward against the L2-gather forward (both checked
+    against the reference elsewhere) — outputs to fp32 summation order, alphas bitwise where the
+    layer inputs agree (the records pass sums the denominators exactly as the gather pass does)."""
+    import gatx
+    from gatx import data as gd
+    from gatx import tuning
+    from gatx.config import data_config
+    torch.manual_seed(0)
+    model = gatx.GATModel(**data_config["PPI"]).to(device).eval()
+    b = gd.dataset_batch("PPI", 20, graph_seed=42, feature_seed=1)
+    x = torch.from_numpy(b.x).to(device)
+    ei = torch.from_numpy(b.edge_index).to(device)
+    res = []
+    for lds in (0, 1):
+        tuning.set(edge_lds=lds)
+        gatx.clear_graph_cache()
+        with torch.no_grad():
+            out, _, al = model.forward_and_return_attention(x, ei)
+        res.append((out.clone(), [a.clone() for a in al]))
+    tuning.reset()
+    (o0, a0), (o1, a1) = res
+    assert float((o0 - o1).abs().max()) <= 1e-5 * max(1.0, float(o0.abs().max()))
+    # layers 0 (reassociated: the gather pass in both runs) and 1 (LDS-staged) see identical
+    # inputs: their alphas agree bitwise; layer 2's input differs in the last bits
+    assert torch.equal(a0[0], a1[0]) and torch.equal(a0[1], a1[1])
+    assert float((a0[2] - a1[2]).abs().max()) <= 1e-6
+
+
+def test_captured_forward_lds(device, lds_on):
+    """A captured forward that rebuilds its CSR every replay takes the LDS path once the
+    edge_index's blocks are known (decided by the warm-up), and replays equal the eager step."""
+    import gatx
+    from gatx import data as gd
+    from gatx.capture import CapturedStep
+    from gatx.config import data_config
+    torch.manual_seed(0)
+    model = gatx.GATModel(**data_config["PPI"]).to(device).eval()
+    b = gd.dataset_batch("PPI", 3, graph_seed=5, feature_seed=6)
+    x = torch.from_numpy(b.x).to(device)
+    ei = torch.from_numpy(b.edge_index).to(device)
+
+    def step():
+        gatx.clear_graph_cache()
+        with torch.no_grad():
+            return model(x, ei)
+
+    ref = step().clone()
+    cap = CapturedStep(step)
+    for _ in range(5):
+        out = cap()
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)

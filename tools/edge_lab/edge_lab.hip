@@ -198,6 +198,84 @@ __global__ void __launch_bounds__(1024) lds2_kernel(const float* __restrict__ Wh
   }
 }
 
+
+// ---- v3: records hold the source row's absolute byte offset 64 src; the quad broadcast is a
+// legacy mov_dpp (undef old value), so the compiler can fold it into the address add
+// (v_add_u32_dpp); weights broadcast the same way
+template <int T>
+__device__ inline int qb3(int v) {
+  return __builtin_amdgcn_mov_dpp(v, T | (T << 2) | (T << 4) | (T << 6), 0xf, 0xf, true);
+}
+template <int RPL>
+__global__ void __launch_bounds__(1024) lds3_kernel(const float* __restrict__ Wh,
+                                                    const int* __restrict__ rowptr,
+                                                    const int2* __restrict__ rec,
+                                                    const int* __restrict__ seg,
+                                                    int E, float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) float4 rows[MAXR * 4];
+  const int64_t b = xcd_contiguous(blockIdx.x, gridDim.x);
+  const int c = (int)(b % NCH);
+  const int h = (int)((b / NCH) % NH);
+  const int gi = (int)(b / (NCH * NH));
+  const int n0 = seg[gi], R = seg[gi + 1] - n0;
+  const int tid = threadIdx.x;
+  const float4* src4 = (const float4*)Wh;
+  for (int r = tid >> 2; r < R; r += 256)
+    rows[r * 4 + (tid & 3)] = src4[(int64_t)(n0 + r) * (NH * F / 4) + h * (F / 4) + c * 4 + (tid & 3)];
+  __syncthreads();
+  const int lane = tid & 63, wave = tid >> 6, q = lane & 3, j = lane >> 2;
+  const int2* rh = rec + (int64_t)h * E;
+  const int qb = 16 * q - 64 * n0;   // byte offset of this lane's piece, minus the block base
+  const char* img = (const char*)rows;
+  constexpr int G = 4 * RPL;
+  for (int d0 = wave * 16; d0 < R; d0 += 256) {
+    const int dl = d0 + j;
+    const bool live = dl < R;
+    int e = live ? rowptr[n0 + dl] : 0;
+    const int end = live ? rowptr[n0 + dl + 1] : 0;
+    const int last = end > 0 ? end - 1 : 0;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    int2 ra[RPL], rb[RPL];
+    bool va[RPL], vb[RPL];
+    auto load = [&](int2 (&r)[RPL], bool (&ok)[RPL], int e0) {
+#pragma unroll
+      for (int u = 0; u < RPL; ++u) {
+        const int ee = e0 + q * RPL + u;
+        ok[u] = ee < end;
+        r[u] = rh[min(ee, last)];
+      }
+    };
+    auto consume = [&](const int2 (&cur)[RPL], const bool (&ok)[RPL]) {
+#pragma unroll
+      for (int u = 0; u < RPL; ++u) {
+        const int cx = ok[u] ? cur[u].x : 64 * n0;
+        const int cy = ok[u] ? cur[u].y : 0;
+#define STEP(T)                                                                              \
+        {                                                                                    \
+          const float4 v = *(const float4*)(img + (qb3<T>(cx) + qb));                        \
+          const float w = __int_as_float(qb3<T>(cy));                                        \
+          acc.x += w * v.x; acc.y += w * v.y; acc.z += w * v.z; acc.w += w * v.w;            \
+        }
+        STEP(0) STEP(1) STEP(2) STEP(3)
+#undef STEP
+      }
+    };
+    int need = (end - e + G - 1) / G;
+    for (int off = 4; off < 64; off <<= 1) need = max(need, __shfl_xor(need, off));
+    const int trips = __builtin_amdgcn_readfirstlane(need);
+    load(ra, va, e);
+    for (int it = 0; it < trips; it += 2) {
+      load(rb, vb, e + G);
+      consume(ra, va);
+      load(ra, va, e + 2 * G);
+      consume(rb, vb);
+      e += 2 * G;
+    }
+    if (live)
+      ((float4*)out)[(int64_t)(n0 + dl) * (NH * F / 4) + h * (F / 4) + c * 4 + q] = acc;
+  }
+}
+
 __global__ void clobber(float4* p, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     p[i] = make_float4(1.f, (float)i, 0.f, 0.f);
@@ -206,7 +284,8 @@ __global__ void clobber(float4* p, int64_t n) {
 static uint64_t s_ = 88172645463325252ull;
 static uint32_t rnd() { s_ ^= s_ << 13; s_ ^= s_ >> 7; s_ ^= s_ << 17; return (uint32_t)s_; }
 
-int main() {
+int main(int argc, char** argv) {
+  const bool quick = argc > 1;   // one timed run of each kernel (counter passes)
   // graph: per graph EPG random edges + self loops, CSR by destination
   std::vector<std::vector<int>> in(N);
   for (int g = 0; g < G; ++g) {
@@ -221,7 +300,7 @@ int main() {
   const int E = rowptr[N];
   std::vector<float> wt((size_t)NH * E);
   for (auto& x : wt) x = (rnd() % 1000) / 1000.f;
-  std::vector<int2> rec((size_t)NH * E), rec2((size_t)NH * E);
+  std::vector<int2> rec((size_t)NH * E), rec2((size_t)NH * E), rec3((size_t)NH * E);
   std::vector<int> seg(G + 1);
   for (int g = 0; g <= G; ++g) seg[g] = g * NPG;
   for (int h = 0; h < NH; ++h)
@@ -231,23 +310,25 @@ int main() {
         float w = wt[(size_t)h * E + e];
         rec[(size_t)h * E + e] = make_int2((col[e] - n0) * 64, *(int*)&w);
         rec2[(size_t)h * E + e] = make_int2(col[e] * 4, *(int*)&w);
+        rec3[(size_t)h * E + e] = make_int2(col[e] * 64, *(int*)&w);
       }
   std::vector<float> Wh((size_t)N * NH * F);
   for (auto& x : Wh) x = ((int)(rnd() % 2001) - 1000) / 1000.f;
   printf("N=%d E'=%d\n", N, E);
 
-  float *dWh, *dwt, *dout, *dout2; int *drp, *dcol, *dseg; int2* drec; int2* drec2; float4* junk;
+  float *dWh, *dwt, *dout, *dout2; int *drp, *dcol, *dseg; int2* drec; int2* drec2; int2* drec3; float4* junk;
   const int64_t JN = 320ll << 20 >> 4;
   CK(hipMalloc(&dWh, Wh.size() * 4)); CK(hipMalloc(&dwt, wt.size() * 4));
   CK(hipMalloc(&dout, (size_t)N * NH * F * 4)); CK(hipMalloc(&dout2, (size_t)N * NH * F * 4));
   CK(hipMalloc(&drp, rowptr.size() * 4)); CK(hipMalloc(&dcol, col.size() * 4));
-  CK(hipMalloc(&drec, rec.size() * 8)); CK(hipMalloc(&drec2, rec2.size() * 8)); CK(hipMalloc(&dseg, seg.size() * 4)); CK(hipMalloc(&junk, JN * 16));
+  CK(hipMalloc(&drec, rec.size() * 8)); CK(hipMalloc(&drec2, rec2.size() * 8)); CK(hipMalloc(&drec3, rec3.size() * 8)); CK(hipMalloc(&dseg, seg.size() * 4)); CK(hipMalloc(&junk, JN * 16));
   CK(hipMemcpy(dWh, Wh.data(), Wh.size() * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(dwt, wt.data(), wt.size() * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(drp, rowptr.data(), rowptr.size() * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(dcol, col.data(), col.size() * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(drec, rec.data(), rec.size() * 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(drec2, rec2.data(), rec2.size() * 8, hipMemcpyHostToDevice));
+  CK(hipMemcpy(drec3, rec3.data(), rec3.size() * 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(dseg, seg.data(), seg.size() * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(dout2, Wh.data(), Wh.size() * 4, hipMemcpyHostToDevice));   // pristine copy of Wh
   hipEvent_t a, bb; CK(hipEventCreate(&a)); CK(hipEventCreate(&bb));
@@ -286,13 +367,22 @@ int main() {
   auto l4 = [&] { lds_kernel<4><<<G * NH * NCH, 1024>>>(dWh, drp, drec, dseg, E, dout); };
   auto m1 = [&] { lds2_kernel<1><<<G * NH * NCH, 1024>>>(dWh, drp, drec2, dseg, E, dout); };
   auto m2 = [&] { lds2_kernel<2><<<G * NH * NCH, 1024>>>(dWh, drp, drec2, dseg, E, dout); };
+  auto k1 = [&] { lds3_kernel<1><<<G * NH * NCH, 1024>>>(dWh, drp, drec3, dseg, E, dout); };
+  auto k2 = [&] { lds3_kernel<2><<<G * NH * NCH, 1024>>>(dWh, drp, drec3, dseg, E, dout); };
   auto m4 = [&] { lds2_kernel<4><<<G * NH * NCH, 1024>>>(dWh, drp, drec2, dseg, E, dout); };
   (void)l2;
+  if (quick) {
+    run("gather (library-like)", g1, dout, true);
+    run("lds2 RPL=2", m2, dout, true);
+    run("lds3 RPL=2", k2, dout, true);
+    return 0;
+  }
   for (int rep = 0; rep < 2; ++rep) {
     run("gather (library-like)", g1, dout, true);
     run("lds2 RPL=1", m1, dout, true);
     run("lds2 RPL=2", m2, dout, true);
-    run("lds2 RPL=4", m4, dout, true);
+    run("lds3 RPL=1", k1, dout, true);
+    run("lds3 RPL=2", k2, dout, true);
     run("lds2 RPL=2 warm", m2, dout, false);
   }
   return 0;
