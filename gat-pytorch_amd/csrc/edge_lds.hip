@@ -179,6 +179,7 @@ struct LdsArgs {
   const int32_t* segs;       // block b = nodes [segs[b], segs[b + 1])
   const int32_t* seg_count;
   int64_t seg_bound;         // grid's block dimension (>= *seg_count)
+  int64_t N;
   int NH, F, Fp, nchunks;
   const float* bias;         // [NH * F] or nullptr
   float* out;
@@ -191,11 +192,12 @@ struct LdsArgs {
   int vec_out;               // F % 4 == 0 and 16-byte aligned rows of out / resid
 };
 
+template <bool DROP>
 __device__ inline float lds_epilogue(float v, const LdsArgs& g, int64_t n, int64_t col) {
   if (g.bias) v += g.bias[col];
   if (g.resid) v += g.resid[n * g.resid_ld + col];
   if (g.elu) v = elu_act(v);
-  if (g.out_p > 0.f)
+  if (DROP)
     v = dropout_keep(*g.out_seed, n * (int64_t)(g.NH * g.F) + col, g.out_p) ? v * (1.f / (1.f - g.out_p))
                                                                           : 0.f;
   return v;
@@ -208,15 +210,91 @@ __device__ inline int quad_bcast(int v) {
   return __builtin_amdgcn_mov_dpp(v, T | (T << 2) | (T << 4) | (T << 6), 0xf, 0xf, true);
 }
 
+// the walk's epilogue for destination n, features [f0, f0 + 4) of column block cb = h F + f0
+template <bool DROP>
+__device__ inline void lds_store(const LdsArgs& g, int64_t n, int64_t cb, int f0, float4 acc) {
+  float* orow = g.out + n * g.out_ld;
+  if (g.vec_out) {
+    float4 o = acc;
+    if (g.bias) o = add4(o, *(const float4*)(g.bias + cb));
+    if (g.resid) o = add4(o, *(const float4*)(g.resid + n * g.resid_ld + cb));
+    if (g.elu) {
+      o.x = elu_act(o.x); o.y = elu_act(o.y); o.z = elu_act(o.z); o.w = elu_act(o.w);
+    }
+    if (DROP) {
+      const float sc = 1.f / (1.f - g.out_p);
+      const int64_t base = n * (int64_t)(g.NH * g.F) + cb;
+      const uint64_t sd = *g.out_seed;
+      o.x = dropout_keep(sd, base, g.out_p) ? o.x * sc : 0.f;
+      o.y = dropout_keep(sd, base + 1, g.out_p) ? o.y * sc : 0.f;
+      o.z = dropout_keep(sd, base + 2, g.out_p) ? o.z * sc : 0.f;
+      o.w = dropout_keep(sd, base + 3, g.out_p) ? o.w * sc : 0.f;
+    }
+    *(float4*)(orow + cb) = o;
+  } else {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      if (f0 + t < g.F) orow[cb + t] = lds_epilogue<DROP>(get4(acc, t), g, n, cb + t);
+  }
+}
+
+// a value another kernel of the same step wrote, read past the scalar / vector L1 caches
+__device__ inline int coherent_load(const int32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Fallback walk when the graph no longer cuts into at most seg_bound blocks (a captured step
+// replayed on edges whose node blocks differ from the ones its launch was sized for): the
+// workgroups split the node range evenly and gather rows from global memory. Correct, slow, and
+// never taken by a step whose edges kept their block structure.
+template <bool DROP>
+__device__ void lds_global_walk(const LdsArgs& g, int64_t k, int c, int h) {
+  const int64_t per = ceil_div(g.N, g.seg_bound);
+  const int64_t n0 = k * per;
+  const int64_t R = min(per, g.N - n0);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane & 3, j = lane >> 2;
+  const int f0 = c * kChunk + q * 4;
+  const int2* rh = g.rec + (int64_t)h * g.E_bound;
+  const float* base = g.rows + (int64_t)h * g.Fp + f0;
+  for (int64_t d0 = wave * 16; d0 < R; d0 += 256) {
+    if (d0 + j >= R) continue;
+    const int64_t n = n0 + d0 + j;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (f0 < g.Fp)
+      for (int e = g.rowptr[n], end = g.rowptr[n + 1]; e < end; ++e) {
+        const int2 r = rh[e];
+        const float4 v = *(const float4*)(base + (int64_t)(r.x >> 6) * g.row_stride);
+        acc = fma4(__int_as_float(r.y), v, acc);
+      }
+    if (f0 < g.F) lds_store<DROP>(g, n, (int64_t)h * g.F + f0, f0, acc);
+  }
+}
+
 // RPL records per lane (4 RPL per quad per group), groups loaded unconditionally (clamped index,
 // out-of-range records masked when consumed) in a counted ping-pong loop, so the next group's
 // loads are in flight while this group's rows are read from LDS (tools/edge_lab: 245 vs 300 us
 // for the PPI-L1 aggregation with the loads issued inside the walk)
+// one record {64 src, alpha~} at byte offset off of a head's records (base: wave-uniform)
+__device__ inline uint64_t load_rec(const int2* base, int off) {
+  uint64_t v;
+  asm volatile("global_load_dwordx2 %0, %1, %2" : "=v"(v) : "v"(off), "s"(base));
+  return v;
+}
+// wait until at most N vector-memory operations of this wave are outstanding (loads return in
+// issue order, so the N newest are the ones still allowed in flight)
+template <int N, int RPL>
+__device__ inline void wait_vm(uint64_t (&r)[RPL]) {
+  if constexpr (RPL == 1)
+    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(r[0]) : "n"(N));
+  else
+    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(r[0]), "+v"(r[1]) : "n"(N));
+}
+
 constexpr int kDegBins = 64;   // degree buckets of the in-workgroup destination sort
 static_assert(kLdsRows <= 3 * 1024, "the destination sort gives each thread <= 3 destinations");
 
-template <int RPL>
-__global__ void __launch_bounds__(1024) edge_lds_kernel(LdsArgs g) {
+template <int RPL, bool DROP>   // DROP: output dropout in the epilogue (its hoisted hash constants
+__global__ void __launch_bounds__(1024) edge_lds_kernel(LdsArgs g) {   // spill at 128 VGPRs)
   __shared__ __attribute__((aligned(16))) float4 img[kLdsRows * 4];
   __shared__ unsigned short order[kLdsRows];   // the block's destinations, grouped by degree
   __shared__ int bins[kDegBins];
@@ -224,8 +302,13 @@ __global__ void __launch_bounds__(1024) edge_lds_kernel(LdsArgs g) {
   const int c = (int)(b % g.nchunks);                           // run on one XCD: its records
   const int h = (int)((b / g.nchunks) % g.NH);                  // stay in that L2
   const int64_t k = b / ((int64_t)g.nchunks * g.NH);
-  if (k >= (int64_t)*g.seg_count) return;
-  const int n0 = g.segs[k], R = g.segs[k + 1] - n0;
+  const int cnt = coherent_load(g.seg_count);
+  if (cnt < 0 || cnt > g.seg_bound) {
+    lds_global_walk<DROP>(g, k, c, h);
+    return;
+  }
+  if (k >= cnt) return;
+  const int n0 = coherent_load(g.segs + k), R = coherent_load(g.segs + k + 1) - n0;
   const int tid = threadIdx.x;
   const int F4 = g.Fp / 4;
   if (tid < kDegBins) bins[tid] = 0;
@@ -282,21 +365,22 @@ __global__ void __launch_bounds__(1024) edge_lds_kernel(LdsArgs g) {
     const int end = live ? g.rowptr[n + 1] : 0;
     const int last = end > 0 ? end - 1 : 0;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    int2 ra[RPL], rb[RPL];
-    bool va[RPL], vb[RPL];
-    auto load = [&](int2 (&r)[RPL], bool (&ok)[RPL], int e0) {
+    // records as raw 64-bit loads issued from inline asm and retired by counted vmcnt waits: the
+    // compiler sinks ordinary loads to just before their use (at the 128-VGPR cap it would rather
+    // wait than keep a group in flight), which left every group's latency exposed. The wait asm
+    // takes the loaded registers as in/out operands, so no use can be scheduled above it.
+    uint64_t ra[RPL], rb[RPL];
+    const int lim = last * 8;
+    auto issue = [&](uint64_t (&r)[RPL], int e0) {
 #pragma unroll
-      for (int u = 0; u < RPL; ++u) {
-        const int ee = e0 + q * RPL + u;
-        ok[u] = ee < end;
-        r[u] = rh[min(ee, last)];
-      }
+      for (int u = 0; u < RPL; ++u) r[u] = load_rec(rh, min((e0 + q * RPL + u) * 8, lim));
     };
-    auto consume = [&](const int2 (&cur)[RPL], const bool (&ok)[RPL]) {
+    auto consume = [&](const uint64_t (&cur)[RPL], int e0) {
 #pragma unroll
       for (int u = 0; u < RPL; ++u) {
-        const int cx = ok[u] ? cur[u].x : 64 * n0;
-        const int cy = ok[u] ? cur[u].y : 0;
+        const bool ok = e0 + q * RPL + u < end;
+        const int cx = ok ? (int)(uint32_t)cur[u] : 64 * n0;
+        const int cy = ok ? (int)(uint32_t)(cur[u] >> 32) : 0;
 #define GATX_LDS_STEP(T)                                                        \
         {                                                                       \
           const float4 v = *(const float4*)(imgb + (quad_bcast<T>(cx) + qb));   \
@@ -310,39 +394,19 @@ __global__ void __launch_bounds__(1024) edge_lds_kernel(LdsArgs g) {
     int need = (end - e + G - 1) / G;
     for (int off = 4; off < 64; off <<= 1) need = max(need, __shfl_xor(need, off));
     const int trips = uni(need);
-    load(ra, va, e);
+    issue(ra, e);
     for (int it = 0; it < trips; it += 2) {
-      load(rb, vb, e + G);
-      consume(ra, va);
-      load(ra, va, e + 2 * G);
-      consume(rb, vb);
+      issue(rb, e + G);
+      wait_vm<RPL>(ra);   // ra landed; rb in flight
+      consume(ra, e);
+      issue(ra, e + 2 * G);
+      wait_vm<RPL>(rb);
+      consume(rb, e + G);
       e += 2 * G;
     }
+    wait_vm<0>(ra);       // nothing may still write these registers after the walk
     if (!live || f0 >= g.F) continue;
-    const int64_t cb = (int64_t)h * g.F + f0;
-    float* orow = g.out + n * g.out_ld;
-    if (g.vec_out) {
-      float4 o = acc;
-      if (g.bias) o = add4(o, *(const float4*)(g.bias + cb));
-      if (g.resid) o = add4(o, *(const float4*)(g.resid + n * g.resid_ld + cb));
-      if (g.elu) {
-        o.x = elu_act(o.x); o.y = elu_act(o.y); o.z = elu_act(o.z); o.w = elu_act(o.w);
-      }
-      if (g.out_p > 0.f) {
-        const float sc = 1.f / (1.f - g.out_p);
-        const int64_t base = n * (int64_t)(g.NH * g.F) + cb;
-        const uint64_t sd = *g.out_seed;
-        o.x = dropout_keep(sd, base, g.out_p) ? o.x * sc : 0.f;
-        o.y = dropout_keep(sd, base + 1, g.out_p) ? o.y * sc : 0.f;
-        o.z = dropout_keep(sd, base + 2, g.out_p) ? o.z * sc : 0.f;
-        o.w = dropout_keep(sd, base + 3, g.out_p) ? o.w * sc : 0.f;
-      }
-      *(float4*)(orow + cb) = o;
-    } else {
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-        if (f0 + t < g.F) orow[cb + t] = lds_epilogue(get4(acc, t), g, n, cb + t);
-    }
+    lds_store<DROP>(g, n, (int64_t)h * g.F + f0, f0, acc);
   }
 }
 
@@ -380,14 +444,15 @@ extern "C" int gatx_edge_records(const float* S, const uint32_t* M_ord, const in
 }
 
 extern "C" int gatx_edge_lds_forward(const float* rows, int64_t row_stride,
-                                     const int32_t* rowptr, const void* rec,
+                                     const int32_t* rowptr, int64_t N, const void* rec,
                                      int64_t E_bound, const int32_t* segs,
                                      const int32_t* seg_count, int64_t seg_bound, int NH, int F,
                                      const float* bias, float* out, int64_t out_ld,
                                      const float* resid, int64_t resid_ld, int elu,
                                      float out_p, const uint64_t* out_seed, gatx_stream_t s) {
   const int Fp = (int)round_up(F, 4);
-  GATX_REQUIRE(NH >= 1 && F >= 1 && seg_bound >= 0 && row_stride >= (int64_t)NH * Fp &&
+  GATX_REQUIRE(NH >= 1 && F >= 1 && N >= 0 && seg_bound >= 0 && E_bound < (1ll << 28) &&
+                   row_stride >= (int64_t)NH * Fp &&
                    row_stride % 4 == 0 && (uintptr_t)rows % 16 == 0,
                "edge_lds_forward: bad arguments");
   GATX_REQUIRE(out_p == 0.f || out_seed != nullptr, "edge_lds_forward: dropout needs its seed");
@@ -395,6 +460,7 @@ extern "C" int gatx_edge_lds_forward(const float* rows, int64_t row_stride,
   LdsArgs g;
   g.rows = rows; g.row_stride = row_stride; g.rowptr = rowptr; g.rec = (const int2*)rec;
   g.E_bound = E_bound; g.segs = segs; g.seg_count = seg_count; g.seg_bound = seg_bound;
+  g.N = N;
   g.NH = NH; g.F = F; g.Fp = Fp; g.nchunks = (int)ceil_div(Fp, kChunk);
   g.bias = bias; g.out = out; g.out_ld = out_ld; g.resid = resid; g.resid_ld = resid_ld;
   g.elu = elu; g.out_p = out_p; g.out_seed = out_seed;
@@ -402,7 +468,10 @@ extern "C" int gatx_edge_lds_forward(const float* rows, int64_t row_stride,
   g.vec_out = (F % 4 == 0) && al(out, out_ld) && al(resid, resid_ld) && al(bias, 0);
   const int64_t blocks = seg_bound * NH * g.nchunks;
   GATX_REQUIRE(blocks < (1ll << 31), "edge_lds_forward: too many workgroups");
-  edge_lds_kernel<2><<<(unsigned)blocks, 1024, 0, (hipStream_t)s>>>(g);
+  if (out_p > 0.f)
+    edge_lds_kernel<2, true><<<(unsigned)blocks, 1024, 0, (hipStream_t)s>>>(g);
+  else
+    edge_lds_kernel<2, false><<<(unsigned)blocks, 1024, 0, (hipStream_t)s>>>(g);
   GATX_LAUNCH_CHECK("edge_lds_forward");
   return 0;
 }

@@ -964,14 +964,15 @@ __global__ void __launch_bounds__(1024) seg_tile_kernel(const int32_t* __restric
   }
 }
 
-// scan pass 2: every free boundary b (0 < b < N: max_{d<b} hi[d] < b and min_{d>=b} lo[d] >= b)
-// appended to list[] (unordered; at most kSegMax kept, the count is exact)
+// scan pass 2: the free boundaries as a bit set (bit b: 0 < b < N, max_{d<b} hi[d] < b and
+// min_{d>=b} lo[d] >= b), one 64-bit ballot per wave. Every word is rewritten on every call: no
+// memset, no atomics, nothing that differs between two runs on the same CSR (a captured step's
+// replays recompute identical words)
 __global__ void __launch_bounds__(1024) seg_free_kernel(const int32_t* __restrict__ phi,
                                                         const int32_t* __restrict__ slo,
                                                         const int32_t* __restrict__ agg,
                                                         int64_t N, int ntiles,
-                                                        int32_t* __restrict__ list,
-                                                        int32_t* __restrict__ count) {
+                                                        uint32_t* __restrict__ bits) {
   __shared__ int pre_hi, suf_lo;
   const int t = threadIdx.x, k = blockIdx.x;
   const int n = (int)N;
@@ -984,39 +985,59 @@ __global__ void __launch_bounds__(1024) seg_free_kernel(const int32_t* __restric
   }
   __syncthreads();
   const int64_t bd = (int64_t)k * 1024 + t;   // boundary between nodes bd - 1 and bd
-  if (bd <= 0 || bd >= N) return;
-  const int before = t > 0 ? max(pre_hi, phi[bd - 1]) : pre_hi;   // max hi over d < bd
-  const int after = min(suf_lo, slo[bd]);                           // min lo over d >= bd
-  if (before < (int)bd && after >= (int)bd) {
-    const int slot = atomicAdd(count, 1);
-    if (slot < kSegMax) list[slot] = (int)bd;
+  bool fr = false;
+  if (bd > 0 && bd < N) {
+    const int before = t > 0 ? max(pre_hi, phi[bd - 1]) : pre_hi;   // max hi over d < bd
+    const int after = min(suf_lo, slo[bd]);                           // min lo over d >= bd
+    fr = before < (int)bd && after >= (int)bd;
   }
+  const uint64_t m = __ballot(fr);
+  const int lane = t & 63;
+  const int64_t w = bd >> 5;   // this lane's 32-bit word (lanes 0 and 32 write them)
+  if ((lane & 31) == 0 && w < ceil_div(N, (int64_t)64) * 2)
+    bits[w] = (uint32_t)(lane == 0 ? m : m >> 32);
 }
 
-// pack: sort the free boundaries (rank by counting, in LDS) and pack the gap-free runs greedily
-// into blocks of <= max_rows nodes (thread 0)
-__global__ void __launch_bounds__(1024) seg_pack_kernel(const int32_t* __restrict__ list,
-                                                        const int32_t* __restrict__ count_in,
+// pack: the free boundaries in order (a block-wide scan of the words' popcounts), then the
+// gap-free runs packed greedily into blocks of <= max_rows nodes (thread 0)
+__global__ void __launch_bounds__(1024) seg_pack_kernel(const uint32_t* __restrict__ bits,
                                                         int64_t N, int max_rows,
                                                         int32_t* __restrict__ segs,
                                                         int32_t* __restrict__ seg_count) {
-  __shared__ int in[kSegMax], bnd[kSegMax + 2];
-  const int t = threadIdx.x, n = (int)N;
-  const int nb = *count_in;
+  __shared__ int bnd[kSegMax + 2];
+  __shared__ int wsum[16];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, n = (int)N;
+  const int64_t nw = ceil_div(N, (int64_t)64) * 2;   // words (<= 2^17 / 32 = 4096)
+  int base = 0;
+  for (int64_t w0 = 0; w0 < nw; w0 += 1024) {
+    const int64_t w = w0 + t;
+    const uint32_t word = w < nw ? bits[w] : 0u;
+    const int c = __popc(word);
+    int x = c;   // inclusive wave scan
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(x, off);
+      if (lane >= off) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    int before = 0, total = 0;
+    for (int i = 0; i < 16; ++i) {
+      const int v = wsum[i];
+      before += i < wave ? v : 0;
+      total += v;
+    }
+    int pos = base + before + x - c;
+    for (uint32_t m = word; m != 0u; m &= m - 1u, ++pos)
+      if (pos < kSegMax) bnd[1 + pos] = (int)(w * 32 + __ffs(m) - 1);
+    base += total;
+    __syncthreads();   // wsum reused
+  }
+  if (t != 0) return;
+  const int nb = base;
   if (nb > kSegMax) {
-    if (t == 0) *seg_count = -1;
+    *seg_count = -1;
     return;
   }
-  for (int i = t; i < nb; i += 1024) in[i] = list[i];
-  __syncthreads();
-  for (int i = t; i < nb; i += 1024) {   // boundaries are distinct: rank = # smaller
-    const int v = in[i];
-    int r = 0;
-    for (int j = 0; j < nb; ++j) r += in[j] < v;
-    bnd[1 + r] = v;
-  }
-  __syncthreads();
-  if (t != 0) return;
   bnd[0] = 0;
   bnd[nb + 1] = n;
   int count = 0, start = 0;
@@ -1042,8 +1063,8 @@ __global__ void seg_none_kernel(int32_t* seg_count) {
 
 extern "C" size_t gatx_graph_segments_workspace_bytes(int64_t N) {
   const size_t nn = align256(sizeof(int32_t) * (size_t)(N > 0 ? N : 1));
-  return 4 * nn + align256(sizeof(int32_t) * (2 * (size_t)ceil_div(N > 0 ? N : 1, 1024) + 1)) +
-         align256(sizeof(int32_t) * kSegMax);
+  return 4 * nn + align256(sizeof(int32_t) * 2 * (size_t)ceil_div(N > 0 ? N : 1, 1024)) +
+         align256(sizeof(uint32_t) * 2 * (size_t)ceil_div(N > 0 ? N : 1, 64));
 }
 
 extern "C" int gatx_graph_segments(const int32_t* rowptr, const int32_t* col, int64_t N,
@@ -1064,23 +1085,17 @@ extern "C" int gatx_graph_segments(const int32_t* rowptr, const int32_t* col, in
   int32_t* hi = (int32_t*)p; p += nn;
   int32_t* phi = (int32_t*)p; p += nn;
   int32_t* slo = (int32_t*)p; p += nn;
-  int32_t* agg = (int32_t*)p; p += align256(sizeof(int32_t) * (2 * (size_t)ntiles + 1));
-  int32_t* list = (int32_t*)p;
-  int32_t* cnt = agg + 2 * ntiles;
-  const hipError_t me = hipMemsetAsync(cnt, 0, sizeof(int32_t), st);
-  if (me != hipSuccess) {
-    set_error("graph_segments: %s", hipGetErrorString(me));
-    return (int)me;
-  }
+  int32_t* agg = (int32_t*)p; p += align256(sizeof(int32_t) * 2 * (size_t)ntiles);
+  uint32_t* bits = (uint32_t*)p;
   if (N > 0) {
     seg_hilo_kernel<<<(unsigned)ceil_div(N, (int64_t)4), 256, 0, st>>>(rowptr, col, N, lo, hi);
     GATX_LAUNCH_CHECK("graph_segments hilo");
     seg_tile_kernel<<<(unsigned)ntiles, 1024, 0, st>>>(lo, hi, N, phi, slo, agg);
     GATX_LAUNCH_CHECK("graph_segments tile");
-    seg_free_kernel<<<(unsigned)ntiles, 1024, 0, st>>>(phi, slo, agg, N, ntiles, list, cnt);
+    seg_free_kernel<<<(unsigned)ntiles, 1024, 0, st>>>(phi, slo, agg, N, ntiles, bits);
     GATX_LAUNCH_CHECK("graph_segments free");
   }
-  seg_pack_kernel<<<1, 1024, 0, st>>>(list, cnt, N, max_rows, segs, seg_count);
+  seg_pack_kernel<<<1, 1024, 0, st>>>(bits, N, max_rows, segs, seg_count);
   GATX_LAUNCH_CHECK("graph_segments pack");
   return 0;
 }

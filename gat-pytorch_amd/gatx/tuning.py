@@ -17,7 +17,7 @@ threshold of one); the defaults are the measured-best choices (§
   fused_scores    1     node scores reduced in the projection GEMM's epilogue
   dropout_fuse    1     the next layer's input dropout in this layer's edge-pass epilogue
   skip_fold       1     GATModel's Linear skips folded into the projection GEMM
-  edge_lds        0     concat layers on graphs cut into node blocks of <= 2304 nodes: the
+  edge_lds        1     concat layers on graphs cut into node blocks of <= 2304 nodes: the
                         LDS-staged edge pass (csrc/edge_lds.hip) instead of the L2-gather one
 
     import gatx
@@ -41,7 +41,7 @@ DEFAULTS = {
     "fused_scores": 1,
     "dropout_fuse": 1,
     "skip_fold": 1,
-    "edge_lds": 0,
+    "edge_lds": 1,
 }
 
 _current = dict(DEFAULTS)

@@ -420,7 +420,10 @@ int gatx_pad_rows(const float* src, int64_t rows, int64_t cols, int64_t ld_src, 
  *   stages that chunk of every row of its block in LDS and sums alpha~ x row over each
  *   destination's segment, then bias / resid / ELU / the next layer's input dropout as
  *   gatx_edge_forward_drop. rows: Wh with row_stride >= NH * round4(F) floats, 16-byte aligned.
- *   seg_bound: the grid's block bound (>= *seg_count; blocks past the count exit). */
+ *   seg_bound: the grid's block bound (>= *seg_count; blocks past the count exit). When the
+ *   device count is -1 or exceeds seg_bound (a captured step replayed on edges that no longer cut
+ *   into those blocks), the workgroups split the num_nodes rows evenly and gather from global
+ *   memory instead: slower, same result. */
 int gatx_edge_lds_rows(void);
 int gatx_edge_records(const float* S, const uint32_t* M_ord, const int32_t* rowptr,
                       const int32_t* col, const int32_t* perm, int64_t num_nodes,
@@ -428,7 +431,7 @@ int gatx_edge_records(const float* S, const uint32_t* M_ord, const int32_t* rowp
                       const uint64_t* seed, void* rec, float* den, float* alpha,
                       long long* argmax, gatx_stream_t stream);
 int gatx_edge_lds_forward(const float* rows, int64_t row_stride, const int32_t* rowptr,
-                          const void* rec, int64_t E_bound, const int32_t* segs,
+                          int64_t num_nodes, const void* rec, int64_t E_bound, const int32_t* segs,
                           const int32_t* seg_count, int64_t seg_bound, int num_heads,
                           int out_features, const float* bias, float* out, int64_t out_ld,
                           const float* resid, int64_t resid_ld, int elu, float out_p,

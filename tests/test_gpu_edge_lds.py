@@ -124,3 +124,81 @@ def test_captured_forward_lds(device, lds_on):
         out = cap()
     torch.cuda.synchronize()
     assert torch.equal(out, ref)
+
+
+def test_captured_forward_lds_interleaved(device, lds_on):
+    """Replays that each follow a kernel launched outside the graph (a torch fill, as bench.py's
+    fallback-counter read and region marks): the node blocks are recomputed in every replay and
+    the LDS pass must see them (round 5: a memset + atomic counter read by the next kernel came
+    back stale on exactly these replays, so the pass skipped its work)."""
+    import gatx
+    from gatx import data as gd
+    from gatx.capture import CapturedStep
+    from gatx.config import data_config
+    from gatx.graph import graph_cache
+    torch.manual_seed(0)
+    model = gatx.GATModel(**data_config["PPI"]).to(device).eval()
+    b = gd.dataset_batch("PPI", 3, graph_seed=5, feature_seed=6)
+    x = torch.from_numpy(b.x).to(device)
+    ei = torch.from_numpy(b.edge_index).to(device)
+
+    def step():
+        gatx.clear_graph_cache()
+        with torch.no_grad():
+            return model(x, ei)
+
+    ref = step().clone()
+    cap = CapturedStep(step)
+    segs, count = graph_cache.get(ei, b.num_nodes, True)._hub_plans[("blocks", 2304)]
+    for _ in range(4):
+        torch.zeros(1, device=device)
+        out = cap()
+        torch.cuda.synchronize()
+        assert int(count.item()) == 3   # the round-5 failure left -1 here
+        assert torch.equal(out, ref)
+
+
+def _blocked_edges(N, E, runs, seed):
+    """E random edges that stay inside consecutive node runs of the given lengths."""
+    rng = np.random.default_rng(seed)
+    starts = np.concatenate([[0], np.cumsum(runs)[:-1]])
+    which = rng.integers(0, len(runs), E)
+    lo = starts[which]
+    ln = np.asarray(runs)[which]
+    src = lo + rng.integers(0, ln)
+    dst = lo + rng.integers(0, ln)
+    assert starts[-1] + runs[-1] == N
+    return np.stack([src, dst]).astype(np.int64)
+
+
+def test_captured_forward_lds_blocks_change(device, lds_on):
+    """A captured LDS forward replayed on edges copied into its edge_index whose node blocks no
+    longer match the launch (more blocks than the grid holds, then none at all): the pass falls
+    back to gathering rows from global memory and still equals the eager (L2-gather) step."""
+    import gatx
+    from gatx import tuning
+    from gatx.capture import CapturedStep
+    from gatx.config import data_config
+    torch.manual_seed(0)
+    model = gatx.GATModel(**data_config["PPI"]).to(device).eval()
+    N, E = 4490, 60000
+    x = torch.randn(N, 50, device=device)
+    ei = torch.from_numpy(_blocked_edges(N, E, [2245, 2245], 1)).to(device)
+
+    def step():
+        gatx.clear_graph_cache()
+        with torch.no_grad():
+            return model(x, ei)
+
+    cap = CapturedStep(step)
+    out = cap().clone()
+    tuning.set(edge_lds=0)
+    assert float((out - step()).abs().max()) <= 1e-5
+    tuning.set(edge_lds=1)
+    for runs in ([1200, 1200, 1200, 890], [N]):   # 4 blocks > the grid's 2; one 4490-node run
+        ei.copy_(torch.from_numpy(_blocked_edges(N, E, runs, 2)).to(device))
+        out = cap().clone()
+        tuning.set(edge_lds=0)
+        ref = step()
+        tuning.set(edge_lds=1)
+        assert float((out - ref).abs().max()) <= 1e-5 * max(1.0, float(ref.abs().max()))
