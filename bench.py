@@ -118,7 +118,7 @@ def run_timed(step, steps, world, dev, instr_step=None, instr_outside=False):
     The region is bracketed by two gatx_region_mark dispatches (the first carries `steps` in its
     grid size) enqueued outside the clock, so a rocprofv3 counter pass can cut exactly these
     steps' dispatches out of its trace (tools/pmc_summary.py).
-    instr_outside (launch-bound captured steps: PATTERN, Planetoid): all `steps` timed steps are
+    instr_outside (launch-bound captured steps: PATTERN, Planetoid, training): all `steps` timed steps are
     graph replays and the instrumented eager steps run right after the clock stops — an eager
     step of ~80 small launches is host-bound (it took ~3x a replay), so inside the clock it would
     measure the Python launch path, not the step."""
@@ -1040,8 +1040,10 @@ def main():
     from gatx import _lib
     fb = torch.zeros(1, dtype=torch.int64, device=dev)
     _lib.call("gatx_gemm_fallback_read", _lib.ptr(fb), 1, _lib.stream())   # reset the counter
-    # (small batches are launch-bound: their instrumented eager steps run after the clock)
-    instr_outside = use_graph and (ds != "PPI" or args.graphs < 20)
+    # launch-bound eager steps run their HIP-event instrumentation after the clock: small batches,
+    # and every training step (autograd + ~110 launches: the eager PPI-20 step is host-bound,
+    # ~1 ms of launch gaps in rocprof traces, so inside the clock it timed the Python path)
+    instr_outside = use_graph and (args.mode == "train" or ds != "PPI" or args.graphs < 20)
     elapsed, summ, n_instr = run_timed(step, args.steps, world, dev,
                                        step.eager if use_graph else None, instr_outside)
     _lib.call("gatx_gemm_fallback_read", _lib.ptr(fb), 1, _lib.stream())

@@ -297,7 +297,8 @@ template <int RPL, bool DROP>   // DROP: output dropout in the epilogue (its hoi
 __global__ void __launch_bounds__(1024) edge_lds_kernel(LdsArgs g) {   // spill at 128 VGPRs)
   __shared__ __attribute__((aligned(16))) float4 img[kLdsRows * 4];
   __shared__ unsigned short order[kLdsRows];   // the block's destinations, grouped by degree
-  __shared__ int bins[kDegBins];
+  __shared__ int lrp[kLdsRows + 1];             // the block's row pointers (the walk's segment
+  __shared__ int bins[kDegBins];                // bounds without a global-latency hop)
   const int64_t b = xcd_contiguous(blockIdx.x, gridDim.x);   // the chunks of one (block, head)
   const int c = (int)(b % g.nchunks);                           // run on one XCD: its records
   const int h = (int)((b / g.nchunks) % g.NH);                  // stay in that L2
@@ -330,7 +331,11 @@ __global__ void __launch_bounds__(1024) edge_lds_kernel(LdsArgs g) {   // spill 
 #pragma unroll
   for (int t = 0; t < 3; ++t) {
     const int d = tid + 1024 * t;
-    degs[t] = d < R ? min(g.rowptr[n0 + d + 1] - g.rowptr[n0 + d], kDegBins - 1) : -1;
+    int lo = 0, hi = 0;
+    if (d <= R) lo = g.rowptr[n0 + d];
+    if (d < R) hi = g.rowptr[n0 + d + 1];
+    if (d <= R) lrp[d] = lo;
+    degs[t] = d < R ? min(hi - lo, kDegBins - 1) : -1;
   }
   __syncthreads();
 #pragma unroll
@@ -357,24 +362,35 @@ __global__ void __launch_bounds__(1024) edge_lds_kernel(LdsArgs g) {   // spill 
   const char* imgb = (const char*)img;
   const int f0 = c * kChunk + q * 4;   // this lane's first feature in the head's row
   constexpr int G = 4 * RPL;           // records per quad per group
-  for (int d0 = wave * 16; d0 < R; d0 += 256) {
-    const bool live = d0 + j < R;
-    const int dl = live ? (int)order[d0 + j] : 0;
-    const int64_t n = n0 + dl;
-    int e = live ? g.rowptr[n] : 0;
-    const int end = live ? g.rowptr[n + 1] : 0;
-    const int last = end > 0 ? end - 1 : 0;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    // records as raw 64-bit loads issued from inline asm and retired by counted vmcnt waits: the
-    // compiler sinks ordinary loads to just before their use (at the 128-VGPR cap it would rather
-    // wait than keep a group in flight), which left every group's latency exposed. The wait asm
-    // takes the loaded registers as in/out operands, so no use can be scheduled above it.
-    uint64_t ra[RPL], rb[RPL];
-    const int lim = last * 8;
-    auto issue = [&](uint64_t (&r)[RPL], int e0) {
+  // records as raw 64-bit loads issued from inline asm and retired by counted vmcnt waits: the
+  // compiler sinks ordinary loads to just before their use (at the 128-VGPR cap it would rather
+  // wait than keep a group in flight), which left every group's latency exposed. The wait asm
+  // takes the loaded registers as in/out operands, so no use can be scheduled above it. The
+  // first group of a wave's next 16 destinations is issued during the current walk's last step,
+  // so no destination set starts with a full L2 round trip.
+  uint64_t ra[RPL], rb[RPL];
+  auto issue = [&](uint64_t (&r)[RPL], int e0, int lim) {
 #pragma unroll
-      for (int u = 0; u < RPL; ++u) r[u] = load_rec(rh, min((e0 + q * RPL + u) * 8, lim));
-    };
+    for (int u = 0; u < RPL; ++u) r[u] = load_rec(rh, min((e0 + q * RPL + u) * 8, lim));
+  };
+  // this lane's destination of the set starting at d0 (segment [e, end); lim: its last record)
+  auto dest = [&](int d0, bool& live, int& dl, int& e, int& end, int& lim) {
+    live = d0 + j < R;
+    dl = live ? (int)order[d0 + j] : 0;
+    e = live ? lrp[dl] : 0;
+    end = live ? lrp[dl + 1] : 0;
+    lim = (end > 0 ? end - 1 : 0) * 8;
+  };
+  bool live;
+  int dl, e, end, lim;
+  dest(wave * 16, live, dl, e, end, lim);
+  issue(ra, e, lim);
+  for (int d0 = wave * 16; d0 < R; d0 += 256) {
+    bool live1;
+    int dl1, e1, end1, lim1;
+    dest(d0 + 256, live1, dl1, e1, end1, lim1);   // the next set (beyond R: empty, loads clamp)
+    const int64_t n = n0 + dl;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     auto consume = [&](const uint64_t (&cur)[RPL], int e0) {
 #pragma unroll
       for (int u = 0; u < RPL; ++u) {
@@ -394,20 +410,28 @@ __global__ void __launch_bounds__(1024) edge_lds_kernel(LdsArgs g) {   // spill 
     int need = (end - e + G - 1) / G;
     for (int off = 4; off < 64; off <<= 1) need = max(need, __shfl_xor(need, off));
     const int trips = uni(need);
-    issue(ra, e);
     for (int it = 0; it < trips; it += 2) {
-      issue(rb, e + G);
+      issue(rb, e + G, lim);
       wait_vm<RPL>(ra);   // ra landed; rb in flight
       consume(ra, e);
-      issue(ra, e + 2 * G);
+      if (it + 2 < trips)
+        issue(ra, e + 2 * G, lim);
+      else
+        issue(ra, e1, lim1);   // the next set's first group
       wait_vm<RPL>(rb);
       consume(rb, e + G);
       e += 2 * G;
     }
-    wait_vm<0>(ra);       // nothing may still write these registers after the walk
-    if (!live || f0 >= g.F) continue;
+    if (trips == 0) {     // ra still holds this set's (empty) first group
+      wait_vm<0>(ra);
+      issue(ra, e1, lim1);
+    }
+    const bool live_cur = live;
+    live = live1; dl = dl1; e = e1; end = end1; lim = lim1;
+    if (!live_cur || f0 >= g.F) continue;
     lds_store<DROP>(g, n, (int64_t)h * g.F + f0, f0, acc);
   }
+  wait_vm<0>(ra);   // nothing may still write these registers after the walk
 }
 
 }  // namespace

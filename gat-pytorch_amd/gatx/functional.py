@@ -8,11 +8,13 @@ SURVEY.md §8(a) a14 and oracle/gat_oracle.py:gat_layer_backward.
 """
 from __future__ import annotations
 
+from contextlib import contextmanager
+
 import torch
 
 from . import tuning
 from ._lib import ARGMAX_CAP, call, lib, ptr, stream, version
-from .graph import Graph
+from .graph import Graph, join_side
 
 
 class KernelTimer:
@@ -253,6 +255,39 @@ def projection_planes(W_aug, sh: "LayerShape", N: int):
     return build_weight_planes(W_aug, rows, sh.F_in, sh.F_in)
 
 
+_SIDE_ALPHA = [False]
+
+
+@contextmanager
+def side_alpha(on: bool):
+    """Within: a layer's alpha pass (and its max() tie records) is launched on the side stream,
+    forked after the edge pass, so it runs under the next layer's projection GEMM; the next
+    layer joins it after launching that GEMM, and GATModel joins before returning (the alphas
+    and tie records are read by nothing in between). Only GATModel sets it, for all but its last
+    layer."""
+    prev = _SIDE_ALPHA[0]
+    _SIDE_ALPHA[0] = on
+    try:
+        yield
+    finally:
+        _SIDE_ALPHA[0] = prev
+
+
+def _alpha_pass(graph: Graph, S, M_ord, den, sh: "LayerShape", alpha, argmax, dev):
+    """_attention_alpha on the current stream, or forked onto the side stream (side_alpha)."""
+    if not (_SIDE_ALPHA[0] and tuning.get("side_stream")):
+        with _span("attention_alpha", (graph.edge_bound, sh.NH)):
+            _attention_alpha(graph, S, M_ord, den, sh, alpha, argmax, stream())
+        return
+    from .graph import side_stream, _SIDE_PENDING
+    side = side_stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        with _span("attention_alpha", (graph.edge_bound, sh.NH)):
+            _attention_alpha(graph, S, M_ord, den, sh, alpha, argmax, stream())
+    _SIDE_PENDING[dev] = True
+
+
 def _attention_alpha(graph: Graph, S, M_ord, den, sh: "LayerShape", alpha, argmax, s):
     """alpha in edge_index' order (models/gat_layer.py:106-110): iterates edge_index' itself, so
     both its reads and the alpha writes are coalesced; |edge_index'| is read on the device."""
@@ -342,13 +377,14 @@ def _edge_pass(rows, row_stride, S, M_ord, graph, sh, bias, p, seed, out, resid_
                  *(drop_args if last else (0.0, None)), None, s)
 
 
-def lds_blocks(graph: Graph, sh: LayerShape):
+def lds_blocks(graph: Graph, sh: LayerShape, side: bool = False):
     """(segs, count, n_blocks) when this layer's edge pass takes the LDS-staged kernels
     (csrc/edge_lds.hip; tuning edge_lds): a concat layer of <= 8 heads on a graph whose node
-    blocks (gatx_graph_segments) fit the LDS image; else None."""
+    blocks (gatx_graph_segments) fit the LDS image; else None. side: a first build of the blocks
+    runs on the side stream (the caller joins it before the LDS pass)."""
     if not tuning.get("edge_lds") or not sh.concat or sh.NH > 8:
         return None
-    return graph.lds_blocks(lib.gatx_edge_lds_rows())
+    return graph.lds_blocks(lib.gatx_edge_lds_rows(), side)
 
 
 def fold_scores_into_gemm(sh: LayerShape) -> bool:
@@ -488,8 +524,7 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
                  int(sh.const), None, float(p), ptr(seed), ptr(Z), sh.NH * Fin_p, None, 0, 0,
                  ptr(den), chunk, *hub, s)
         if want_alpha:
-            with _span("attention_alpha", (E2, sh.NH)):
-                _attention_alpha(graph, S, M_ord, den, sh, alpha, argmax, s)
+            _alpha_pass(graph, S, M_ord, den, sh, alpha, argmax, dev)
         else:
             alpha = LazyAlpha(graph, S, M_ord, den, sh, argmax)
         Wp = padded_weight(W, Fin_p, sh.cache_weights)   # float4-readable rows
@@ -500,6 +535,8 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
                  ptr(bias), sh.F, resid_p, sh.out_cols, sh.F, int(elu), s)
         saved.update(S=S, reassoc=True, Z=Z, x_rows=x_rows)
         return out, alpha, saved
+    # node blocks of an LDS-staged layer: built on the side stream while the projection GEMM runs
+    blocks = lds_blocks(graph, sh, side=True)
     Wh = torch.empty((N, sh.Dp), **f32)
     S = torch.empty((N, max(sh.H2, 1)), **f32)
     # the weight operand pre-split into fp16 planes (gemm_f16p.hip; None: in-loop split)
@@ -530,11 +567,12 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
                  *gemm_workspace(N, sh.Dp, sh.F_in, dev), s)
         with _span("node_scores", (N, sh.NH, sh.F)):
             call("gatx_node_scores", ptr(Wh), N, sh.NH, sh.F, ptr(a), ptr(S), s)
+    # the previous layer's side-stream alpha pass and this layer's node blocks ran under the GEMM
+    join_side(dev)
     if not sh.const:
         with _span("attention_max", (E2, sh.NH)):
             call("gatx_attention_max", ptr(graph.col), ptr(graph.rowidx), E2, graph.e2_ptr,
                  ptr(S), sh.NH, ptr(M_ord), ptr(argmax), ptr(_max_ws(dev)), s)
-    blocks = lds_blocks(graph, sh)
     if blocks is not None:
         # LDS-staged edge pass (csrc/edge_lds.hip): records (den, alpha, ties, {4 src, alpha~}
         # per head and CSR slot), then one workgroup per (node block, head, 16-float chunk)
@@ -557,8 +595,7 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
         _edge_pass(Wh, sh.Dp, S, M_ord, graph, sh, bias, p, seed, out, resid_p, elu, den, chunk,
                    drop_args, dev, s)
     if want_alpha:
-        with _span("attention_alpha", (E2, sh.NH)):
-            _attention_alpha(graph, S, M_ord, den, sh, alpha, argmax, s)
+        _alpha_pass(graph, S, M_ord, den, sh, alpha, argmax, dev)
     else:
         alpha = LazyAlpha(graph, S, M_ord, den, sh, argmax)
     saved.update(Wh=Wh, S=S, reassoc=False)

@@ -223,12 +223,16 @@ class Graph:
             plan = self._hub_plans[key] = (hubs, count, bound)
         return plan
 
-    def node_blocks(self, max_rows: int):
+    def node_blocks(self, max_rows: int, side: bool = False):
         """(segs, count) of gatx_graph_segments for this CSR (device tensors, built once per graph
         and max_rows): contiguous node blocks no edge crosses, each <= max_rows nodes; count -1
         when the graph has none (a gap-free run longer than max_rows). The workspace is a
-        per-device scratch that lives as long as the process (stream-ordered reuse), so no
-        buffer a captured step reads is ever freed and handed to another allocation."""
+        per-device scratch that lives as long as the process, so a captured step's launches
+        keep its address.
+        side: launch on the per-device side stream (forked from the current stream; the caller
+        joins it with join_side before reading the result), so the four small launches run
+        under the projection GEMM instead of after it. The tensors are allocated on the current
+        stream either way."""
         key = ("blocks", max_rows)
         hit = self._hub_plans.get(key)
         if hit is None:
@@ -238,12 +242,21 @@ class Graph:
             count = torch.empty(1, dtype=torch.int32, device=dev)
             wb = _lib.lib.gatx_graph_segments_workspace_bytes(self.num_nodes)
             ws = _seg_ws(dev, wb)
-            call("gatx_graph_segments", ptr(self.rowptr), ptr(self.col), self.num_nodes,
-                 int(max_rows), ptr(segs), ptr(count), ptr(ws), wb, stream())
+            from . import tuning
+            if side and tuning.get("side_stream"):
+                sst = side_stream(dev)
+                sst.wait_stream(torch.cuda.current_stream(dev))
+                call("gatx_graph_segments", ptr(self.rowptr), ptr(self.col), self.num_nodes,
+                     int(max_rows), ptr(segs), ptr(count), ptr(ws), wb, sst.cuda_stream)
+                _SIDE_PENDING[dev] = True
+            else:
+                join_side(dev)   # (the scratch may still be in use by a side-stream build)
+                call("gatx_graph_segments", ptr(self.rowptr), ptr(self.col), self.num_nodes,
+                     int(max_rows), ptr(segs), ptr(count), ptr(ws), wb, stream())
             hit = self._hub_plans[key] = (segs, count)
         return hit
 
-    def lds_blocks(self, max_rows: int):
+    def lds_blocks(self, max_rows: int, side: bool = False):
         """(segs, count, n_blocks) of node_blocks(max_rows) when this edge_index is known to cut
         into such blocks, else None. Known: decided once per edge_index tensor (storage, version,
         shape, node count) by one read of the device count (outside a capture), cached across
@@ -261,7 +274,7 @@ class Graph:
                 _BLOCKS.pop(next(iter(_BLOCKS)))
         if known <= 0:
             return None
-        segs, count = self.node_blocks(max_rows)
+        segs, count = self.node_blocks(max_rows, side)
         return segs, count, known
 
     def csr_host(self):
@@ -295,6 +308,29 @@ def expect_num_edges(edge_index: torch.Tensor, num_nodes: int, add_self_loops: b
         _HINTS.pop(k, None)
     else:
         _HINTS[k] = int(num_edges)
+
+
+_SIDE: dict = {}
+
+
+def side_stream(dev) -> torch.cuda.Stream:
+    """A per-device second stream for short launches that can run beside the current stream's
+    work (forked with wait_stream, joined with join_side; both are captured as graph edges)."""
+    st = _SIDE.get(dev)
+    if st is None:
+        st = _SIDE[dev] = torch.cuda.Stream(device=dev)
+    return st
+
+
+def join_side(dev) -> None:
+    """The current stream waits for what was launched on the side stream since the last join
+    (nothing to wait for: no event, so a capture never waits on an uncaptured stream)."""
+    st = _SIDE.get(dev)
+    if st is not None and _SIDE_PENDING.pop(dev, False):
+        torch.cuda.current_stream(dev).wait_stream(st)
+
+
+_SIDE_PENDING: dict = {}
 
 
 _SEG_WS: dict = {}

@@ -16,6 +16,8 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from .functional import side_alpha
+from .graph import join_side
 from .layer import GATLayer
 
 # Linear skips of at least this many multiply-adds run on the gatx GEMM (x3: the PPI-scale
@@ -168,13 +170,19 @@ class GATModel(nn.Module):
             if fuse_next:
                 extra["out_dropout"] = (self.dropout, seeds[i + 1])
             pre_dropped = fuse_next
-            out = self.gat_layer_list[i](x, edge_index, return_attention_weights=with_attention,
-                                         resid=resid, elu=(i != L - 1), **extra)
+            # all but the last layer: the alpha pass runs on the side stream under the next
+            # layer's projection GEMM (functional.side_alpha; joined there and below)
+            with side_alpha(i != L - 1 and x.is_cuda and not torch.compiler.is_compiling()):
+                out = self.gat_layer_list[i](x, edge_index,
+                                             return_attention_weights=with_attention,
+                                             resid=resid, elu=(i != L - 1), **extra)
             if with_attention:
                 x, (edge_index, att) = out
                 attention_weights_list.append(att)
             else:
                 x = out
+        if x.is_cuda:
+            join_side(x.device)
         return x, edge_index, attention_weights_list
 
     @staticmethod

@@ -19,6 +19,8 @@ threshold of one); the defaults are the measured-best choices (§
   skip_fold       1     GATModel's Linear skips folded into the projection GEMM
   edge_lds        1     concat layers on graphs cut into node blocks of <= 2304 nodes: the
                         LDS-staged edge pass (csrc/edge_lds.hip) instead of the L2-gather one
+  side_stream     1     short independent launches (node blocks, GATModel's non-final alpha
+                        passes) on a second stream, under the projection GEMM
 
     import gatx
     with gatx.tuning.override(edge_chunk=2245):   # or gatx.tuning.set(...) / reset()
@@ -42,6 +44,7 @@ DEFAULTS = {
     "dropout_fuse": 1,
     "skip_fold": 1,
     "edge_lds": 1,
+    "side_stream": 1,
 }
 
 _current = dict(DEFAULTS)

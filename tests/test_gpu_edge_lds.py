@@ -202,3 +202,44 @@ def test_captured_forward_lds_blocks_change(device, lds_on):
         ref = step()
         tuning.set(edge_lds=1)
         assert float((out - ref).abs().max()) <= 1e-5 * max(1.0, float(ref.abs().max()))
+
+
+@pytest.mark.parametrize("side", [0, 1])
+def test_side_stream_model_equals_serial(side, device):
+    """tuning side_stream (node blocks and GATModel's non-final alpha passes on a second stream,
+    joined before use): the PPI model's outputs and every alpha equal the one-stream run bitwise,
+    eager and captured, forward and a training step's gradients."""
+    import gatx
+    from gatx import data as gd
+    from gatx import tuning
+    from gatx.capture import CapturedStep
+    from gatx.config import data_config
+    b = gd.dataset_batch("PPI", 3, graph_seed=9, feature_seed=10)
+    x = torch.from_numpy(b.x).to(device)
+    ei = torch.from_numpy(b.edge_index).to(device)
+    res = []
+    for sd in (0, side):
+        tuning.set(side_stream=sd)
+        torch.manual_seed(0)
+        model = gatx.GATModel(**data_config["PPI"]).to(device)
+        gatx.clear_graph_cache()
+        with torch.no_grad():
+            out, _, al = model.eval().forward_and_return_attention(x, ei)
+
+        def step():
+            gatx.clear_graph_cache()
+            with torch.no_grad():
+                return model(x, ei)
+        cap = CapturedStep(step)
+        rep = cap().clone()
+        model.train()
+        gatx.clear_graph_cache()
+        o, ei2, al2 = model.forward_and_return_attention(x, ei)
+        (o.square().mean() + 0.1 * model.calc_attention_norm(ei2, al2)).backward()
+        res.append((out.clone(), [a.clone() for a in al], rep,
+                    [p.grad.clone() for p in model.parameters()]))
+    tuning.reset()
+    (o0, a0, r0, g0), (o1, a1, r1, g1) = res
+    assert torch.equal(o0, o1) and torch.equal(r0, r1) and torch.equal(r0, o0)
+    assert all(torch.equal(u, v) for u, v in zip(a0, a1))
+    assert all(torch.equal(u, v) for u, v in zip(g0, g1))

@@ -15,6 +15,7 @@ tail -2 "$OUT/gpu_tests.log"
 step bench timeout -k 10 300 python "$R/bench.py" > "$OUT/bench.json" 2> "$OUT/bench.err"
 step bench_train timeout -k 10 300 python "$R/bench.py" --mode train --no-cpu-baseline > "$OUT/bench_train.json" 2> "$OUT/bench_train.err"
 step bench_rmat timeout -k 10 400 python "$R/bench.py" --workload rmat --steps 5 --warmup 2 > "$OUT/bench_rmat.json" 2> "$OUT/bench_rmat.err"
+step bench_ppi2 timeout -k 10 300 python "$R/bench.py" --graphs 2 --mode train --no-cpu-baseline > "$OUT/bench_ppi2_train.json" 2> "$OUT/bench_ppi2_train.err"
 step bench_pattern timeout -k 10 300 python "$R/bench.py" --workload pattern --graphs 8 --mode train --no-cpu-baseline > "$OUT/bench_pattern_train.json" 2> "$OUT/bench_pattern_train.err"
 cd /tmp && export TMPDIR=/tmp
 step prof_fwd timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_fwd" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/prof_fwd.log" 2>&1

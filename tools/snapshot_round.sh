@@ -9,7 +9,7 @@ T=$1
 S=gpurun_out/$T
 D=profiles/$T
 mkdir -p "$D"
-cp "$S"/bench.json "$S"/bench_train.json "$S"/bench_rmat.json "$S"/bench_pattern_train.json "$S"/gpu_tests.log "$D"/
+cp "$S"/bench.json "$S"/bench_train.json "$S"/bench_rmat.json "$S"/bench_pattern_train.json "$S"/bench_ppi2_train.json "$S"/gpu_tests.log "$D"/
 for p in fwd train rmat pattern; do
   cp "$S/prof_$p/run_kernel_stats.csv" "$D/${p}_kernel_stats.csv"
   python tools/trace_window.py "$S/prof_$p" "$D/${p}_breakdown.txt" > /dev/null
