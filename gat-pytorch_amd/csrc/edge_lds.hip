@@ -286,10 +286,13 @@ template <int N, int RPL>
 __device__ inline void wait_vm(uint64_t (&r)[RPL]) {
   if constexpr (RPL == 1)
     asm volatile("s_waitcnt vmcnt(%1)" : "+v"(r[0]) : "n"(N));
-  else
+  else if constexpr (RPL == 2)
     asm volatile("s_waitcnt vmcnt(%2)" : "+v"(r[0]), "+v"(r[1]) : "n"(N));
+  else
+    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]) : "n"(N));
 }
 
+constexpr int kRPL = 2;        // records per lane per group
 constexpr int kDegBins = 64;   // degree buckets of the in-workgroup destination sort
 static_assert(kLdsRows <= 3 * 1024, "the destination sort gives each thread <= 3 destinations");
 
@@ -493,9 +496,9 @@ extern "C" int gatx_edge_lds_forward(const float* rows, int64_t row_stride,
   const int64_t blocks = seg_bound * NH * g.nchunks;
   GATX_REQUIRE(blocks < (1ll << 31), "edge_lds_forward: too many workgroups");
   if (out_p > 0.f)
-    edge_lds_kernel<2, true><<<(unsigned)blocks, 1024, 0, (hipStream_t)s>>>(g);
+    edge_lds_kernel<kRPL, true><<<(unsigned)blocks, 1024, 0, (hipStream_t)s>>>(g);
   else
-    edge_lds_kernel<2, false><<<(unsigned)blocks, 1024, 0, (hipStream_t)s>>>(g);
+    edge_lds_kernel<kRPL, false><<<(unsigned)blocks, 1024, 0, (hipStream_t)s>>>(g);
   GATX_LAUNCH_CHECK("edge_lds_forward");
   return 0;
 }

@@ -275,7 +275,8 @@ def side_alpha(on: bool):
 
 def _alpha_pass(graph: Graph, S, M_ord, den, sh: "LayerShape", alpha, argmax, dev):
     """_attention_alpha on the current stream, or forked onto the side stream (side_alpha)."""
-    if not (_SIDE_ALPHA[0] and tuning.get("side_stream")):
+    if not (_SIDE_ALPHA[0] and tuning.get("side_stream")
+            and graph.edge_bound >= tuning.get("lds_min_edges")):
         with _span("attention_alpha", (graph.edge_bound, sh.NH)):
             _attention_alpha(graph, S, M_ord, den, sh, alpha, argmax, stream())
         return
@@ -382,7 +383,8 @@ def lds_blocks(graph: Graph, sh: LayerShape, side: bool = False):
     (csrc/edge_lds.hip; tuning edge_lds): a concat layer of <= 8 heads on a graph whose node
     blocks (gatx_graph_segments) fit the LDS image; else None. side: a first build of the blocks
     runs on the side stream (the caller joins it before the LDS pass)."""
-    if not tuning.get("edge_lds") or not sh.concat or sh.NH > 8:
+    if (not tuning.get("edge_lds") or not sh.concat or sh.NH > 8
+            or graph.edge_bound < tuning.get("lds_min_edges")):
         return None
     return graph.lds_blocks(lib.gatx_edge_lds_rows(), side)
 

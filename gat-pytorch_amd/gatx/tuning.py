@@ -21,6 +21,9 @@ threshold of one); the defaults are the measured-best choices (§
                         LDS-staged edge pass (csrc/edge_lds.hip) instead of the L2-gather one
   side_stream     1     short independent launches (node blocks, GATModel's non-final alpha
                         passes) on a second stream, under the projection GEMM
+  lds_min_edges   2^18  edge_lds / side_stream only on graphs of at least this many edges
+                        (edge_index' bound): below it a step is launch-bound, and the extra
+                        launches and cross-queue joins cost more than they save (PATTERN G=8)
 
     import gatx
     with gatx.tuning.override(edge_chunk=2245):   # or gatx.tuning.set(...) / reset()
@@ -45,6 +48,7 @@ DEFAULTS = {
     "skip_fold": 1,
     "edge_lds": 1,
     "side_stream": 1,
+    "lds_min_edges": 1 << 18,
 }
 
 _current = dict(DEFAULTS)
