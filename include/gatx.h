@@ -124,8 +124,7 @@ int gatx_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t sam, 
  * copy of W_aug, so g_x = G_aug W_aug runs with both operands k-contiguous). */
 int gatx_transpose_f32(int64_t rows, int64_t cols, const float* src, int64_t ld_src, float* dst,
                        int64_t ld_dst, gatx_stream_t stream);
-/* Arithmetic of every gatx GEMM (process-wide; env GATX_GEMM=f32|x3|f16x3 sets the initial
- * value):
+/* Arithmetic of every gatx GEMM (process-wide; nothing is read from the environment; default 2):
  * 2 = "f16x3" (default): each fp32 operand split into an fp16 plane and a 2^11-scaled fp16
  *     residual plane, three products on v_mfma_f32_32x32x16_f16 with f32 accumulation — fp32
  *     GEMM accuracy at 2x fewer MFMA cycles than x3; k-contiguous operand pairs only, and a
@@ -181,7 +180,8 @@ int gatx_absmax_rows_cols(const float* X, int64_t rows, int64_t cols, int64_t ld
                           float* colmax, gatx_stream_t stream);
 /* The arithmetic (2 f16x3, 1 x3, 0 f32) the tiled GEMMs run for an operand layout: a_kc / b_kc
  * = whether A's rows / B's columns are k-contiguous (the weight gradient G_aug^T x has neither:
- * f16x3 through gatx_gemm_wgrad with the column maxima, unless GATX_F16P=0). */
+ * f16x3 through gatx_gemm_wgrad with the column maxima; the host takes it unless gatx.tuning
+ * f16p=0). */
 int gatx_gemm_layout_mode(int a_kc, int b_kc);
 /* Diagnostic (not on the reference path): enqueue a copy of the count of f16x3 GEMM workgroups
  * that tripped the range check and recomputed their tile as x3 (each costs ~1.5x its tile) into
