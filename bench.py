@@ -473,6 +473,11 @@ def kernel_summary(summ, n_instr):
 L2_GATHER_TBS = 17.8   # the guide's L2-resident row-gather rate (16.8-18.8 TB/s, MI355X_MICROARCH.md)
 
 
+def _lds_record(info):
+    """An edge_forward record of the LDS-staged pass (gatx.functional: info ends with "lds")."""
+    return len(info) > 5 and info[5] == "lds"
+
+
 def gathered_row_bytes(E2, info):
     """Bytes of source rows one edge_forward record gathers through L2 (one row per edge): the
     reassociated first layer's 4*round4(F_in)-byte x rows (info[4] == "x", info[3] = the padded
@@ -518,7 +523,9 @@ def roofline_objects(summ, edge_bytes, pm, n_instr, pm_path="", gather_E2=None):
         by = [edge_bytes(i, info) for i, (info, _) in enumerate(edg)]
         ms_ = sum(t for _, t in edg)
         gbs = sum(by) / (ms_ * 1e-3) / 1e9
-        roofs["edge_forward"] = {"bound": "hbm", "kernel": "edge_forward_kernel<*> (all layers)",
+        roofs["edge_forward"] = {"bound": "hbm",
+                                 "kernel": "edge passes, all layers (edge_forward_shared_kernel, "
+                                           "edge_lds_kernel, edge_forward_kernel<*>)",
                                  "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                  "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
                                  "bytes_per_launch": sum(by) / len(edg),
@@ -528,19 +535,23 @@ def roofline_objects(summ, edge_bytes, pm, n_instr, pm_path="", gather_E2=None):
                                                 "once per edge; CSR, scores, den, output (+ "
                                                 "residual) once",
                                  "avg_launch_ms": ms_ / len(edg),
-                                 "_prefix": "edge_forward_kernel", "_ms": ms_,
+                                 "_prefix": ("edge_forward", "edge_lds"), "_ms": ms_,
                                  "_per_step": len(edg) / n_instr}
         if gather_E2:
             # what bounds the pass in cache-resident batches: the per-edge row gathers served by
             # L2, against the guide's L2-gather rate
-            gb = sum(gathered_row_bytes(gather_E2, info) for info, _ in edg)
-            g_tbs = gb / (ms_ * 1e-3) / 1e12
-            roofs["edge_forward"]["l2_gather"] = {
-                "achieved": round(g_tbs, 2), "peak": L2_GATHER_TBS, "unit": "TB/s",
-                "frac": round(g_tbs / L2_GATHER_TBS, 4),
-                "basis": "one source row per edge through L2 (4 NH round4(F) B, the reassociated "
-                         "layer 4 round4(F_in) B) / mean launch time; peak = the guide's "
-                         "L2-resident gather rate"}
+            # (records of the LDS-staged pass read their rows from LDS: not L2 gathers)
+            gat = [(info, t) for info, t in edg if not _lds_record(info)]
+            if gat:
+                gb = sum(gathered_row_bytes(gather_E2, info) for info, _ in gat)
+                g_tbs = gb / (sum(t for _, t in gat) * 1e-3) / 1e12
+                roofs["edge_forward"]["l2_gather"] = {
+                    "achieved": round(g_tbs, 2), "peak": L2_GATHER_TBS, "unit": "TB/s",
+                    "frac": round(g_tbs / L2_GATHER_TBS, 4),
+                    "basis": "the L2-gather passes only (not the LDS-staged one): one source row "
+                             "per edge through L2 (4 NH round4(F) B, the reassociated layer "
+                             "4 round4(F_in) B) / their mean launch time; peak = the guide's "
+                             "L2-resident gather rate"}
     if pm is not None:
         from pmc_summary import prefix_bytes_per_step
         for r in roofs.values():
@@ -564,7 +575,7 @@ TRAIN_PHASES = {
     "bwd_gemm_gx": ("mfma", ("gemm_f16p_kernel<16, 1", "gemm_f16p_kernel<32, 1",
                              "gemm_x3_kernel<true, true, true, 1,")),
     "bwd_gemm_gw": ("mfma", ("gemm_f16rc_kernel<", "gemm_x3_kernel<false, false, true, 2, 1>")),
-    "edge_forward": ("hbm", "edge_forward_kernel"),
+    "edge_forward": ("hbm", ("edge_forward", "edge_lds")),
     "bwd_edge_dst": ("hbm", "edge_bwd_dst"),
     "bwd_edge_src": ("hbm", "edge_bwd_src"),
     "bwd_prepare_go": ("hbm", "prepare_go"),
@@ -615,7 +626,7 @@ def train_gathered_row_bytes(phase, E2, info):
     edge for every head of a concat layer and once for a head-mean one (go is then shared by the
     heads). The reassociated first layer's backward is not priced (its rows are x's)."""
     if phase == "edge_forward":
-        return gathered_row_bytes(E2, info)
+        return None if _lds_record(info) else gathered_row_bytes(E2, info)
     _, _, _, nh, f, cc = info[:6]
     if len(info) > 8 and info[8]:
         return None
@@ -666,7 +677,8 @@ def train_roofline_objects(summ, price, pm, n_instr, pm_path="", gather_E2=None)
                                   "unit": "TB/s", "frac": round(g_tbs / L2_GATHER_TBS, 4),
                                   "basis": "one gathered row per edge (and head): Wh[src] in the "
                                            "forward and the destination pass, go[dst] in the "
-                                           "source pass; reassociated first layer excluded"}
+                                           "source pass; the reassociated first layer and the "
+                                           "LDS-staged pass (rows from LDS) excluded"}
         if pm is not None and prefix:
             from pmc_summary import prefix_bytes_per_step
             b = prefix_bytes_per_step(pm, prefix)

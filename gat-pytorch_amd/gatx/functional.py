@@ -585,7 +585,7 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
                  ptr(graph.perm), N, E2, sh.NH, int(sh.const), float(p), ptr(seed), ptr(rec),
                  ptr(den), ptr(alpha) if want_alpha else None,
                  ptr(argmax) if want_alpha else None, s)
-        with _span("edge_forward", (N, E2, sh.NH, sh.F, sh.concat)):
+        with _span("edge_forward", (N, E2, sh.NH, sh.F, sh.concat, "lds")):
             call("gatx_edge_lds_forward", ptr(Wh), sh.Dp, ptr(graph.rowptr), N, ptr(rec), E2,
                  ptr(segs), ptr(count), nblocks, sh.NH, sh.F, ptr(bias), ptr(out), sh.out_cols,
                  resid_p, sh.out_cols, int(elu), *drop_args, s)

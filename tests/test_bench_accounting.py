@@ -155,6 +155,30 @@ def test_roofline_traffic_is_per_record():
     assert abs(r["traffic"] - 320 / 3) < 1e-9
 
 
+def test_lds_records_in_the_edge_family():
+    """The LDS-staged pass's record (span info ending in "lds") is priced as its layer like any
+    edge record, its kernel's PMC traffic counts in the family (edge_lds_kernel beside
+    edge_forward*), and it is left out of the L2-gather rate (its rows come from LDS)."""
+    dims, flows = _ppi_flows()
+    price = bench.edge_pricer(dims, flows)
+    infos = [(N_PPI, E2_PPI, 4, 52, "x"), (N_PPI, E2_PPI, 4, 256, True, "lds"),
+             (N_PPI, E2_PPI, 6, 121, False)]
+    summ = {"edge_forward": [(infos[0], 0.05), (infos[1], 0.25), (infos[2], 0.25)]}
+    pm = {"steps": 1, "window": "marks", "kernels": {
+        "edge_forward_shared_kernel<16, 4>": {"launches": 1, "hbm_read_bytes": 10.0,
+                                              "hbm_write_bytes": 0.0},
+        "edge_lds_kernel<2, false>": {"launches": 1, "hbm_read_bytes": 20.0,
+                                      "hbm_write_bytes": 0.0},
+        "edge_forward_kernel<64, 2, 4, false>": {"launches": 2, "hbm_read_bytes": 30.0,
+                                                 "hbm_write_bytes": 0.0}}}
+    r = bench.roofline_objects(summ, price, pm, 1, gather_E2=E2_PPI)[0]
+    assert abs(r["traffic"] - (10 + 20 + 60) / 3) < 1e-9
+    assert r["bytes_per_layer"][1] == price(1, infos[1])
+    g = r["l2_gather"]
+    rows = bench.gathered_row_bytes(E2_PPI, infos[0]) + bench.gathered_row_bytes(E2_PPI, infos[2])
+    assert abs(g["achieved"] - round(rows / 0.3e-3 / 1e12, 2)) < 0.02
+
+
 def test_pmc_step_bytes_refuses_unwindowed_summaries(tmp_path):
     import json
     p = tmp_path / "old.json"

@@ -243,3 +243,35 @@ def test_side_stream_model_equals_serial(side, device):
     assert torch.equal(o0, o1) and torch.equal(r0, r1) and torch.equal(r0, o0)
     assert all(torch.equal(u, v) for u, v in zip(a0, a1))
     assert all(torch.equal(u, v) for u, v in zip(g0, g1))
+
+
+def test_lds_output_dropout_training_equals_gather(device, lds_on):
+    """GATModel training with input dropout: the next layer's dropout rides on the LDS pass's
+    epilogue (edge_lds_kernel<.., DROP=true>, gatx's counter-based mask): outputs, alphas and every
+    parameter gradient equal the L2-gather pass's to fp32 summation order."""
+    import gatx
+    from gatx import data as gd
+    from gatx import tuning
+    from gatx.config import data_config
+    cfg = dict(data_config["PPI"])
+    cfg["dropout"] = 0.3
+    b = gd.dataset_batch("PPI", 3, graph_seed=13, feature_seed=14)
+    x = torch.from_numpy(b.x).to(device)
+    ei = torch.from_numpy(b.edge_index).to(device)
+    res = []
+    for lds in (1, 0):
+        tuning.set(edge_lds=lds)
+        torch.manual_seed(0)
+        model = gatx.GATModel(**cfg).to(device).train()
+        gatx.clear_graph_cache()
+        torch.manual_seed(1)              # the per-layer dropout seeds
+        out, ei2, al = model.forward_and_return_attention(x, ei)
+        (out.square().mean() + 0.1 * model.calc_attention_norm(ei2, al)).backward()
+        res.append((out.detach().clone(), [a.detach().clone() for a in al],
+                    [p.grad.clone() for p in model.parameters()]))
+    (o1, a1, g1), (o0, a0, g0) = res
+    scale = max(1.0, float(o0.abs().max()))
+    assert float((o1 - o0).abs().max()) <= 1e-5 * scale
+    assert all(float((u - v).abs().max()) <= 1e-6 for u, v in zip(a1, a0))
+    for u, v in zip(g1, g0):
+        assert float((u - v).abs().max()) <= 1e-4 * max(1.0, float(v.abs().max()))
