@@ -368,15 +368,20 @@ __global__ void __launch_bounds__(1024) edge_lds_kernel(LdsArgs g) {   // spill 
   // records as raw 64-bit loads issued from inline asm and retired by counted vmcnt waits: the
   // compiler sinks ordinary loads to just before their use (at the 128-VGPR cap it would rather
   // wait than keep a group in flight), which left every group's latency exposed. The wait asm
-  // takes the loaded registers as in/out operands, so no use can be scheduled above it. The
-  // first group of a wave's next 16 destinations is issued during the current walk's last step,
-  // so no destination set starts with a full L2 round trip.
-  uint64_t ra[RPL], rb[RPL];
+  // takes the loaded registers as in/out operands, so no use can be scheduled above it. Groups
+  // go in pairs through a flattened loop over the wave's destination sets: step A consumes the
+  // pair in (ra, rb) while the next pair loads into (rc, rd), step B the reverse, so every
+  // register keeps one role and a pair is issued a whole pair ahead of its use (the next set's
+  // first pair during a set's last one). Targets are selected, not branched on, so every path
+  // issues the same loads (tools/check_asm_loads.py checks that no register is touched while
+  // its load is in flight).
+  uint64_t ra[RPL], rb[RPL], rc[RPL], rd[RPL];
   auto issue = [&](uint64_t (&r)[RPL], int e0, int lim) {
 #pragma unroll
     for (int u = 0; u < RPL; ++u) r[u] = load_rec(rh, min((e0 + q * RPL + u) * 8, lim));
   };
   // this lane's destination of the set starting at d0 (segment [e, end); lim: its last record)
+  // and the set's wave-uniform count of record pairs (at least 1)
   auto dest = [&](int d0, bool& live, int& dl, int& e, int& end, int& lim) {
     live = d0 + j < R;
     dl = live ? (int)order[d0 + j] : 0;
@@ -384,16 +389,21 @@ __global__ void __launch_bounds__(1024) edge_lds_kernel(LdsArgs g) {   // spill 
     end = live ? lrp[dl + 1] : 0;
     lim = (end > 0 ? end - 1 : 0) * 8;
   };
-  bool live;
-  int dl, e, end, lim;
-  dest(wave * 16, live, dl, e, end, lim);
-  issue(ra, e, lim);
-  for (int d0 = wave * 16; d0 < R; d0 += 256) {
-    bool live1;
-    int dl1, e1, end1, lim1;
-    dest(d0 + 256, live1, dl1, e1, end1, lim1);   // the next set (beyond R: empty, loads clamp)
-    const int64_t n = n0 + dl;
+  auto pairs_of = [&](int e, int end) {
+    int need = (end - e + 2 * G - 1) / (2 * G);
+    for (int off = 4; off < 64; off <<= 1) need = max(need, __shfl_xor(need, off));
+    return max(uni(need), 1);
+  };
+  int d0 = uni(wave * 16);
+  if (d0 < R) {
+    bool live, live1;
+    int dl, e, end, lim, dl1, e1, end1, lim1;
+    dest(d0, live, dl, e, end, lim);
+    dest(d0 + 256, live1, dl1, e1, end1, lim1);
+    int left = pairs_of(e, end);
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    issue(ra, e, lim);
+    issue(rb, e + G, lim);
     auto consume = [&](const uint64_t (&cur)[RPL], int e0) {
 #pragma unroll
       for (int u = 0; u < RPL; ++u) {
@@ -409,32 +419,39 @@ __global__ void __launch_bounds__(1024) edge_lds_kernel(LdsArgs g) {   // spill 
 #undef GATX_LDS_STEP
       }
     };
-    // wave-uniform trip count (groups of G records, in pairs for the ping-pong)
-    int need = (end - e + G - 1) / G;
-    for (int off = 4; off < 64; off <<= 1) need = max(need, __shfl_xor(need, off));
-    const int trips = uni(need);
-    for (int it = 0; it < trips; it += 2) {
-      issue(rb, e + G, lim);
-      wait_vm<RPL>(ra);   // ra landed; rb in flight
-      consume(ra, e);
-      if (it + 2 < trips)
-        issue(ra, e + 2 * G, lim);
-      else
-        issue(ra, e1, lim1);   // the next set's first group
-      wait_vm<RPL>(rb);
-      consume(rb, e + G);
+    // one pair: consume (c0, c1), prefetch the pair after it into (p0, p1); true when the
+    // wave's last set is done
+    auto step = [&](uint64_t (&c0)[RPL], uint64_t (&c1)[RPL], uint64_t (&p0)[RPL],
+                    uint64_t (&p1)[RPL]) {
+      const bool more = left > 1;
+      const int pe = more ? e + 2 * G : e1, pl = more ? lim : lim1;
+      issue(p0, pe, pl);
+      issue(p1, pe + G, pl);
+      wait_vm<3 * RPL>(c0);   // c0 landed; c1, p0, p1 in flight
+      consume(c0, e);
+      wait_vm<2 * RPL>(c1);
+      consume(c1, e + G);
       e += 2 * G;
+      left = uni(left - 1);   // (kept provably uniform: the set loop stays scalar control flow)
+      if (left > 0) return false;
+      if (live && f0 < g.F) lds_store<DROP>(g, n0 + dl, (int64_t)h * g.F + f0, f0, acc);
+      d0 = uni(d0 + 256);
+      if (d0 >= R) return true;
+      live = live1; dl = dl1; e = e1; end = end1; lim = lim1;
+      dest(d0 + 256, live1, dl1, e1, end1, lim1);
+      left = pairs_of(e, end);
+      acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      return false;
+    };
+    for (;;) {
+      if (step(ra, rb, rc, rd)) break;
+      if (step(rc, rd, ra, rb)) break;
     }
-    if (trips == 0) {     // ra still holds this set's (empty) first group
-      wait_vm<0>(ra);
-      issue(ra, e1, lim1);
-    }
-    const bool live_cur = live;
-    live = live1; dl = dl1; e = e1; end = end1; lim = lim1;
-    if (!live_cur || f0 >= g.F) continue;
-    lds_store<DROP>(g, n, (int64_t)h * g.F + f0, f0, acc);
   }
   wait_vm<0>(ra);   // nothing may still write these registers after the walk
+  wait_vm<0>(rb);
+  wait_vm<0>(rc);
+  wait_vm<0>(rd);
 }
 
 }  // namespace
