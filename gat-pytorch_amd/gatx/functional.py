@@ -748,6 +748,10 @@ def layer_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShape, 
     return (g_x, (g_W if need_W else None), (g_a if need_a else None), g_bias, g_resid)
 
 
+# _reassoc_backward: smallest N * C whose skip-gradient copy costs more than one more launch
+SKIP_FROM_GO_MIN = 1 << 22
+
+
 def _reassoc_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShape, p, seed,
                       saved, need_W, need_a, need_bias, out, elu, need_resid, need_skip=False):
     """Backward of the reassociated first layer when its input needs no gradient (the model
@@ -769,12 +773,18 @@ def _reassoc_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShap
     go = torch.empty((N, sh.Dp), **f32)
     C = sh.skip_cols
     # [g_s_src | g_s_dst | g_skip]: a folded skip's gradient in G_s's last columns, so the score
-    # rows' split-K GEMM also yields the skip weight's gradient
-    lds = _round4(2 * NH + C) if C else 2 * NH
+    # rows' split-K GEMM also yields the skip weight's gradient. When go already holds it (F % 4
+    # == 0: go's head-padded rows ARE the skip output's layout, C = NH F = Dp) the skip rows'
+    # GEMM reads go itself instead: no 4 N C-byte copy (184 MB at the all-skip PPI variant's L0
+    # over 20 graphs) for one more launch, so only where the copy outweighs a launch
+    skip_from_go = bool(C) and C == sh.Dp and F % 4 == 0 and N * C >= SKIP_FROM_GO_MIN
+    lds = _round4(2 * NH + C) if (C and not skip_from_go) else 2 * NH
     G_s = torch.empty((N, lds), **f32)
     g_pre, pre_ld, pre_p = None, sh.out_cols, None
-    if C:
+    if C and not skip_from_go:
         pre_ld, pre_p = lds, ptr(G_s) + 4 * 2 * NH
+    elif C:
+        pass
     elif need_resid or (need_bias and elu):
         g_pre = torch.empty((N, sh.out_cols), **f32)
         pre_p = ptr(g_pre)
@@ -815,11 +825,18 @@ def _reassoc_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShap
             call("gatx_gemm_f32_splitk_batched", NH, F, F_in, N, ptr(go), 1, sh.Dp, Fp, ptr(Z),
                  NH * Fin_p, 1, Fin_p, ptr(gW_aug), F_in, Fp * F_in, 0, ptr(ws), wb, s)
         # score rows (+ folded skip rows): G_s^T (2NH + C x N) . x (N x F_in)
-        wb2 = lib.gatx_gemm_splitk_workspace_bytes(2 * NH + C, F_in, N)
+        rows_s = 2 * NH if skip_from_go else 2 * NH + C
+        wb2 = lib.gatx_gemm_splitk_workspace_bytes(rows_s, F_in, N)
         ws2 = torch.empty(max(wb2, 1), dtype=torch.uint8, device=dev)
         with _span("bwd_gemm_gs", binfo):
-            call("gatx_gemm_f32_splitk", 2 * NH + C, F_in, N, ptr(G_s), 1, lds, ptr(x), F_in, 1,
+            call("gatx_gemm_f32_splitk", rows_s, F_in, N, ptr(G_s), 1, lds, ptr(x), F_in, 1,
                  ptr(gW_aug) + 4 * sh.Dp * F_in, F_in, 0, ptr(ws2), wb2, s)
+        if skip_from_go:   # the skip rows: go^T (C x N) . x (N x F_in)
+            wb3 = lib.gatx_gemm_splitk_workspace_bytes(C, F_in, N)
+            ws3 = torch.empty(max(wb3, 1), dtype=torch.uint8, device=dev)
+            with _span("bwd_gemm_gs", binfo):
+                call("gatx_gemm_f32_splitk", C, F_in, N, ptr(go), 1, sh.Dp, ptr(x), F_in, 1,
+                     ptr(gW_aug) + 4 * sh.K_aug * F_in, F_in, 0, ptr(ws3), wb3, s)
         g_W = torch.empty_like(W)
         g_a = torch.empty_like(a)
         with _span("bwd_weight_grads", binfo):
@@ -830,6 +847,8 @@ def _reassoc_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShap
     if need_bias and bias is not None:
         g_bias = torch.empty_like(bias)
         src_p, src_ld = (pre_p, pre_ld) if elu else (ptr(g_out), sh.out_cols)
+        if elu and pre_p is None:   # (skip_from_go: go is the gradient before ELU, same layout)
+            src_p, src_ld = ptr(go), sh.Dp
         with _span("bwd_colsum", binfo):
             call("gatx_colsum", src_p, N, sh.out_cols, src_ld, ptr(g_bias), s)
     return (None, (g_W if need_W else None), (g_a if need_a else None), g_bias,

@@ -36,9 +36,20 @@ def _skip_ref(x, Ws, NH, F, concat):
     (5, 4, 12, True, True, False, False),     # const attention, reassociated
 ])
 def test_folded_skip_layer_vs_oracle(fin, NH, F, concat, const, elu, need_x, device):
+    _check_folded_skip_layer(fin, NH, F, concat, const, elu, need_x, device, 150, 1800)
+
+
+def test_folded_skip_reassoc_large(device):
+    """The all-skip PPI variant's first layer (50 -> 4 x 256, reassociated, no input gradient)
+    at a size where the skip weight's gradient GEMM reads go directly (N C >= 2^22) instead of a
+    copy in G_s (functional._reassoc_backward skip_from_go)."""
+    _check_folded_skip_layer(50, 4, 256, True, False, True, False, device, 1400, 12000)
+
+
+def _check_folded_skip_layer(fin, NH, F, concat, const, elu, need_x, device, nodes, edges):
     import gatx
     from gatx import data as gd
-    b = gd.uniform_graph_batch(3, 150, 1800, fin, feature_seed=31 + fin)
+    b = gd.uniform_graph_batch(3, nodes, edges, fin, feature_seed=31 + fin)
     W = gd.xavier_uniform(32 + NH, NH * F, fin)
     a = gd.xavier_uniform(33 + NH, NH, NH * 2 * F)
     Ws = gd.xavier_uniform(34 + F, NH * F, fin)
