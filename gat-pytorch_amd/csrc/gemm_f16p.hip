@@ -706,21 +706,23 @@ __global__ void __launch_bounds__(256) planes_split_kernel(const float* __restri
 
 // Exact max |x| per row and per column of X (rows x cols, row stride ld): a wave takes two rows
 // at a time, all their float4 loads issued before any is used, the row max by a wave reduction,
-// every lane keeping its columns' running max over the block's rows; the block's 4 waves combine
-// in LDS, then one atomicMax per column (non-negative floats order as their bit patterns; nan
-// counts as inf; 256-B wave-instructions at the memory side). Short blocks (32 rows) and CH
-// sized to the columns keep ~5 blocks per CU resident: with 128-row blocks of 8 waves (64 KB of
-// LDS, 151 VGPRs: one block per CU, two rounds of serial row pairs) the PPI pass ran at ~2 TB/s.
+// every lane keeping its columns' running max over the block's rows; the block's kStatWaves
+// waves combine in LDS, then one atomicMax per column (non-negative floats order as their bit
+// patterns; nan counts as inf; 256-B wave-instructions at the memory side). The column atomics
+// are the cost beyond the read (tools/absmax_lab.hip, PPI G_aug 44906 x 1032: 32-row blocks of
+// 4 waves 46 us, the same without column maxima 31 us), so a block of kStatWaves waves takes
+// ~rows / kStatBlocks rows: ~2 blocks per CU, a third of the atomics, the same waves in flight
+// (33 us; the 128-row, 8-wave, 151-VGPR form of round 3 held one block per CU: ~2 TB/s).
 // colmax must be zero on entry. Either output may be NULL.
 // VEC (ld % 4 == 0, X 16-byte aligned): unconditional float4 loads (a column index past cols
 // reads column 0 of the row and is zeroed; a partial last float4 stays inside the row stride).
-constexpr int kStatRows = 32;   // rows per block (8 per wave)
+constexpr int kStatWaves = 8;
+constexpr int64_t kStatBlocks = 512;
 template <int CH, bool VEC>     // CH: 256-column chunks per lane (cols <= 256 CH)
-__global__ void __launch_bounds__(256) absmax_rows_cols_kernel(const float* __restrict__ X,
-                                                               int64_t rows, int64_t cols,
-                                                               int64_t ld, float* rowmax,
-                                                               uint32_t* colmax) {
-  __shared__ float red[4][CH * 256];
+__global__ void __launch_bounds__(64 * kStatWaves)
+absmax_rows_cols_kernel(const float* __restrict__ X, int64_t rows, int64_t cols, int64_t ld,
+                        int64_t rpb, float* rowmax, uint32_t* colmax) {
+  __shared__ float red[kStatWaves][CH * 256];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float4 cm[CH];
 #pragma unroll
@@ -742,8 +744,8 @@ __global__ void __launch_bounds__(256) absmax_rows_cols_kernel(const float* __re
     }
     return v;
   };
-  const int64_t r0 = blockIdx.x * (int64_t)kStatRows, rend = min(rows, r0 + kStatRows);
-  for (int64_t r = r0 + 2 * wave; r < rend; r += 8) {
+  const int64_t r0 = blockIdx.x * rpb, rend = min(rows, r0 + rpb);
+  for (int64_t r = r0 + 2 * wave; r < rend; r += 2 * kStatWaves) {
     const bool two = r + 1 < rend;
     const float* x0 = X + r * ld;
     const float* x1 = X + (two ? r + 1 : r) * ld;
@@ -779,8 +781,10 @@ __global__ void __launch_bounds__(256) absmax_rows_cols_kernel(const float* __re
 #pragma unroll
   for (int j = 0; j < CH; ++j) *(float4*)&red[wave][256 * j + 4 * lane] = cm[j];
   __syncthreads();
-  for (int c = threadIdx.x; c < cols; c += 256) {
-    const float v = fmaxf(fmaxf(red[0][c], red[1][c]), fmaxf(red[2][c], red[3][c]));
+  for (int c = threadIdx.x; c < cols; c += 64 * kStatWaves) {
+    float v = red[0][c];
+#pragma unroll
+    for (int w = 1; w < kStatWaves; ++w) v = fmaxf(v, red[w][c]);
     atomicMax(colmax + c, __float_as_uint(v));
   }
 }
@@ -788,13 +792,14 @@ __global__ void __launch_bounds__(256) absmax_rows_cols_kernel(const float* __re
 template <int CH>
 void launch_absmax(const float* X, int64_t rows, int64_t cols, int64_t ld, float* rowmax,
                    float* colmax, hipStream_t stream) {
-  const unsigned nb = (unsigned)ceil_div(rows, (int64_t)kStatRows);
+  const int64_t rpb = ceil_div(rows, kStatBlocks);
+  const unsigned nb = (unsigned)ceil_div(rows, rpb);
   if (ld % 4 == 0 && (uintptr_t)X % 16 == 0)
-    absmax_rows_cols_kernel<CH, true><<<nb, 256, 0, stream>>>(X, rows, cols, ld, rowmax,
-                                                             (uint32_t*)colmax);
+    absmax_rows_cols_kernel<CH, true><<<nb, 64 * kStatWaves, 0, stream>>>(X, rows, cols, ld, rpb,
+                                                                          rowmax, (uint32_t*)colmax);
   else
-    absmax_rows_cols_kernel<CH, false><<<nb, 256, 0, stream>>>(X, rows, cols, ld, rowmax,
-                                                              (uint32_t*)colmax);
+    absmax_rows_cols_kernel<CH, false><<<nb, 64 * kStatWaves, 0, stream>>>(X, rows, cols, ld, rpb,
+                                                                           rowmax, (uint32_t*)colmax);
 }
 
 }  // namespace
