@@ -313,17 +313,39 @@ __global__ void __launch_bounds__(1024) edge_lds_kernel(LdsArgs g) {   // spill 
   }
   if (k >= cnt) return;
   const int n0 = coherent_load(g.segs + k), R = coherent_load(g.segs + k + 1) - n0;
+  if (R <= 0) return;
   const int tid = threadIdx.x;
   const int F4 = g.Fp / 4;
   if (tid < kDegBins) bins[tid] = 0;
-  // stage: 4 lanes per row (64 B); pieces past the head's padded row end stage zeros
+  // stage: 4 lanes per row (64 B); pieces past the head's padded row end stage zeros. Every
+  // load of the prologue (the <= 9 row pieces of this thread and its <= 3 row-pointer pairs) is
+  // issued before the first is waited on: with one workgroup per CU nothing else covers this
+  // phase, and a load / wait / store loop paid one memory round trip per 256 rows.
+  constexpr int kStage = kLdsRows / 256;
+  float4 st[kStage];
   {
+    // unconditional loads of clamped addresses (a guarded load made the compiler wait for it
+    // before the next one went out), zeroed when consumed
     const int q = tid & 3;
     const int f4 = c * 4 + q;
-    const float4* src = (const float4*)(g.rows + (int64_t)h * g.Fp) + f4;
+    const float4* src = (const float4*)(g.rows + (int64_t)h * g.Fp) + min(f4, F4 - 1);
     const int64_t rs4 = g.row_stride / 4;
-    for (int r = tid >> 2; r < R; r += 256)
-      img[r * 4 + q] = f4 < F4 ? src[(int64_t)(n0 + r) * rs4] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int i = 0; i < kStage; ++i)
+      st[i] = src[(int64_t)(n0 + min((tid >> 2) + 256 * i, R - 1)) * rs4];
+  }
+  int lo[3], hi[3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    const int d = tid + 1024 * t;
+    lo[t] = 0; hi[t] = 0;
+    if (d <= R) lo[t] = g.rowptr[n0 + d];
+    if (d < R) hi[t] = g.rowptr[n0 + d + 1];
+  }
+#pragma unroll
+  for (int i = 0; i < kStage; ++i) {
+    const int r = (tid >> 2) + 256 * i;
+    if (r < R) img[r * 4 + (tid & 3)] = c * 4 + (tid & 3) < F4 ? st[i] : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   // destinations grouped by in-degree (a counting sort in LDS), so the 16 destinations a wave
   // walks together have similar trip counts: the walk's padding to the longest segment of the
@@ -334,11 +356,8 @@ __global__ void __launch_bounds__(1024) edge_lds_kernel(LdsArgs g) {   // spill 
 #pragma unroll
   for (int t = 0; t < 3; ++t) {
     const int d = tid + 1024 * t;
-    int lo = 0, hi = 0;
-    if (d <= R) lo = g.rowptr[n0 + d];
-    if (d < R) hi = g.rowptr[n0 + d + 1];
-    if (d <= R) lrp[d] = lo;
-    degs[t] = d < R ? min(hi - lo, kDegBins - 1) : -1;
+    if (d <= R) lrp[d] = lo[t];
+    degs[t] = d < R ? min(hi[t] - lo[t], kDegBins - 1) : -1;
   }
   __syncthreads();
 #pragma unroll

@@ -907,106 +907,123 @@ extern "C" int gatx_graph_transpose(const int32_t* col, const int32_t* rowidx, i
 constexpr int kSegMax = 4096;
 constexpr int64_t kSegMaxNodes = int64_t(1) << 17;
 
-// one wave per destination: lo / hi over its in-neighbours (lanes stride the segment)
+// 16 lanes per destination (four per wave): lo / hi over its in-neighbours, lanes striding the
+// segment (PPI's ~28-edge segments: a whole wave per destination left 3/4 of its lanes idle)
 __global__ void __launch_bounds__(256) seg_hilo_kernel(const int32_t* __restrict__ rowptr,
                                                        const int32_t* __restrict__ col, int64_t N,
                                                        int32_t* __restrict__ lo,
                                                        int32_t* __restrict__ hi) {
-  const int lane = threadIdx.x & 63;
-  const int64_t d = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (d >= N) return;
-  const int beg = rowptr[d], end = rowptr[d + 1];
+  const int sub = threadIdx.x & 15;
+  const int64_t d = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
+  const bool live = d < N;
+  const int beg = live ? rowptr[d] : 0, end = live ? rowptr[d + 1] : 0;
   int mn = (int)d, mx = (int)d;
-  for (int e = beg + lane; e < end; e += 64) {
+  for (int e = beg + sub; e < end; e += 16) {
     const int s = col[e];
     mn = min(mn, s);
     mx = max(mx, s);
   }
-  for (int off = 32; off > 0; off >>= 1) {
+  for (int off = 8; off > 0; off >>= 1) {
     mn = min(mn, __shfl_xor(mn, off));
     mx = max(mx, __shfl_xor(mx, off));
   }
-  if (lane == 0) {
+  if (live && sub == 0) {
     lo[d] = mn;
     hi[d] = mx;
   }
 }
 
-// scan pass 1 (one 1024-node tile per workgroup): within-tile inclusive prefix max of hi and
-// suffix min of lo per node, and the tile's aggregates
-__global__ void __launch_bounds__(1024) seg_tile_kernel(const int32_t* __restrict__ lo,
-                                                        const int32_t* __restrict__ hi, int64_t N,
-                                                        int32_t* __restrict__ phi,
-                                                        int32_t* __restrict__ slo,
-                                                        int32_t* __restrict__ agg) {
-  __shared__ int sa[1024], sb[1024];
-  const int t = threadIdx.x;
-  const int64_t d = (int64_t)blockIdx.x * 1024 + t;
-  const int n = (int)N;
-  sa[t] = d < N ? hi[d] : -1;
-  sb[t] = d < N ? lo[d] : n;
+// The free boundaries of one 1024-boundary tile [T0, T0 + 1024) from a window of halo H =
+// min(max_rows, kSegHalo) nodes on each side. Blocks of at most max_rows nodes can only exist if
+// every interval [lo[d], hi[d]] spans at most H nodes (its two ends share a block); under that
+// condition an interval that covers a boundary b has its destination within H of b, so the
+// prefix max of hi over [T0 - H, b) and the suffix min of lo over [b, T0 + 1024 + H) decide b
+// exactly as the whole-range scans would. A tile holding a longer interval sets its flag word and
+// the pack reports no blocks. Tiles run in parallel (no whole-range scan, no atomics); every bit
+// word and flag is rewritten on every call, so a captured step's replays recompute them.
+constexpr int kSegHalo = 4096;
+__global__ void __launch_bounds__(1024) seg_window_kernel(const int32_t* __restrict__ lo,
+                                                          const int32_t* __restrict__ hi,
+                                                          int64_t N, int H,
+                                                          uint32_t* __restrict__ bits,
+                                                          uint32_t* __restrict__ tflag) {
+  constexpr int kW = kSegHalo + 1024;
+  __shared__ int A[kW], B[kW];    // hi over [T0 - H, T0 + 1024), lo over [T0, T0 + 1024 + H)
+  __shared__ int carry_a[1024], carry_b[1024];
+  const int t = threadIdx.x, n = (int)N;
+  const int T0 = blockIdx.x * 1024, W = H + 1024;
+  for (int i = t; i < W; i += 1024) {
+    const int da = T0 - H + i, db = T0 + i;
+    A[i] = (da >= 0 && da < n) ? hi[da] : -1;
+    B[i] = db < n ? lo[db] : n;
+  }
+  const int d = T0 + t;
+  const bool lng = d < n && hi[d] - lo[d] > H;
+  __syncthreads();
+  // thread t scans A / B over [t C, t C + C) (C = ceil(W / 1024)): inclusive prefix max of A,
+  // inclusive suffix min of B; the thread aggregates are scanned across the block
+  const int C = (W + 1023) / 1024, c0 = t * C;
+  int ma = -1, mb = n;
+  for (int i = 0; i < C; ++i)
+    if (c0 + i < W) {
+      ma = max(ma, A[c0 + i]);
+      A[c0 + i] = ma;
+    }
+  for (int i = C - 1; i >= 0; --i)
+    if (c0 + i < W) {
+      mb = min(mb, B[c0 + i]);
+      B[c0 + i] = mb;
+    }
+  carry_a[t] = ma;
+  carry_b[t] = mb;
   __syncthreads();
   for (int off = 1; off < 1024; off <<= 1) {
-    const int a = t >= off ? sa[t - off] : -1;
-    const int b = t + off < 1024 ? sb[t + off] : n;
+    const int x = t >= off ? carry_a[t - off] : -1;
+    const int y = t + off < 1024 ? carry_b[t + off] : n;
     __syncthreads();
-    sa[t] = max(sa[t], a);
-    sb[t] = min(sb[t], b);
+    carry_a[t] = max(carry_a[t], x);
+    carry_b[t] = min(carry_b[t], y);
     __syncthreads();
   }
-  if (d < N) {
-    phi[d] = sa[t];
-    slo[d] = sb[t];
-  }
-  if (t == 0) {
-    agg[2 * blockIdx.x] = sa[1023];
-    agg[2 * blockIdx.x + 1] = sb[0];
-  }
-}
-
-// scan pass 2: the free boundaries as a bit set (bit b: 0 < b < N, max_{d<b} hi[d] < b and
-// min_{d>=b} lo[d] >= b), one 64-bit ballot per wave. Every word is rewritten on every call: no
-// memset, no atomics, nothing that differs between two runs on the same CSR (a captured step's
-// replays recompute identical words)
-__global__ void __launch_bounds__(1024) seg_free_kernel(const int32_t* __restrict__ phi,
-                                                        const int32_t* __restrict__ slo,
-                                                        const int32_t* __restrict__ agg,
-                                                        int64_t N, int ntiles,
-                                                        uint32_t* __restrict__ bits) {
-  __shared__ int pre_hi, suf_lo;
-  const int t = threadIdx.x, k = blockIdx.x;
-  const int n = (int)N;
-  if (t == 0) {   // aggregates of the tiles before / after this one (<= 128 tiles)
-    int a = -1, b = n;
-    for (int i = 0; i < k; ++i) a = max(a, agg[2 * i]);
-    for (int i = k + 1; i < ntiles; ++i) b = min(b, agg[2 * i + 1]);
-    pre_hi = a;
-    suf_lo = b;
+  {
+    const int pa = t > 0 ? carry_a[t - 1] : -1, pb = t < 1023 ? carry_b[t + 1] : n;
+    for (int i = 0; i < C; ++i)
+      if (c0 + i < W) {
+        A[c0 + i] = max(A[c0 + i], pa);
+        B[c0 + i] = min(B[c0 + i], pb);
+      }
   }
   __syncthreads();
-  const int64_t bd = (int64_t)k * 1024 + t;   // boundary between nodes bd - 1 and bd
+  // boundary b = T0 + t: max hi over d < b is A[H + t - 1], min lo over d >= b is B[t]
   bool fr = false;
-  if (bd > 0 && bd < N) {
-    const int before = t > 0 ? max(pre_hi, phi[bd - 1]) : pre_hi;   // max hi over d < bd
-    const int after = min(suf_lo, slo[bd]);                           // min lo over d >= bd
-    fr = before < (int)bd && after >= (int)bd;
+  if (d > 0 && d < n) {
+    const int before = H + t >= 1 ? A[H + t - 1] : -1;
+    fr = before < d && B[t] >= d;
   }
   const uint64_t m = __ballot(fr);
   const int lane = t & 63;
-  const int64_t w = bd >> 5;   // this lane's 32-bit word (lanes 0 and 32 write them)
+  const int64_t w = (int64_t)d >> 5;
   if ((lane & 31) == 0 && w < ceil_div(N, (int64_t)64) * 2)
     bits[w] = (uint32_t)(lane == 0 ? m : m >> 32);
+  if (__syncthreads_or(lng) && t == 0) tflag[blockIdx.x] = 1u;
+  else if (t == 0) tflag[blockIdx.x] = 0u;
 }
 
-// pack: the free boundaries in order (a block-wide scan of the words' popcounts), then the
-// gap-free runs packed greedily into blocks of <= max_rows nodes (thread 0)
+// pack: no blocks if a tile flagged a long interval; else the free boundaries in order (a
+// block-wide scan of the words' popcounts), then the gap-free runs packed greedily into blocks of
+// <= max_rows nodes (thread 0)
 __global__ void __launch_bounds__(1024) seg_pack_kernel(const uint32_t* __restrict__ bits,
-                                                        int64_t N, int max_rows,
+                                                        const uint32_t* __restrict__ tflag,
+                                                        int ntiles, int64_t N, int max_rows,
                                                         int32_t* __restrict__ segs,
                                                         int32_t* __restrict__ seg_count) {
   __shared__ int bnd[kSegMax + 2];
   __shared__ int wsum[16];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, n = (int)N;
+  if (__syncthreads_or(t < ntiles && tflag[t] != 0u)) {
+    if (t == 0) *seg_count = -1;
+    return;
+  }
   const int64_t nw = ceil_div(N, (int64_t)64) * 2;   // words (<= 2^17 / 32 = 4096)
   int base = 0;
   for (int64_t w0 = 0; w0 < nw; w0 += 1024) {
@@ -1062,9 +1079,9 @@ __global__ void seg_none_kernel(int32_t* seg_count) {
 }
 
 extern "C" size_t gatx_graph_segments_workspace_bytes(int64_t N) {
-  const size_t nn = align256(sizeof(int32_t) * (size_t)(N > 0 ? N : 1));
-  return 4 * nn + align256(sizeof(int32_t) * 2 * (size_t)ceil_div(N > 0 ? N : 1, 1024)) +
-         align256(sizeof(uint32_t) * 2 * (size_t)ceil_div(N > 0 ? N : 1, 64));
+  const size_t n1 = (size_t)(N > 0 ? N : 1);
+  return 2 * align256(sizeof(int32_t) * n1) + align256(sizeof(uint32_t) * 2 * ceil_div(n1, 64)) +
+         align256(sizeof(uint32_t) * ceil_div(n1, 1024));
 }
 
 extern "C" int gatx_graph_segments(const int32_t* rowptr, const int32_t* col, int64_t N,
@@ -1078,24 +1095,22 @@ extern "C" int gatx_graph_segments(const int32_t* rowptr, const int32_t* col, in
     return 0;
   }
   GATX_REQUIRE(ws_bytes >= gatx_graph_segments_workspace_bytes(N), "graph_segments: workspace");
-  const size_t nn = align256(sizeof(int32_t) * (size_t)(N > 0 ? N : 1));
-  const int ntiles = (int)ceil_div(N > 0 ? N : 1, (int64_t)1024);
+  const size_t n1 = (size_t)(N > 0 ? N : 1);
   char* p = (char*)ws;
-  int32_t* lo = (int32_t*)p; p += nn;
-  int32_t* hi = (int32_t*)p; p += nn;
-  int32_t* phi = (int32_t*)p; p += nn;
-  int32_t* slo = (int32_t*)p; p += nn;
-  int32_t* agg = (int32_t*)p; p += align256(sizeof(int32_t) * 2 * (size_t)ntiles);
-  uint32_t* bits = (uint32_t*)p;
+  int32_t* lo = (int32_t*)p; p += align256(sizeof(int32_t) * n1);
+  int32_t* hi = (int32_t*)p; p += align256(sizeof(int32_t) * n1);
+  uint32_t* bits = (uint32_t*)p; p += align256(sizeof(uint32_t) * 2 * ceil_div(n1, 64));
+  uint32_t* tflag = (uint32_t*)p;
+  const int ntiles = (int)ceil_div(n1, 1024);   // <= 128
   if (N > 0) {
-    seg_hilo_kernel<<<(unsigned)ceil_div(N, (int64_t)4), 256, 0, st>>>(rowptr, col, N, lo, hi);
+    seg_hilo_kernel<<<(unsigned)ceil_div(N, (int64_t)16), 256, 0, st>>>(rowptr, col, N, lo, hi);
     GATX_LAUNCH_CHECK("graph_segments hilo");
-    seg_tile_kernel<<<(unsigned)ntiles, 1024, 0, st>>>(lo, hi, N, phi, slo, agg);
-    GATX_LAUNCH_CHECK("graph_segments tile");
-    seg_free_kernel<<<(unsigned)ntiles, 1024, 0, st>>>(phi, slo, agg, N, ntiles, bits);
-    GATX_LAUNCH_CHECK("graph_segments free");
+    seg_window_kernel<<<(unsigned)ntiles, 1024, 0, st>>>(lo, hi, N, std::min(max_rows, kSegHalo),
+                                                         bits, tflag);
+    GATX_LAUNCH_CHECK("graph_segments window");
   }
-  seg_pack_kernel<<<1, 1024, 0, st>>>(bits, N, max_rows, segs, seg_count);
+  seg_pack_kernel<<<1, 1024, 0, st>>>(bits, tflag, N > 0 ? ntiles : 0, N, max_rows, segs,
+                                      seg_count);
   GATX_LAUNCH_CHECK("graph_segments pack");
   return 0;
 }

@@ -283,6 +283,14 @@ def _alpha_pass(graph: Graph, S, M_ord, den, sh: "LayerShape", alpha, argmax, de
     from .graph import side_stream, _SIDE_PENDING
     side = side_stream(dev)
     side.wait_stream(torch.cuda.current_stream(dev))
+    # the pass outlives the caller's references under no_grad (the autograd ctx that holds S /
+    # den / argmax is dropped when apply returns): mark every buffer it touches as in use on the
+    # side stream, so the caching allocator cannot hand one to the next layer's GEMM before the
+    # pass has finished with it (LazyAlpha.materialize does the same)
+    ei = graph._ei_flat if graph._ei_flat is not None else graph.source
+    for t in (S, M_ord, den, argmax, alpha, ei, graph.rowptr, graph.perm, graph.meta):
+        if t is not None:
+            t.record_stream(side)
     with torch.cuda.stream(side):
         with _span("attention_alpha", (graph.edge_bound, sh.NH)):
             _attention_alpha(graph, S, M_ord, den, sh, alpha, argmax, stream())
@@ -378,13 +386,20 @@ def _edge_pass(rows, row_stride, S, M_ord, graph, sh, bias, p, seed, out, resid_
                  *(drop_args if last else (0.0, None)), None, s)
 
 
+LDS_MAX_EDGES = 1 << 28   # edge_lds.hip: 32-bit record byte offsets
+LDS_MAX_NODES = 1 << 25   # edge_lds.hip: records hold 64 src in an int32
+
+
 def lds_blocks(graph: Graph, sh: LayerShape, side: bool = False):
     """(segs, count, n_blocks) when this layer's edge pass takes the LDS-staged kernels
     (csrc/edge_lds.hip; tuning edge_lds): a concat layer of <= 8 heads on a graph whose node
     blocks (gatx_graph_segments) fit the LDS image; else None. side: a first build of the blocks
-    runs on the side stream (the caller joins it before the LDS pass)."""
+    runs on the side stream (the caller joins it before the LDS pass). Graphs past the kernels'
+    index limits take the L2-gather pass: the records hold 64 src in an int32 (N < 2^25) and the
+    walk addresses them by 32-bit byte offsets (E' < 2^28, gatx_edge_lds_forward's check)."""
     if (not tuning.get("edge_lds") or not sh.concat or sh.NH > 8
-            or graph.edge_bound < tuning.get("lds_min_edges")):
+            or graph.edge_bound < tuning.get("lds_min_edges")
+            or graph.edge_bound >= LDS_MAX_EDGES or graph.num_nodes >= LDS_MAX_NODES):
         return None
     return graph.lds_blocks(lib.gatx_edge_lds_rows(), side)
 

@@ -110,7 +110,7 @@ class Graph:
         # |edge_index'| promised by the caller (expect_num_edges): answers num_edges without a
         # device read (so a captured step may return edge_index' / alpha); checked against the
         # device count whenever that is read
-        self._E2_hint = _HINTS.get(_hint_key(edge_index, N, add_self_loops))
+        self._E2_hint = _hint_lookup(edge_index, N, add_self_loops)
         self._error = None
         self._edge_index = None
         # non-blocking validation: the meta lands in pinned memory behind an event
@@ -307,7 +307,22 @@ def expect_num_edges(edge_index: torch.Tensor, num_nodes: int, add_self_loops: b
     if num_edges is None:
         _HINTS.pop(k, None)
     else:
-        _HINTS[k] = int(num_edges)
+        # the promise is bound to this tensor object at its current version: an in-place rewrite
+        # of it, or another tensor the allocator later places at the same address, finds no
+        # promise (and the count is read from the device as usual)
+        _HINTS[k] = (int(num_edges), version(edge_index), weakref.ref(edge_index))
+
+
+def _hint_lookup(edge_index: torch.Tensor, num_nodes, add_self_loops: bool):
+    """The count promised by expect_num_edges for exactly this tensor, unmodified since; else
+    None."""
+    hit = _HINTS.get(_hint_key(edge_index, num_nodes, add_self_loops))
+    if hit is None:
+        return None
+    n, ver, ref = hit
+    if ref() is not edge_index or version(edge_index) != ver:
+        return None
+    return n
 
 
 _SIDE: dict = {}

@@ -19,8 +19,12 @@ threshold of one); the defaults are the measured-best choices (§
   skip_fold       1     GATModel's Linear skips folded into the projection GEMM
   edge_lds        1     concat layers on graphs cut into node blocks of <= 2304 nodes: the
                         LDS-staged edge pass (csrc/edge_lds.hip) instead of the L2-gather one
-  side_stream     1     short independent launches (node blocks, GATModel's non-final alpha
-                        passes) on a second stream, under the projection GEMM
+  side_stream     0     short independent launches (node blocks, GATModel's non-final alpha
+                        passes) on a second stream, under the projection GEMM. Off since round 6:
+                        with the windowed node-block build (~21 us serial) the fork / join gaps
+                        of a replayed graph (~5-9 us each) and the alpha pass sharing CUs with the
+                        output projection cost more than the overlap saved (PPI fwd 1.427 serial
+                        vs 1.435 ms, interleaved A/B, profiles/r08d)
   lds_min_edges   2^18  edge_lds / side_stream only on graphs of at least this many edges
                         (edge_index' bound): below it a step is launch-bound, and the extra
                         launches and cross-queue joins cost more than they save (PATTERN G=8)
@@ -47,7 +51,7 @@ DEFAULTS = {
     "dropout_fuse": 1,
     "skip_fold": 1,
     "edge_lds": 1,
-    "side_stream": 1,
+    "side_stream": 0,
     "lds_min_edges": 1 << 18,
 }
 

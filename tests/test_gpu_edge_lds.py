@@ -275,3 +275,44 @@ def test_lds_output_dropout_training_equals_gather(device, lds_on):
     assert all(float((u - v).abs().max()) <= 1e-6 for u, v in zip(a1, a0))
     for u, v in zip(g1, g0):
         assert float((u - v).abs().max()) <= 1e-4 * max(1.0, float(v.abs().max()))
+
+
+def test_side_alpha_pass_keeps_its_buffers(device, monkeypatch):
+    """The side-stream alpha pass of a no_grad forward (tuning side_stream=1) reads S, M_ord, den
+    and writes argmax / alpha after the caller has dropped them: a delayed pass (a sleep on the
+    side stream ahead of it) must still read its own buffers, not blocks the caching allocator
+    handed to the next layer's projection GEMM (functional._alpha_pass records them on the side
+    stream). Alphas and outputs equal the one-stream forward bitwise."""
+    import gatx
+    from gatx import data as gd
+    from gatx import functional as gf
+    from gatx import tuning
+    from gatx.config import data_config
+    b = gd.dataset_batch("PPI", 3, graph_seed=19, feature_seed=20)
+    x = torch.from_numpy(b.x).to(device)
+    ei = torch.from_numpy(b.edge_index).to(device)
+    torch.manual_seed(0)
+    model = gatx.GATModel(**data_config["PPI"]).to(device).eval()
+    res = []
+    orig = gf._attention_alpha
+
+    def delayed(*a, **k):
+        torch.cuda._sleep(20_000_000)   # ~10 ms on the stream the pass runs on
+        return orig(*a, **k)
+
+    try:
+        for sd in (0, 1):
+            tuning.set(side_stream=sd, lds_min_edges=0)
+            if sd:
+                monkeypatch.setattr(gf, "_attention_alpha", delayed)
+            gatx.clear_graph_cache()
+            with torch.no_grad():
+                out, _, al = model.forward_and_return_attention(x, ei)
+            torch.cuda.synchronize()
+            res.append((out.clone(), [a.clone() for a in al]))
+    finally:
+        tuning.reset()
+    (o0, a0), (o1, a1) = res
+    assert torch.equal(o0, o1)
+    for u, v in zip(a0, a1):
+        assert torch.equal(u, v)

@@ -89,3 +89,46 @@ def test_split_gemm_kernel_choices(monkeypatch):
     finally:
         lib.gatx_set_gemm_mode(2)
         tuning.reset()
+
+
+def test_lds_pass_bounded_by_its_index_limits():
+    """The LDS-staged pass is chosen only inside the kernels' index limits: E' < 2^28 (32-bit
+    record byte offsets) and N < 2^25 (64 src in an int32); past them the layer takes the
+    L2-gather pass instead of raising in gatx_edge_lds_forward (no GPU call: a stand-in graph)."""
+    from gatx import functional as gf
+    from gatx.functional import LayerShape
+
+    class FakeGraph:
+        def __init__(self, edge_bound, num_nodes):
+            self.edge_bound, self.num_nodes = edge_bound, num_nodes
+
+        def lds_blocks(self, max_rows, side=False):
+            return ("segs", "count", 20)
+
+    sh = LayerShape(4, 256, 1024, True, False)
+    assert gf.lds_blocks(FakeGraph(1 << 21, 44900), sh) is not None
+    assert gf.lds_blocks(FakeGraph((1 << 28) - 1, 44900), sh) is not None
+    assert gf.lds_blocks(FakeGraph(1 << 28, 44900), sh) is None
+    assert gf.lds_blocks(FakeGraph(1 << 21, (1 << 25) - 1), sh) is not None
+    assert gf.lds_blocks(FakeGraph(1 << 21, 1 << 25), sh) is None
+    assert gf.lds_blocks(FakeGraph(1 << 10, 100), sh) is None    # below lds_min_edges
+
+
+def test_edge_count_promise_bound_to_tensor_and_version():
+    """expect_num_edges binds its promise to the tensor object at its current version: an in-place
+    rewrite, or another tensor at the same address, finds no promise (CPU tensors: the lookup
+    reads only identity, shape and version)."""
+    import torch
+    from gatx.graph import expect_num_edges, _hint_lookup
+    ei = torch.zeros(2, 10, dtype=torch.int64)
+    expect_num_edges(ei, 5, True, 13)
+    assert _hint_lookup(ei, 5, True) == 13
+    assert _hint_lookup(ei, 6, True) is None
+    alias = ei.view(2, 10)             # same storage and shape, another tensor object
+    assert _hint_lookup(alias, 5, True) is None
+    ei.add_(1)                         # rewritten in place
+    assert _hint_lookup(ei, 5, True) is None
+    expect_num_edges(ei, 5, True, 14)
+    assert _hint_lookup(ei, 5, True) == 14
+    expect_num_edges(ei, 5, True, None)
+    assert _hint_lookup(ei, 5, True) is None

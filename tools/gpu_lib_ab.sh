@@ -1,0 +1,22 @@
+#!/bin/bash
+# Interleaved A/B of library builds on one box: the same bench.py command against each .so
+# (loaded through GATX_LIB), round-robin, so box and clock drift hit every variant alike.
+#   bash tools/gpu_lib_ab.sh TAG ROUNDS "BENCH ARGS" LIB_A LIB_B ...
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/$1; mkdir -p "$OUT"; shift
+ROUNDS=$1; shift
+COMMON=$1; shift
+cd "$R"
+for r in $(seq 1 "$ROUNDS"); do
+  i=0
+  for lib in "$@"; do
+    i=$((i+1))
+    GATX_LIB=$R/$lib timeout -k 10 300 python bench.py --no-cpu-baseline $COMMON > "$OUT/v${i}_r${r}.json" 2> "$OUT/v${i}_r${r}.err" || { echo "variant $i round $r failed rc=$?"; tail -5 "$OUT/v${i}_r${r}.err"; exit 1; }
+    python - "$OUT/v${i}_r${r}.json" "$lib" <<'PY'
+import json, sys
+d = json.load(open(sys.argv[1]))
+k = {a: round(b["total_ms_per_step"], 4) for a, b in d.get("kernels", {}).items()}
+print(f"{sys.argv[2]:32s} {d['ms_per_step']:.4f} {k}")
+PY
+  done
+done
