@@ -850,6 +850,75 @@ def dry_run(args, world: int, rank: int, local: int) -> int:
     return 0
 
 
+def replay_check(replay, eager, out, alphas, eager_alphas, x, x_alt):
+    """Proof that a replay of the captured step does its work (verdict r5: a stale node-block
+    count once made the LDS pass skip its work on every timed replay, invisible because the
+    buffers still held the previous replay's results). The static input x is replaced by x_alt,
+    the captured step's static output and every layer's static alpha are poisoned with NaN by
+    launches outside the graph (what triggered that bug), the graph is replayed once and its
+    output / alphas compared BITWISE with an eager step on x_alt; x is restored after. A pass
+    that skips its work leaves NaN or values of the old input in some layer, and every later layer
+    inherits them. Returns (ok, detail)."""
+    keep = x.clone()
+    try:
+        x.copy_(x_alt)
+        out.fill_(float("nan"))
+        for a in alphas:
+            a.fill_(float("nan"))
+        replay()
+        got_out = out.clone()
+        got_al = [a.clone() for a in alphas]
+        ref_out = eager().clone()
+        ref_al = eager_alphas()
+        if x.is_cuda:
+            torch.cuda.synchronize()
+        bad = []
+        if not torch.equal(got_out, ref_out):
+            bad.append("output")
+        for i, (g, r) in enumerate(zip(got_al, ref_al)):
+            n = r.shape[0]
+            if g.shape[0] < n or not torch.equal(g[:n], r):
+                bad.append(f"alpha[{i}]")
+        return not bad, ("bitwise equal to an eager step" if not bad
+                         else "differs from an eager step: " + ", ".join(bad))
+    finally:
+        x.copy_(keep)
+
+
+def train_leg_command(args) -> list:
+    """The default forward run's second leg (BASELINE config 3, PPI 3-layer fwd+bwd train step,
+    models/ppi_gat.py:15-33): this bench in --mode train as a child process (its own model,
+    optimizer and captured step), with the same steps / warmup / graphs / tuning switches."""
+    cmd = [sys.executable, os.path.abspath(__file__), "--mode", "train", "--no-cpu-baseline",
+           "--no-train-leg", "--steps", str(args.steps), "--warmup", str(args.warmup)]
+    if args.graphs is not None:
+        cmd += ["--graphs", str(args.graphs)]
+    for t in args.tune:
+        cmd += ["--tune", t]
+    return cmd
+
+
+def train_leg_keys(line: dict) -> dict:
+    """The train leg's figures as extra keys of the forward line (never `value`)."""
+    return {"train_ms_per_step": line["ms_per_step"],
+            "train_value": line["value"],
+            "train_unit": line["unit"],
+            "train_roofline_time_frac": line.get("roofline_time_frac"),
+            "train_roofline": line.get("roofline"),
+            "train_workload": line["config"]["workload"],
+            "train_launch": line["config"].get("launch")}
+
+
+def run_train_leg(args) -> dict:
+    import subprocess
+    proc = subprocess.run(train_leg_command(args), stdout=subprocess.PIPE, text=True,
+                          timeout=900)
+    if proc.returncode != 0:
+        raise SystemExit(f"bench.py: the train leg failed (rc {proc.returncode})")
+    lines = [ln for ln in proc.stdout.splitlines() if ln.startswith("{")]
+    return train_leg_keys(json.loads(lines[-1]))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -882,6 +951,9 @@ def main():
     ap.add_argument("--verify", action="store_true",
                     help="after timing, compare one more timed-path step's output with an eager "
                          "step's (stderr; diagnostic)")
+    ap.add_argument("--no-train-leg", action="store_true",
+                    help="skip the forward run's train-step leg (train_* keys; a child "
+                         "bench.py --mode train, N=1 only)")
     ap.add_argument("--dry-run", action="store_true",
                     help="exercise the launch path only: --gpus N starts N ranks, each joins a "
                          "gloo group and runs the barrier / max-over-ranks timing around an empty "
@@ -1040,8 +1112,12 @@ def main():
 
     eager_step = step
     from gatx.capture import CapturedStep
+    static_att = None
     if use_graph:
         step = CapturedStep(eager_step)
+        # the captured forward's static alphas (each layer's (graph, alpha) as the capture left
+        # it; later eager steps rebind the layers' attributes), for the replay check
+        static_att = [l.__dict__.get("_attention") for l in model.gat_layer_list]
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -1060,6 +1136,18 @@ def main():
                                        step.eager if use_graph else None, instr_outside)
     _lib.call("gatx_gemm_fallback_read", _lib.ptr(fb), 1, _lib.stream())
     fallback_tiles = int(fb.item())
+    replay_verified = None
+    replay_detail = None
+    if use_graph and args.mode == "fwd" and static_att and all(
+            a is not None and isinstance(a[1], torch.Tensor) for a in static_att):
+        gen = torch.Generator(device=dev).manual_seed(2024 + rank)
+        x_alt = torch.randn(x.shape, generator=gen, device=dev, dtype=x.dtype)
+
+        def _eager_alphas():
+            return [l.normalised_attention_coeffs.clone() for l in model.gat_layer_list]
+        replay_verified, replay_detail = replay_check(
+            step.graph.replay, step.eager, step.out, [a for _, a in static_att], _eager_alphas,
+            x, x_alt)
     if args.verify and args.mode == "fwd":
         from gatx.graph import graph_cache as _gcv
         o1 = step().clone()
@@ -1171,11 +1259,22 @@ def main():
         "roofline_other": ordered[1] if len(ordered) > 1 else None,
         "kernels": kernel_summary(summ, n_instr),
     }
+    if replay_verified is not None:
+        result["replay_verified"] = replay_verified
+        result["replay_check"] = ("after the timed loop: static input replaced, static output and "
+                                  "every layer's alpha poisoned with NaN outside the graph, one "
+                                  "replay; " + replay_detail)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.mode == "fwd":
         result["cpu_baseline"] = cpu_baseline(model, cfg, ds, 8 if ds == "PATTERN" else 1)
     result["config"]["tuning"] = tuning_changes()
+    if (rank == 0 and world == 1 and args.mode == "fwd" and ds == "PPI"
+            and not args.no_train_leg):
+        result.update(run_train_leg(args))
     if rank == 0:
         print(json.dumps(result), flush=True)
+    if replay_verified is False:
+        raise SystemExit("bench.py: a replay of the captured step differs from an eager step ("
+                         + replay_detail + ")")
     if reducer is not None:
         reducer.remove()
     if world > 1:

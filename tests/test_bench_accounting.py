@@ -324,3 +324,72 @@ def test_bench_dry_run_launches_8_ranks():
     assert d["n_gpus"] == 8 and d["dry_run"] and d["steps"] == 3
     assert sorted(r for r, _ in d["ranks"]) == list(range(8))
     assert sorted(lr for _, lr in d["ranks"]) == list(range(8))
+
+
+# ---- replay check and train leg ------------------------------------------
+
+def _fake_capture(x, stale: bool):
+    """A stand-in captured step over CPU tensors: `replay` recomputes out / alpha from x (or, with
+    stale=True, leaves them as the previous replay wrote them — round 5's skipped LDS pass)."""
+    import torch
+    out = torch.zeros(4, 3)
+    alpha = torch.zeros(10, 2)
+
+    def compute():
+        return x[:4, :3] * 2.0, x.sum() * torch.ones(7, 2)
+
+    def replay():
+        if not stale:
+            o, a = compute()
+            out.copy_(o)
+            alpha[:7].copy_(a)
+
+    def eager():
+        return compute()[0]
+
+    def eager_alphas():
+        return [compute()[1]]
+    replay()
+    return replay, eager, out, [alpha], eager_alphas
+
+
+def test_replay_check_passes_a_working_replay():
+    import torch
+    x = torch.randn(8, 5)
+    replay, eager, out, alphas, eal = _fake_capture(x, stale=False)
+    keep = x.clone()
+    ok, detail = bench.replay_check(replay, eager, out, alphas, eal, x, torch.randn(8, 5))
+    assert ok, detail
+    assert torch.equal(x, keep)   # the static input is restored
+
+
+def test_replay_check_catches_a_replay_that_skips_its_work():
+    """A replay that writes nothing (stale buffers from the previous replay, all values right
+    for the OLD input) must fail: the check changes the input and poisons the outputs first."""
+    import torch
+    x = torch.randn(8, 5)
+    replay, eager, out, alphas, eal = _fake_capture(x, stale=True)
+    ok, detail = bench.replay_check(replay, eager, out, alphas, eal, x, torch.randn(8, 5))
+    assert not ok and "output" in detail and "alpha[0]" in detail
+
+
+def test_forward_run_carries_the_train_leg():
+    """The driver's default `bench.py --gpus 1` runs the PPI train step (BASELINE config 3) as a
+    second leg with the same steps / warmup / tuning, and its figures ride as train_* keys."""
+    import argparse
+    args = argparse.Namespace(steps=20, warmup=3, graphs=None, tune=["edge_lds=1"])
+    cmd = bench.train_leg_command(args)
+    assert cmd[1].endswith("bench.py")
+    i = cmd.index("--mode")
+    assert cmd[i + 1] == "train" and "--no-train-leg" in cmd and "--no-cpu-baseline" in cmd
+    assert cmd[cmd.index("--steps") + 1] == "20" and cmd[cmd.index("--warmup") + 1] == "3"
+    assert cmd[cmd.index("--tune") + 1] == "edge_lds=1"
+    line = {"ms_per_step": 4.5, "value": 8.5e8, "unit": "layer-edges/s",
+            "roofline_time_frac": 0.26, "roofline": {"bound": "mfma"},
+            "config": {"workload": "PPI 3-layer GAT train", "launch": "hipGraph replay"}}
+    keys = bench.train_leg_keys(line)
+    assert keys["train_ms_per_step"] == 4.5 and keys["train_roofline_time_frac"] == 0.26
+    assert keys["train_value"] == 8.5e8 and keys["train_workload"].startswith("PPI")
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert "result.update(run_train_leg(args))" in src
+    assert '"replay_verified"' in src

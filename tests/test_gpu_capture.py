@@ -162,3 +162,52 @@ def test_captured_ppi_train_step_equals_eager(device, interleave):
     finally:
         expect_num_edges(ei, b.num_nodes, True, None)
         gatx.clear_graph_cache()
+
+
+@pytest.mark.parametrize("G,lds_min", [(3, 0), (20, None)])
+def test_replay_does_its_work_with_poisoned_outputs(G, lds_min, device):
+    """replays compared with outputs that persist across replays cannot catch a
+    pass that skips its work (round 5's stale node-block count left the LDS pass idle on every
+    timed replay while the buffers held the previous replay's results). Here every replay gets a
+    NEW input, its static output and every layer's alpha are poisoned with NaN by launches
+    outside the graph, and the replay must equal an eager step on that input bitwise
+    (bench.replay_check, what the driver's bench run reports as replay_verified). The LDS pass,
+    the node blocks and the records pass are on (lds_min_edges=0 for the 3-graph batch; the
+    default threshold at the headline's 20 graphs)."""
+    import os
+    import sys
+    import gatx
+    from gatx import tuning
+    from gatx.capture import CapturedStep
+    from gatx.config import data_config
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    if lds_min is not None:
+        tuning.set(lds_min_edges=lds_min)
+    try:
+        torch.manual_seed(0)
+        model = gatx.GATModel(**data_config["PPI"]).to(device).eval()
+        x, ei, _ = _batch("PPI", G, device, seed=31)
+
+        def step():
+            gatx.clear_graph_cache()
+            with torch.no_grad():
+                return model(x, ei)
+
+        cap = CapturedStep(step)
+        static = [layer.__dict__["_attention"][1] for layer in model.gat_layer_list]
+        from gatx.functional import lds_blocks, LayerShape
+        from gatx.graph import graph_cache
+        g = graph_cache.get(ei, x.shape[0], True)
+        assert lds_blocks(g, LayerShape(4, 256, 1024, True, False)) is not None   # LDS path on
+
+        def eager_alphas():
+            return [layer.normalised_attention_coeffs.clone() for layer in model.gat_layer_list]
+        gen = torch.Generator(device=device).manual_seed(5)
+        for _ in range(4):
+            x_alt = torch.randn(x.shape, generator=gen, device=device)
+            ok, detail = bench.replay_check(cap.graph.replay, cap.eager, cap.out, static,
+                                            eager_alphas, x, x_alt)
+            assert ok, detail
+    finally:
+        tuning.reset()

@@ -11,7 +11,7 @@ for r in $(seq 1 "$ROUNDS"); do
   for v in "$@"; do
     i=$((i+1))
     [ "$v" = "-" ] && v=""
-    timeout -k 10 300 python bench.py --no-cpu-baseline $COMMON $v > "$OUT/v${i}_r${r}.json" 2> "$OUT/v${i}_r${r}.err" || { echo "variant $i round $r failed rc=$?"; tail -5 "$OUT/v${i}_r${r}.err"; exit 1; }
+    timeout -k 10 300 python bench.py --no-cpu-baseline --no-train-leg $COMMON $v > "$OUT/v${i}_r${r}.json" 2> "$OUT/v${i}_r${r}.err" || { echo "variant $i round $r failed rc=$?"; tail -5 "$OUT/v${i}_r${r}.err"; exit 1; }
     python - "$OUT/v${i}_r${r}.json" "$v" <<'PY'
 import json, sys
 d = json.load(open(sys.argv[1]))

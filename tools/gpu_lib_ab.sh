@@ -11,7 +11,7 @@ for r in $(seq 1 "$ROUNDS"); do
   i=0
   for lib in "$@"; do
     i=$((i+1))
-    GATX_LIB=$R/$lib timeout -k 10 300 python bench.py --no-cpu-baseline $COMMON > "$OUT/v${i}_r${r}.json" 2> "$OUT/v${i}_r${r}.err" || { echo "variant $i round $r failed rc=$?"; tail -5 "$OUT/v${i}_r${r}.err"; exit 1; }
+    GATX_LIB=$R/$lib timeout -k 10 300 python bench.py --no-cpu-baseline --no-train-leg $COMMON > "$OUT/v${i}_r${r}.json" 2> "$OUT/v${i}_r${r}.err" || { echo "variant $i round $r failed rc=$?"; tail -5 "$OUT/v${i}_r${r}.err"; exit 1; }
     python - "$OUT/v${i}_r${r}.json" "$lib" <<'PY'
 import json, sys
 d = json.load(open(sys.argv[1]))

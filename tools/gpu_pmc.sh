@@ -12,7 +12,7 @@ i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "GRBM_GUI_ACTIVE SQ_WAVES"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace -d "$OUT/${NAME}_p$i" -o run \
-    --output-format csv -- python3 "$R/bench.py" --no-cpu-baseline "$@" \
+    --output-format csv -- python3 "$R/bench.py" --no-cpu-baseline --no-train-leg "$@" \
     > "$OUT/${NAME}_p$i.log" 2>&1
   rc=$?
   echo "pmc pass $i ($grp) rc=$rc"

@@ -18,14 +18,14 @@ step bench_rmat timeout -k 10 400 python "$R/bench.py" --workload rmat --steps 5
 step bench_ppi2 timeout -k 10 300 python "$R/bench.py" --graphs 2 --mode train --no-cpu-baseline > "$OUT/bench_ppi2_train.json" 2> "$OUT/bench_ppi2_train.err"
 step bench_pattern timeout -k 10 300 python "$R/bench.py" --workload pattern --graphs 8 --mode train --no-cpu-baseline > "$OUT/bench_pattern_train.json" 2> "$OUT/bench_pattern_train.err"
 cd /tmp && export TMPDIR=/tmp
-step prof_fwd timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_fwd" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/prof_fwd.log" 2>&1
+step prof_fwd timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_fwd" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-train-leg > "$OUT/prof_fwd.log" 2>&1
 step prof_train timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_train" -o run --output-format csv -- python3 "$R/bench.py" --mode train --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/prof_train.log" 2>&1
 step prof_rmat timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_rmat" -o run --output-format csv -- python3 "$R/bench.py" --workload rmat --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/prof_rmat.log" 2>&1
 step prof_pattern timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_pattern" -o run --output-format csv -- python3 "$R/bench.py" --workload pattern --graphs 8 --mode train --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/prof_pattern.log" 2>&1
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "GRBM_GUI_ACTIVE SQ_WAVES"; do
   i=$((i+1))
-  step pmc$i timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace -d "$OUT/pmc_p$i" -o run --output-format csv -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc_p$i.log" 2>&1
+  step pmc$i timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace -d "$OUT/pmc_p$i" -o run --output-format csv -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-train-leg > "$OUT/pmc_p$i.log" 2>&1
 done
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "GRBM_GUI_ACTIVE SQ_WAVES"; do
