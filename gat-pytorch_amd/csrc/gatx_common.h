@@ -113,6 +113,12 @@ __device__ inline float get4(const float4& v, int j) {
   return j == 0 ? v.x : (j == 1 ? v.y : (j == 2 ? v.z : v.w));
 }
 
+// n 32-bit words set to 0 (the library's zero fill: no hipMemsetAsync inside a captured step)
+static __global__ void zero_words_kernel(uint32_t* p, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = 0u;
+}
+
 // Intra-wave LDS hand-off: order this wave's LDS writes before its later LDS reads.
 __device__ inline void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

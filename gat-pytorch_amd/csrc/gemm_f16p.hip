@@ -813,7 +813,15 @@ int read_f16p_fallbacks(unsigned long long* dst, int reset, hipStream_t stream) 
 int absmax_rows_cols(const float* X, int64_t rows, int64_t cols, int64_t ld, float* rowmax,
                      float* colmax, hipStream_t stream) {
   GATX_REQUIRE(cols <= 2048, "absmax_rows_cols: at most 2048 columns");
-  if (colmax) GATX_CALL(hipMemsetAsync(colmax, 0, cols * sizeof(float), stream));
+  // zeroed by a kernel, not hipMemsetAsync: inside a captured hipGraph the memset node was not
+  // ordered before the atomicMax kernel once a kernel had run outside the graph between replays
+  // (PPI train step: the stale maxima of the previous replay sent every weight-gradient tile of
+  // the second layer to the x3 fallback, 270 -> 570 us; the same failure as round 5's node-block
+  // count)
+  if (colmax) {
+    zero_words_kernel<<<(unsigned)ceil_div(cols, (int64_t)256), 256, 0, stream>>>((uint32_t*)colmax, cols);
+    GATX_LAUNCH_CHECK("absmax_rows_cols zero");
+  }
   if (rows == 0) return 0;
   if (cols <= 512) launch_absmax<2>(X, rows, cols, ld, rowmax, colmax, stream);
   else if (cols <= 1024) launch_absmax<4>(X, rows, cols, ld, rowmax, colmax, stream);

@@ -1127,11 +1127,10 @@ extern "C" int gatx_graph_hub_plan(const int32_t* rowptr, int64_t N, int hub_edg
                                    gatx_stream_t s) {
   GATX_REQUIRE(hub_edges > 0 && N >= 0, "graph_hub_plan: bad arguments");
   hipStream_t st = (hipStream_t)s;
-  const hipError_t e = hipMemsetAsync(hub_count, 0, sizeof(int32_t), st);
-  if (e != hipSuccess) {
-    set_error("graph_hub_plan: %s", hipGetErrorString(e));
-    return (int)e;
-  }
+  // a kernel, not hipMemsetAsync (memset nodes of a captured step were not ordered before the
+  // next kernel once a kernel had run outside the graph: gemm_f16p.hip absmax_rows_cols)
+  zero_words_kernel<<<1, 64, 0, st>>>((uint32_t*)hub_count, 1);
+  GATX_LAUNCH_CHECK("graph_hub_plan zero");
   if (N == 0) return 0;
   const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(N, 256), 8192);
   hub_plan_kernel<<<grid, 256, 0, st>>>(rowptr, N, hub_edges, hubs, hub_bound, hub_count);
