@@ -190,6 +190,8 @@ struct LdsArgs {
   float out_p;
   const uint64_t* out_seed;
   int vec_out;               // F % 4 == 0 and 16-byte aligned rows of out / resid
+  int64_t ocols;             // output row width: NH F (concat) or F (head mean)
+  int nranges;               // head-mean kernel: destination ranges per node block
 };
 
 template <bool DROP>
@@ -198,7 +200,7 @@ __device__ inline float lds_epilogue(float v, const LdsArgs& g, int64_t n, int64
   if (g.resid) v += g.resid[n * g.resid_ld + col];
   if (g.elu) v = elu_act(v);
   if (DROP)
-    v = dropout_keep(*g.out_seed, n * (int64_t)(g.NH * g.F) + col, g.out_p) ? v * (1.f / (1.f - g.out_p))
+    v = dropout_keep(*g.out_seed, n * g.ocols + col, g.out_p) ? v * (1.f / (1.f - g.out_p))
                                                                           : 0.f;
   return v;
 }
@@ -223,7 +225,7 @@ __device__ inline void lds_store(const LdsArgs& g, int64_t n, int64_t cb, int f0
     }
     if (DROP) {
       const float sc = 1.f / (1.f - g.out_p);
-      const int64_t base = n * (int64_t)(g.NH * g.F) + cb;
+      const int64_t base = n * g.ocols + cb;
       const uint64_t sd = *g.out_seed;
       o.x = dropout_keep(sd, base, g.out_p) ? o.x * sc : 0.f;
       o.y = dropout_keep(sd, base + 1, g.out_p) ? o.y * sc : 0.f;
@@ -473,6 +475,225 @@ __global__ void __launch_bounds__(1024) edge_lds_kernel(LdsArgs g) {   // spill 
   wait_vm<0>(rd);
 }
 
+
+// ---- head mean (round 6): PPI's last layer, out[n] = mean_h sum_e alpha~[e,h] Wh[src,h,:] + bias
+// (models/gat_layer.py:117-135 with concat=False). One workgroup per (node block, 16-float chunk,
+// destination range): the heads are staged one after another into the same image and every
+// head's walk adds into the same registers, so the head mean is fused, with no per-head partials
+// in memory and no cross-workgroup combine. 12 waves (768 threads: 168 VGPRs per lane) hold four
+// float4 set accumulators per lane across the heads, so a range is at most 768 destinations and
+// PPI's 2245-node blocks split into three: 20 blocks x 8 chunks x 3 ranges = 480 workgroups.
+// Each head's first record pair is issued before that head's rows are staged, so the two memory
+// round trips overlap.
+constexpr int kMeanThreads = 768;
+constexpr int kMeanWaves = kMeanThreads / 64;
+constexpr int kMeanStride = 16 * kMeanWaves;              // destinations per sweep of the waves
+constexpr int kMeanSets = 4;                              // sweeps (set accumulators per lane)
+constexpr int kMeanRange = kMeanStride * kMeanSets;       // 768 destinations per workgroup
+constexpr int kMeanStage = (kLdsRows + kMeanThreads / 4 - 1) / (kMeanThreads / 4);
+static_assert(kMeanRange <= kMeanThreads, "the degree sort gives each thread one destination");
+
+// fallback of the head-mean walk (see lds_global_walk): node range split evenly, rows from
+// global memory, heads summed in order
+template <bool DROP>
+__device__ __attribute__((always_inline)) void lds_global_walk_mean(const LdsArgs& g,
+                                                                    int64_t unit, int64_t units,
+                                                                    int c) {
+  const int64_t per = ceil_div(g.N, units);
+  const int64_t n0 = unit * per;
+  const int64_t R = min(per, g.N - n0);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane & 3, j = lane >> 2;
+  const int f0 = c * kChunk + q * 4;
+  const float inv = 1.f / (float)g.NH;
+  for (int64_t d0 = wave * 16; d0 < R; d0 += kMeanStride) {
+    if (d0 + j >= R) continue;
+    const int64_t n = n0 + d0 + j;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (f0 < g.Fp)
+      for (int h = 0; h < g.NH; ++h) {
+        const int2* rh = g.rec + (int64_t)h * g.E_bound;
+        const float* base = g.rows + (int64_t)h * g.Fp + f0;
+        float4 ah = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int e = g.rowptr[n], end = g.rowptr[n + 1]; e < end; ++e) {
+          const int2 r = rh[e];
+          const float4 v = *(const float4*)(base + (int64_t)(r.x >> 6) * g.row_stride);
+          ah = fma4(__int_as_float(r.y), v, ah);
+        }
+        acc = add4(acc, ah);
+      }
+    if (f0 < g.F) lds_store<DROP>(g, n, f0, f0, acc * inv);
+  }
+}
+
+template <int RPL, bool DROP>
+__global__ void __launch_bounds__(kMeanThreads) edge_lds_mean_kernel(LdsArgs g) {
+  __shared__ __attribute__((aligned(16))) float4 img[kLdsRows * 4];
+  __shared__ unsigned short order[kMeanRange];   // the range's destinations, grouped by degree
+  __shared__ int lrp[kMeanRange + 1];             // the range's row pointers
+  __shared__ int bins[kDegBins];
+  const int64_t b = xcd_contiguous(blockIdx.x, gridDim.x);   // the ranges and chunks of one
+  const int nr = g.nranges;                                   // block run on one XCD: its
+  const int rr = (int)(b % nr);                               // records stay in that L2
+  const int c = (int)((b / nr) % g.nchunks);
+  const int64_t k = b / ((int64_t)nr * g.nchunks);
+  const int cnt = coherent_load(g.seg_count);
+  if (cnt < 0 || cnt > g.seg_bound) {
+    lds_global_walk_mean<DROP>(g, k * nr + rr, g.seg_bound * nr, c);
+    return;
+  }
+  if (k >= cnt) return;
+  const int n0 = coherent_load(g.segs + k), R = coherent_load(g.segs + k + 1) - n0;
+  if (R <= 0) return;
+  const int r0 = (int)((int64_t)R * rr / nr);
+  const int Rr = (int)((int64_t)R * (rr + 1) / nr) - r0;   // <= ceil(kLdsRows / nr) <= kMeanRange
+  if (Rr <= 0) return;
+  const int tid = threadIdx.x;
+  const int F4 = g.Fp / 4;
+  if (tid < kDegBins) bins[tid] = 0;
+  int deg = -1;
+  if (tid < Rr) {
+    const int lo = g.rowptr[n0 + r0 + tid], hi = g.rowptr[n0 + r0 + tid + 1];
+    lrp[tid] = lo;
+    if (tid == Rr - 1) lrp[Rr] = hi;
+    deg = min(hi - lo, kDegBins - 1);
+  }
+  __syncthreads();
+  if (deg >= 0) atomicAdd(&bins[deg], 1);
+  __syncthreads();
+  if (tid < 64) {
+    const int v = bins[tid];
+    int x = v;
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(x, off);
+      if (tid >= off) x += y;
+    }
+    bins[tid] = x - v;
+  }
+  __syncthreads();
+  if (deg >= 0) order[atomicAdd(&bins[deg], 1)] = (unsigned short)tid;
+  const int lane = tid & 63, wave = tid >> 6, q = lane & 3, j = lane >> 2;
+  const int qb = 16 * q - 64 * n0;
+  const char* imgb = (const char*)img;
+  const int f0 = c * kChunk + q * 4;
+  constexpr int G = 4 * RPL;
+  const int64_t rs4 = g.row_stride / 4;
+  const bool walker = wave * 16 < Rr;   // wave-uniform: this wave has destinations
+  float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0, a2 = a0, a3 = a0;
+  uint64_t ra[RPL], rb[RPL], rc[RPL], rd[RPL];
+  // records of head h at byte hoff = 8 E_bound h past g.rec (the asm loads' scalar base: a kernel
+  // argument; 8 NH E_bound < 2^32, checked by the entry point)
+  uint32_t hoff = 0;
+  const int2* const rec0 = g.rec;
+  auto issue = [&](uint64_t (&r)[RPL], int e0, int lim) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < RPL; ++u)
+      r[u] = load_rec(rec0, (int)(hoff + (uint32_t)min((e0 + q * RPL + u) * 8, lim)));
+  };
+  auto dest = [&](int d0, int& e, int& end, int& lim) __attribute__((always_inline)) {
+    const bool live = d0 + j < Rr;
+    const int dl = live ? (int)order[d0 + j] : 0;
+    e = live ? lrp[dl] : 0;
+    end = live ? lrp[dl + 1] : 0;
+    lim = (end > 0 ? end - 1 : 0) * 8;
+  };
+  auto pairs_of = [&](int e, int end) __attribute__((always_inline)) {
+    int need = (end - e + 2 * G - 1) / (2 * G);
+    for (int off = 4; off < 64; off <<= 1) need = max(need, __shfl_xor(need, off));
+    return max(uni(need), 1);
+  };
+  for (int h = 0; h < g.NH; ++h) {
+    __syncthreads();   // h = 0: order / lrp written; h > 0: every wave is done with head h - 1
+    hoff = (uint32_t)uni((int)((uint32_t)h * (uint32_t)g.E_bound * 8u));
+    // this head's first record pair, in flight while its rows are staged
+    int e = 0, end = 0, lim = 0, e1 = 0, end1 = 0, lim1 = 0;
+    int d0 = uni(wave * 16);
+    if (walker) {
+      dest(d0, e, end, lim);
+      dest(d0 + kMeanStride, e1, end1, lim1);
+      issue(ra, e, lim);
+      issue(rb, e + G, lim);
+    }
+    {
+      const int f4 = c * 4 + (tid & 3);
+      const float4* src = (const float4*)(g.rows + (int64_t)h * g.Fp) + min(f4, F4 - 1);
+      float4 st[kMeanStage];
+#pragma unroll
+      for (int i = 0; i < kMeanStage; ++i)
+        st[i] = src[(int64_t)(n0 + min((tid >> 2) + kMeanThreads / 4 * i, R - 1)) * rs4];
+#pragma unroll
+      for (int i = 0; i < kMeanStage; ++i) {
+        const int r = (tid >> 2) + kMeanThreads / 4 * i;
+        if (r < R) img[r * 4 + (tid & 3)] = f4 < F4 ? st[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+    __syncthreads();
+    if (walker) {
+      int left = pairs_of(e, end);
+      int s = 0;   // the wave's set index (uniform)
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      auto consume = [&](const uint64_t (&cur)[RPL], int e0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int u = 0; u < RPL; ++u) {
+          const bool ok = e0 + q * RPL + u < end;
+          const int cx = ok ? (int)(uint32_t)cur[u] : 64 * n0;
+          const int cy = ok ? (int)(uint32_t)(cur[u] >> 32) : 0;
+#define GATX_LDS_STEP(T)                                                        \
+          {                                                                     \
+            const float4 v = *(const float4*)(imgb + (quad_bcast<T>(cx) + qb)); \
+            acc = fma4(__int_as_float(quad_bcast<T>(cy)), v, acc);              \
+          }
+          GATX_LDS_STEP(0) GATX_LDS_STEP(1) GATX_LDS_STEP(2) GATX_LDS_STEP(3)
+#undef GATX_LDS_STEP
+        }
+      };
+      auto step = [&](uint64_t (&c0)[RPL], uint64_t (&c1)[RPL], uint64_t (&p0)[RPL],
+                      uint64_t (&p1)[RPL]) __attribute__((always_inline)) {
+        const bool more = left > 1;
+        const int pe = more ? e + 2 * G : e1, pl = more ? lim : lim1;
+        issue(p0, pe, pl);
+        issue(p1, pe + G, pl);
+        wait_vm<3 * RPL>(c0);
+        consume(c0, e);
+        wait_vm<2 * RPL>(c1);
+        consume(c1, e + G);
+        e += 2 * G;
+        left = uni(left - 1);
+        if (left > 0) return false;
+        // the set's sum into its accumulator (selects, not branches: static registers)
+        a0 = s == 0 ? add4(a0, acc) : a0;
+        a1 = s == 1 ? add4(a1, acc) : a1;
+        a2 = s == 2 ? add4(a2, acc) : a2;
+        a3 = s == 3 ? add4(a3, acc) : a3;
+        s = uni(s + 1);
+        d0 = uni(d0 + kMeanStride);
+        if (d0 >= Rr) return true;
+        e = e1; end = end1; lim = lim1;
+        dest(d0 + kMeanStride, e1, end1, lim1);
+        left = pairs_of(e, end);
+        acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        return false;
+      };
+      for (;;) {
+        if (step(ra, rb, rc, rd)) break;
+        if (step(rc, rd, ra, rb)) break;
+      }
+      wait_vm<0>(ra);   // the pair prefetched past the last set lands before the next head
+      wait_vm<0>(rb);
+      wait_vm<0>(rc);
+      wait_vm<0>(rd);
+    }
+  }
+  if (!walker || f0 >= g.F) return;
+  const float inv = 1.f / (float)g.NH;
+#pragma unroll
+  for (int s = 0; s < kMeanSets; ++s) {
+    const int d = wave * 16 + kMeanStride * s + j;
+    if (d < Rr) {
+      const float4 a = s == 0 ? a0 : (s == 1 ? a1 : (s == 2 ? a2 : a3));
+      lds_store<DROP>(g, n0 + r0 + (int)order[d], f0, f0, a * inv);
+    }
+  }
+}
 }  // namespace
 
 extern "C" int gatx_edge_lds_rows(void) { return kLdsRows; }
@@ -527,6 +748,7 @@ extern "C" int gatx_edge_lds_forward(const float* rows, int64_t row_stride,
   g.NH = NH; g.F = F; g.Fp = Fp; g.nchunks = (int)ceil_div(Fp, kChunk);
   g.bias = bias; g.out = out; g.out_ld = out_ld; g.resid = resid; g.resid_ld = resid_ld;
   g.elu = elu; g.out_p = out_p; g.out_seed = out_seed;
+  g.ocols = (int64_t)NH * F; g.nranges = 1;
   auto al = [](const void* p, int64_t ld) { return p == nullptr || ((uintptr_t)p % 16 == 0 && ld % 4 == 0); };
   g.vec_out = (F % 4 == 0) && al(out, out_ld) && al(resid, resid_ld) && al(bias, 0);
   const int64_t blocks = seg_bound * NH * g.nchunks;
@@ -536,6 +758,43 @@ extern "C" int gatx_edge_lds_forward(const float* rows, int64_t row_stride,
   else
     edge_lds_kernel<kRPL, false><<<(unsigned)blocks, 1024, 0, (hipStream_t)s>>>(g);
   GATX_LAUNCH_CHECK("edge_lds_forward");
+  return 0;
+}
+
+extern "C" int gatx_edge_lds_mean_forward(const float* rows, int64_t row_stride,
+                                          const int32_t* rowptr, int64_t N, const void* rec,
+                                          int64_t E_bound, const int32_t* segs,
+                                          const int32_t* seg_count, int64_t seg_bound, int NH,
+                                          int F, const float* bias, float* out, int64_t out_ld,
+                                          const float* resid, int64_t resid_ld, int elu,
+                                          float out_p, const uint64_t* out_seed,
+                                          gatx_stream_t s) {
+  const int Fp = (int)round_up(F, 4);
+  GATX_REQUIRE(NH >= 1 && NH <= 8 && F >= 1 && N >= 0 && seg_bound >= 0 &&
+                   E_bound < (1ll << 28) && row_stride >= (int64_t)NH * Fp &&
+                   row_stride % 4 == 0 && (uintptr_t)rows % 16 == 0,
+               "edge_lds_mean_forward: bad arguments");
+  // (a head-mean layer feeding another layer's input dropout takes the L2-gather pass: the
+  // dropout variant of this kernel ran out of scalar registers for the records' base)
+  GATX_REQUIRE(out_p == 0.f, "edge_lds_mean_forward: no fused output dropout");
+  GATX_REQUIRE((int64_t)NH * E_bound * 8 < (1ll << 32),
+               "edge_lds_mean_forward: records past 32-bit offsets");
+  if (seg_bound == 0) return 0;
+  LdsArgs g;
+  g.rows = rows; g.row_stride = row_stride; g.rowptr = rowptr; g.rec = (const int2*)rec;
+  g.E_bound = E_bound; g.segs = segs; g.seg_count = seg_count; g.seg_bound = seg_bound;
+  g.N = N;
+  g.NH = NH; g.F = F; g.Fp = Fp; g.nchunks = (int)ceil_div(Fp, kChunk);
+  g.bias = bias; g.out = out; g.out_ld = out_ld; g.resid = resid; g.resid_ld = resid_ld;
+  g.elu = elu; g.out_p = out_p; g.out_seed = out_seed;
+  g.ocols = F;
+  g.nranges = (int)ceil_div(kLdsRows, kMeanRange);   // every block's range fits kMeanRange
+  auto al = [](const void* p, int64_t ld) { return p == nullptr || ((uintptr_t)p % 16 == 0 && ld % 4 == 0); };
+  g.vec_out = (F % 4 == 0) && al(out, out_ld) && al(resid, resid_ld) && al(bias, 0);
+  const int64_t blocks = seg_bound * g.nranges * g.nchunks;
+  GATX_REQUIRE(blocks < (1ll << 31), "edge_lds_mean_forward: too many workgroups");
+  edge_lds_mean_kernel<kRPL, false><<<(unsigned)blocks, kMeanThreads, 0, (hipStream_t)s>>>(g);
+  GATX_LAUNCH_CHECK("edge_lds_mean_forward");
   return 0;
 }
 

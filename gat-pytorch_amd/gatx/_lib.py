@@ -68,6 +68,8 @@ SIGNATURES = {
     "gatx_edge_records": (c_i, [P, P, P, P, P, c_i64, c_i64, c_i, c_i, c_f, P, P, P, P, P, P]),
     "gatx_edge_lds_forward": (c_i, [P, c_i64, P, c_i64, P, c_i64, P, P, c_i64, c_i, c_i, P, P, c_i64,
                                     P, c_i64, c_i, c_f, P, P]),
+    "gatx_edge_lds_mean_forward": (c_i, [P, c_i64, P, c_i64, P, c_i64, P, P, c_i64, c_i, c_i, P, P,
+                                         c_i64, P, c_i64, c_i, c_f, P, P]),
     "gatx_pad_rows": (c_i, [P, c_i64, c_i64, c_i64, P, c_i64, P]),
     "gatx_projection_gemm": (c_i, [c_i64, c_i64, c_i64, P, c_i64, c_i64, P, c_i64, c_i64, P,
                                    c_i64, c_i64, P, c_i64, P, c_sz, P]),

@@ -390,16 +390,21 @@ LDS_MAX_EDGES = 1 << 28   # edge_lds.hip: 32-bit record byte offsets
 LDS_MAX_NODES = 1 << 25   # edge_lds.hip: records hold 64 src in an int32
 
 
-def lds_blocks(graph: Graph, sh: LayerShape, side: bool = False):
+def lds_blocks(graph: Graph, sh: LayerShape, side: bool = False, out_p: float = 0.0):
     """(segs, count, n_blocks) when this layer's edge pass takes the LDS-staged kernels
-    (csrc/edge_lds.hip; tuning edge_lds): a concat layer of <= 8 heads on a graph whose node
+    (csrc/edge_lds.hip; tuning edge_lds, and edge_lds_mean for head-mean layers): a layer of <= 8
+    heads on a graph whose node
     blocks (gatx_graph_segments) fit the LDS image; else None. side: a first build of the blocks
     runs on the side stream (the caller joins it before the LDS pass). Graphs past the kernels'
     index limits take the L2-gather pass: the records hold 64 src in an int32 (N < 2^25) and the
-    walk addresses them by 32-bit byte offsets (E' < 2^28, gatx_edge_lds_forward's check)."""
-    if (not tuning.get("edge_lds") or not sh.concat or sh.NH > 8
+    walk addresses them by 32-bit byte offsets (E' < 2^28, gatx_edge_lds_forward's check; the
+    head-mean walk all heads' records from one base: 8 NH E' < 2^32; and it fuses no output
+    dropout)."""
+    if (not tuning.get("edge_lds") or (not sh.concat and not tuning.get("edge_lds_mean"))
+            or sh.NH > 8
             or graph.edge_bound < tuning.get("lds_min_edges")
-            or graph.edge_bound >= LDS_MAX_EDGES or graph.num_nodes >= LDS_MAX_NODES):
+            or graph.edge_bound >= LDS_MAX_EDGES or graph.num_nodes >= LDS_MAX_NODES
+            or (not sh.concat and (8 * sh.NH * graph.edge_bound >= (1 << 32) or out_p > 0))):
         return None
     return graph.lds_blocks(lib.gatx_edge_lds_rows(), side)
 
@@ -553,7 +558,7 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
         saved.update(S=S, reassoc=True, Z=Z, x_rows=x_rows)
         return out, alpha, saved
     # node blocks of an LDS-staged layer: built on the side stream while the projection GEMM runs
-    blocks = lds_blocks(graph, sh, side=True)
+    blocks = lds_blocks(graph, sh, side=True, out_p=out_p)
     Wh = torch.empty((N, sh.Dp), **f32)
     S = torch.empty((N, max(sh.H2, 1)), **f32)
     # the weight operand pre-split into fp16 planes (gemm_f16p.hip; None: in-loop split)
@@ -601,7 +606,8 @@ def layer_forward(x, W, a, bias, graph: Graph, sh: LayerShape, p: float, seed: i
                  ptr(den), ptr(alpha) if want_alpha else None,
                  ptr(argmax) if want_alpha else None, s)
         with _span("edge_forward", (N, E2, sh.NH, sh.F, sh.concat, "lds")):
-            call("gatx_edge_lds_forward", ptr(Wh), sh.Dp, ptr(graph.rowptr), N, ptr(rec), E2,
+            call("gatx_edge_lds_forward" if sh.concat else "gatx_edge_lds_mean_forward",
+                 ptr(Wh), sh.Dp, ptr(graph.rowptr), N, ptr(rec), E2,
                  ptr(segs), ptr(count), nblocks, sh.NH, sh.F, ptr(bias), ptr(out), sh.out_cols,
                  resid_p, sh.out_cols, int(elu), *drop_args, s)
         if not want_alpha:

@@ -19,6 +19,8 @@ threshold of one); the defaults are the measured-best choices (§
   skip_fold       1     GATModel's Linear skips folded into the projection GEMM
   edge_lds        1     concat layers on graphs cut into node blocks of <= 2304 nodes: the
                         LDS-staged edge pass (csrc/edge_lds.hip) instead of the L2-gather one
+  edge_lds_mean   1     head-mean layers take it too (gatx_edge_lds_mean_forward: every head
+                        staged in turn, the mean kept in registers), round 6
   side_stream     0     short independent launches (node blocks, GATModel's non-final alpha
                         passes) on a second stream, under the projection GEMM. Off since round 6:
                         with the windowed node-block build (~21 us serial) the fork / join gaps
@@ -51,6 +53,7 @@ DEFAULTS = {
     "dropout_fuse": 1,
     "skip_fold": 1,
     "edge_lds": 1,
+    "edge_lds_mean": 1,
     "side_stream": 0,
     "lds_min_edges": 1 << 18,
 }

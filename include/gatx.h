@@ -436,6 +436,19 @@ int gatx_edge_lds_forward(const float* rows, int64_t row_stride, const int32_t* 
                           int out_features, const float* bias, float* out, int64_t out_ld,
                           const float* resid, int64_t resid_ld, int elu, float out_p,
                           const uint64_t* out_seed, gatx_stream_t stream);
+/* gatx_edge_lds_mean_forward (round 6) — head-mean layers (concat = False, models/gat_layer.py
+ *   :128-135: out = mean over heads, then bias): one workgroup per (node block, 16-float chunk,
+ *   destination range of <= 768 nodes) stages every head's chunk in turn and adds each head's
+ *   alpha~-weighted rows into the same registers, so the mean needs no partials in memory; then
+ *   bias / resid / ELU. Same arguments, records (from gatx_edge_records), fallback and limits
+ *   as gatx_edge_lds_forward, and 8 * num_heads * E_bound < 2^32; out_p must be 0 (a head-mean
+ *   layer that feeds the next layer's input dropout takes gatx_edge_forward_drop). */
+int gatx_edge_lds_mean_forward(const float* rows, int64_t row_stride, const int32_t* rowptr,
+                               int64_t num_nodes, const void* rec, int64_t E_bound,
+                               const int32_t* segs, const int32_t* seg_count, int64_t seg_bound,
+                               int num_heads, int out_features, const float* bias, float* out,
+                               int64_t out_ld, const float* resid, int64_t resid_ld, int elu,
+                               float out_p, const uint64_t* out_seed, gatx_stream_t stream);
 
 /* ---------------------------------------------------------------- backward (autograd of above) */
 

@@ -48,21 +48,46 @@ def test_lds_path_is_taken(device, lds_on):
              "edge_trailing_isolated", "cora_l0_trained", "ppi_small_l2")}
     assert took["ppi_small_l1"] and took["ppi_full_l1"]
     assert not took["cora_l0_trained"]    # one 2708-node component: no block fits the image
-    assert not took["ppi_small_l2"]       # head mean: the L2-gather pass
+    assert took["ppi_small_l2"]           # head mean (round 6: gatx_edge_lds_mean_forward)
     assert not took["edge_dropout"]       # narrow input: the reassociated first-layer pass
 
 
-@pytest.mark.parametrize("G,n,e,fin,NH,F,dropout", [
-    (3, 300, 4000, 64, 2, 16, 0.0),       # several blocks
-    (3, 300, 4000, 64, 2, 16, 0.6),       # attention dropout through the records
-    (2, 200, 3000, 16, 3, 7, 0.0),        # F % 4 != 0: scalar epilogue, padded chunk
-    (1, 2245, 61318, 512, 8, 64, 0.0),    # one full PPI-size graph, 8 heads
-    (1, 2300, 20000, 64, 4, 20, 0.0),     # a block near the 2304-row image
-    (2, 2000, 9000, 96, 4, 40, 0.3),      # blocks packed over two graphs
+@pytest.mark.parametrize("G,n,e,fin,NH,F,dropout,concat", [
+    (3, 300, 4000, 64, 2, 16, 0.0, True),       # several blocks
+    (3, 300, 4000, 64, 2, 16, 0.6, True),       # attention dropout through the records
+    (2, 200, 3000, 16, 3, 7, 0.0, True),        # F % 4 != 0: scalar epilogue, padded chunk
+    (1, 2245, 61318, 512, 8, 64, 0.0, True),    # one full PPI-size graph, 8 heads
+    (1, 2300, 20000, 64, 4, 20, 0.0, True),     # a block near the 2304-row image
+    (2, 2000, 9000, 96, 4, 40, 0.3, True),      # blocks packed over two graphs
+    # head mean (round 6, gatx_edge_lds_mean_forward): heads staged in turn, the mean in registers
+    (3, 300, 4000, 64, 6, 16, 0.0, False),      # several blocks, one range each
+    (1, 2245, 61318, 256, 6, 121, 0.0, False),  # PPI L2's shape on one full graph: 3 ranges,
+                                                # a partial last chunk (124 = 7.75 x 16)
+    (2, 2000, 9000, 96, 4, 40, 0.3, False),     # attention dropout, blocks over two graphs
+    (1, 2300, 20000, 64, 3, 20, 0.0, False),    # a block near the 2304-row image
+    (3, 300, 3000, 16, 1, 1, 0.0, False),       # PATTERN's last layer: one head, one feature
+    (2, 200, 3000, 16, 8, 7, 0.0, False),       # 8 heads, F % 4 != 0
 ])
-def test_lds_vs_oracle(G, n, e, fin, NH, F, dropout, device, lds_on):
+def test_lds_vs_oracle(G, n, e, fin, NH, F, dropout, concat, device, lds_on):
     from test_gpu_layer import _layer_vs_oracle
-    _layer_vs_oracle(device, G, n, e, fin, NH, F, True, dropout=dropout)
+    _layer_vs_oracle(device, G, n, e, fin, NH, F, concat, dropout=dropout)
+
+
+def test_lds_mean_path_is_taken(device, lds_on):
+    """The head-mean cases above really run the LDS-staged mean kernel: the host selects it for
+    a head-mean layer whose graph cuts into blocks, not for one with a fused output dropout."""
+    import gatx
+    from gatx import data as gd
+    from gatx import functional as gf
+    from gatx.graph import graph_cache
+    b = gd.uniform_graph_batch(1, 2245, 61318, 256, feature_seed=5)
+    gatx.clear_graph_cache()
+    g = graph_cache.get(torch.from_numpy(b.edge_index).to(device), b.num_nodes, True)
+    sh = gf.LayerShape(6, 121, 256, False, False)
+    assert gf.lds_blocks(g, sh) is not None
+    assert gf.lds_blocks(g, sh, out_p=0.5) is None
+    gatx.tuning.set(edge_lds_mean=0)
+    assert gf.lds_blocks(g, sh) is None
 
 
 @pytest.mark.parametrize("name", MODEL_CASES)
