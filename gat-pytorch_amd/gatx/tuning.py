@@ -26,7 +26,8 @@ threshold of one); the defaults are the measured-best choices (§
                         with the windowed node-block build (~21 us serial) the fork / join gaps
                         of a replayed graph (~5-9 us each) and the alpha pass sharing CUs with the
                         output projection cost more than the overlap saved (PPI fwd 1.427 serial
-                        vs 1.435 ms, interleaved A/B, profiles/r08d)
+                        vs 1.435 ms, interleaved A/B, round 6 session 1; the run's files were
+                        lost with that session's container)
   lds_min_edges   2^18  edge_lds / side_stream only on graphs of at least this many edges
                         (edge_index' bound): below it a step is launch-bound, and the extra
                         launches and cross-queue joins cost more than they save (PATTERN G=8)

@@ -4,8 +4,8 @@
   (`gd.dataset_batch("PPI", 20, graph_seed=42)`: N = 44 900, E' = 1.27 M per layer, ONE global
   max over all 20 graphs, `models/gat_layer.py:85`), the reference PPI config
   (`run_config.py:18-33`: 4/4/6 heads, 256/256/121, identity skip on layer 1), xavier weights,
-  eval — through the same GATModel path the bench times (CSR built in the step, inference alpha
-  deferred to its read). Checked in full (every output element, every alpha) against the
+  eval — through the same GATModel path the bench times (CSR built in the step, alpha written by
+  every layer in the forward, as the reference does). Checked in full (every output element, every alpha) against the
   reference dataflow restated in torch at fp64 on the device (oracle/torch_dataflow.py: index,
   cat, mm through `a`, max, exp, scatter_add_), with the reference's own fp32 noise floor
   measured the same way (that dataflow in fp32).
@@ -58,7 +58,7 @@ def test_headline_ppi_batch_full_size(device):
     ei = torch.from_numpy(b.edge_index).to(device)
     gatx.clear_graph_cache()
     with torch.no_grad():
-        out = model(x, ei)                     # the bench's step: deferred alpha
+        out = model(x, ei)                     # the bench's step: alpha written eagerly
     alphas = [lay.normalised_attention_coeffs for lay in model.gat_layer_list]
     E2 = graph_cache.get(ei, b.num_nodes, True).num_edges
     assert E2 == 1270712 and all(tuple(a.shape) == (E2, lay.num_heads)

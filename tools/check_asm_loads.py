@@ -1,4 +1,5 @@
-"""Guard for the inline-asm record loads of csrc/edge_lds.hip: compiles the file to gfx950 ISA and
+"""Guard for the inline-asm record loads of csrc/edge_lds.hip (the concat walk edge_lds_kernel and,
+since round 6, the head-mean walk edge_lds_mean_kernel): compiles the file to gfx950 ISA and
 follows each kernel's control flow (loop back edges included) for an instruction that reads or
 writes a register an asm `global_load_dwordx2 ... s[..]` (scalar-base form, only the records use
 it) may still be loading (those loads return in issue order; `s_waitcnt vmcnt(N)` retires one once
@@ -19,7 +20,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 def kernels(asm: str):
     name, body = None, []
     for line in asm.split("\n"):
-        m = re.match(r"^(_Z\S*edge_lds_kernel\S*):", line)
+        m = re.match(r"^(_Z\S*edge_lds(?:_mean)?_kernel\S*):", line)
         if m:
             name, body = m.group(1), []
             continue
