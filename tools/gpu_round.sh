@@ -3,12 +3,16 @@
 # bench (with CPU baseline), the train / RMAT / PATTERN benches, rocprofv3 kernel traces of the
 # forward / train / RMAT / PATTERN-train benches and the windowed PMC passes for the forward and
 # RMAT. Every GPU step has its own time limit; the first failure ends the script.
-#   bash tools/gpu_round.sh TAG      (then: bash tools/snapshot_round.sh TAG)
+#   bash tools/gpu_round.sh TAG [PART]   (then: bash tools/snapshot_round.sh TAG)
+# PART: all (default) | bench (tests, benches, traces) | pmc (the counter passes): a whole refresh
+# can outlast one gpurun call's time limit, so it can run as two calls into the same TAG.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
+PART=${2:-all}
 OUT=$R/gpurun_out/$1
 mkdir -p "$OUT"
 exec 3>&1   # progress lines go to the call's stdout, never into a step's redirected output
 step() { echo "== $1" >&3; shift; "$@"; rc=$?; echo "rc=$rc" >&3; [ $rc -ne 0 ] && exit $rc; return 0; }
+if [ "$PART" != pmc ]; then
 step tests timeout -k 10 900 python -m pytest "$R/tests" -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread \
   --junitxml="$OUT/gpu_tests.xml" > "$OUT/gpu_tests.log" 2>&1
 tail -2 "$OUT/gpu_tests.log"
@@ -22,6 +26,9 @@ step prof_fwd timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_f
 step prof_train timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_train" -o run --output-format csv -- python3 "$R/bench.py" --mode train --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/prof_train.log" 2>&1
 step prof_rmat timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_rmat" -o run --output-format csv -- python3 "$R/bench.py" --workload rmat --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/prof_rmat.log" 2>&1
 step prof_pattern timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_pattern" -o run --output-format csv -- python3 "$R/bench.py" --workload pattern --graphs 8 --mode train --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/prof_pattern.log" 2>&1
+fi
+[ "$PART" = bench ] && { echo "bench part done"; exit 0; }
+cd /tmp && export TMPDIR=/tmp
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "GRBM_GUI_ACTIVE SQ_WAVES"; do
   i=$((i+1))
