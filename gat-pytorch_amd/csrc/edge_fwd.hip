@@ -45,16 +45,18 @@ __global__ void __launch_bounds__(256) attention_max_kernel(const int32_t* __res
     part[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
 }
 
-// The same with the head count known: each thread takes 4 edges per round with every index and
+// The same with the head count known: each thread takes 2 edges per round with every index and
 // score load of the round issued before any max (the plain loop keeps one edge's dependent
-// col -> S chain in flight per thread), score rows as float4 / float2 loads.
+// col -> S chain in flight per thread), score rows as float4 / float2 loads. (Round 6: 2 edges
+// per round ran 0.5-0.8 us faster per PPI launch than 4, and 8 was 2-6 us slower: the pass is
+// bound by the L2 request rate, and fewer registers keep more waves resident.)
 template <int NHC>
 __global__ void __launch_bounds__(256) attention_max_vec_kernel(const int32_t* __restrict__ col,
                                                                 const int32_t* __restrict__ rowidx,
                                                                 int64_t E2b, const long long* e2p,
                                                                 const float* __restrict__ S,
                                                                 float* __restrict__ part) {
-  constexpr int S2 = 2 * NHC, UE = 4;
+  constexpr int S2 = 2 * NHC, UE = 2;
   const int64_t E2 = e2p ? min(E2b, (int64_t)*e2p) : E2b;
   constexpr int VEC = (NHC % 4 == 0) ? 4 : ((NHC % 2 == 0) ? 2 : 1);
   float m = -INFINITY;
@@ -487,7 +489,9 @@ __global__ void __launch_bounds__(256) edge_forward_kernel(EdgeFwdArgs g) {
 template <int LPE, int HSC>
 __global__ void __launch_bounds__(256) edge_forward_shared_kernel(EdgeFwdArgs g) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  constexpr int EPW = 64 / LPE, U = 4;
+  // U: row loads in flight per lane (round 6: 2 ran ~2 us faster per PPI launch than 4, and 8 was
+  // ~9 us slower; same summation order, so the same bits)
+  constexpr int EPW = 64 / LPE, U = 2;
   constexpr int HSP = HSC <= 4 ? 4 : 8;   // weights per edge row in LDS (float4 granules)
   const int lane = threadIdx.x & 63;
   const int wave = uni(threadIdx.x >> 6);

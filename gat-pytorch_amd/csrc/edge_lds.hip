@@ -73,8 +73,8 @@ __device__ inline void load_ssrc(const float* __restrict__ S, int64_t src, float
 }
 
 // one wave per destination; lane j <-> CSR slot beg + j of each 64-edge batch. A segment of at
-// most 64 edges (nearly every PPI node) keeps its sources and logits in registers between the
-// denominator and the record sweeps.
+// most 64 edges (nearly every PPI node) keeps its sources, logits and exponentials in registers
+// between the denominator and the record sweeps (the second sweep divides the first's exp).
 template <int NHC>
 __global__ void __launch_bounds__(256) edge_records_kernel(RecArgs g) {
   const int lane = threadIdx.x & 63;
@@ -93,7 +93,7 @@ __global__ void __launch_bounds__(256) edge_records_kernel(RecArgs g) {
   // sweep 1: denominators (per-lane partials over the batches, then the butterfly, exactly as
   // edge_forward_kernel sums them)
   int src0 = 0;
-  float raw0[NHC];
+  float raw0[NHC], ex0[NHC];
   for (int base = beg; base < end; base += 64) {
     const int e = base + lane;
     if (e < end) {
@@ -103,8 +103,10 @@ __global__ void __launch_bounds__(256) edge_records_kernel(RecArgs g) {
 #pragma unroll
       for (int h = 0; h < NHC; ++h) {
         const float raw = g.const_att ? 0.f : ss[h] + sdst[h];
-        dn[h] += g.const_att ? 1.f : att_exp(raw, M);
+        const float ex = g.const_att ? 1.f : att_exp(raw, M);
+        dn[h] += ex;
         raw0[h] = raw;
+        ex0[h] = ex;
       }
       src0 = src;
     }
@@ -130,22 +132,25 @@ __global__ void __launch_bounds__(256) edge_records_kernel(RecArgs g) {
     const int e = base + lane;
     if (e >= end) continue;
     int src = src0;
-    float raw[NHC];
+    float raw[NHC], exv[NHC];
     if (one) {
 #pragma unroll
-      for (int h = 0; h < NHC; ++h) raw[h] = raw0[h];
+      for (int h = 0; h < NHC; ++h) { raw[h] = raw0[h]; exv[h] = ex0[h]; }
     } else {
       src = g.col[e];
       float ss[NHC];
       if (!g.const_att) load_ssrc<NHC>(g.S, src, ss);
 #pragma unroll
-      for (int h = 0; h < NHC; ++h) raw[h] = g.const_att ? 0.f : ss[h] + sdst[h];
+      for (int h = 0; h < NHC; ++h) {
+        raw[h] = g.const_att ? 0.f : ss[h] + sdst[h];
+        exv[h] = g.const_att ? 1.f : att_exp(raw[h], M);
+      }
     }
     const int64_t p = g.perm[e];
     float a[NHC];
 #pragma unroll
     for (int h = 0; h < NHC; ++h) {
-      a[h] = (g.const_att ? 1.f : att_exp(raw[h], M)) / (dn[h] + kSoftmaxEps);
+      a[h] = exv[h] / (dn[h] + kSoftmaxEps);
       if (!g.const_att && raw[h] == M && g.argmax) {   // rare: every tied argmax (slot, head)
         unsigned long long k = atomicAdd((unsigned long long*)g.argmax, 1ull);
         if (k < GATX_ARGMAX_CAP) g.argmax[1 + k] = (long long)e * NH + h;
