@@ -639,7 +639,10 @@ __global__ void __launch_bounds__(256) edge_bwd_src_hub_combine_kernel(BwdArgs g
 template <int LPE, int CPL>
 __global__ void __launch_bounds__(256) edge_bwd_src_mean_kernel(BwdArgs g) {
   constexpr int EPW = 64 / LPE, NHM = 8;
-  constexpr int U = CPL <= 1 ? 8 : (CPL <= 2 ? 4 : 2);
+  // rows in flight per lane (round 6: 2 instead of 8 at CPL 1, PPI L2: 166 -> 151-154 us, windowed
+  // train traces on one box; the gathers are L2-request-bound and fewer registers keep more
+  // waves resident; the same summation order, so the same bits)
+  constexpr int U = CPL <= 1 ? 2 : (CPL <= 2 ? 4 : 2);
   const int lane = threadIdx.x & 63;
   const int wave = uni(threadIdx.x >> 6);
   const int grp = lane / LPE, li = lane % LPE;
