@@ -50,10 +50,10 @@ struct RecArgs {
   long long* argmax;         // tie records (nullable)
 };
 
-// s_src[src, 0..NHC) of S's row as one vector load when the row allows it
+// NHC consecutive floats at p (a per-node row of NHC or 2 NHC floats, or its second half) as
+// vector loads when the row allows it
 template <int NHC>
-__device__ inline void load_ssrc(const float* __restrict__ S, int64_t src, float (&v)[NHC]) {
-  const float* p = S + src * (2 * NHC);
+__device__ inline void load_nh(const float* __restrict__ p, float (&v)[NHC]) {
   if constexpr (NHC % 4 == 0) {
 #pragma unroll
     for (int h = 0; h < NHC; h += 4) {
@@ -70,6 +70,11 @@ __device__ inline void load_ssrc(const float* __restrict__ S, int64_t src, float
 #pragma unroll
     for (int h = 0; h < NHC; ++h) v[h] = p[h];
   }
+}
+// s_src[src, 0..NHC) of S's row
+template <int NHC>
+__device__ inline void load_ssrc(const float* __restrict__ S, int64_t src, float (&v)[NHC]) {
+  load_nh<NHC>(S + src * (2 * NHC), v);
 }
 
 // one wave per destination; lane j <-> CSR slot beg + j of each 64-edge batch. A segment of at
@@ -172,6 +177,77 @@ __global__ void __launch_bounds__(256) edge_records_kernel(RecArgs g) {
         for (int h = 0; h < NHC; ++h) o[h] = a[h];
       }
     }
+  }
+}
+
+// ---- backward (round 6): the source pass of a concat layer as the same LDS walk.
+// g_Wh[s, h, :] = sum over s's out-edges (s -> d) of alpha~[e, h] go[d, h, :] (autograd of
+// models/gat_layer.py:117-127) is the forward aggregation on the transposed CSR with go's rows in
+// place of Wh's: edge_records_src writes its records — per (head, transposed slot j) {64 d,
+// alpha~} with d = scol[j], alpha~ recomputed from S / den exactly as edge_bwd_src_kernel does —
+// plus that pass's other output, g_s_src[s, h] = sum of g_raw over s's out-edges (the same
+// per-lane partials and butterfly, so the same bits), into G_aug[s, Dp + h]; then
+// gatx_edge_lds_forward walks go with them into G_aug[s, 0 : Dp).
+struct SrcRecArgs {
+  const float* S;            // [N][2NH]
+  const uint32_t* M_ord;
+  const float* den;          // [N][NH]
+  const int32_t* srowptr;    // transposed CSR (by source)
+  const int32_t* scol;       // transposed slot -> destination
+  const int32_t* seid;       // transposed slot -> CSR slot
+  const int32_t* perm;       // CSR slot -> edge_index' position (dropout mask)
+  int64_t N, E_bound;
+  int NH, const_att;
+  float p_drop;
+  const uint64_t* seed;
+  const float* g_raw;        // [NH][E_bound] per CSR slot (nullable)
+  float* G_aug;
+  int64_t ldg, Dp;
+  int2* rec;                 // [NH][E_bound] per transposed slot
+};
+
+template <int NHC>
+__global__ void __launch_bounds__(256) edge_records_src_kernel(SrcRecArgs g) {
+  const int lane = threadIdx.x & 63;
+  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (s >= g.N) return;
+  const int NH = NHC, S2 = 2 * NHC;
+  const int beg = uni(g.srowptr[s]), end = uni(g.srowptr[s + 1]);
+  const float M = g.const_att ? 0.f : ord_to_float(*g.M_ord);
+  const bool drop = g.p_drop > 0.f;
+  const float drop_scale = drop ? 1.f / (1.f - g.p_drop) : 1.f;
+  const uint64_t seed = drop ? *g.seed : 0ull;
+  float ssrc[NHC], gs[NHC];
+#pragma unroll
+  for (int h = 0; h < NHC; ++h) {
+    ssrc[h] = g.const_att ? 0.f : g.S[s * S2 + h];
+    gs[h] = 0.f;
+  }
+  for (int base = beg; base < end; base += 64) {
+    const int j = base + lane;
+    if (j >= end) continue;
+    const int d = g.scol[j];
+    const int e = g.seid[j];
+    const int64_t ep = drop ? (int64_t)g.perm[e] : 0;
+    float sd[NHC], dn[NHC], gr[NHC];
+    if (!g.const_att) load_nh<NHC>(g.S + (int64_t)d * S2 + NH, sd);   // s_dst[d] row
+    load_nh<NHC>(g.den + (int64_t)d * NH, dn);
+#pragma unroll
+    for (int h = 0; h < NHC; ++h) gr[h] = g.g_raw ? g.g_raw[(int64_t)h * g.E_bound + e] : 0.f;
+#pragma unroll
+    for (int h = 0; h < NHC; ++h) {
+      const float ex = g.const_att ? 1.f : att_exp(ssrc[h] + sd[h], M);
+      float w = ex / (dn[h] + kSoftmaxEps);
+      if (drop) w = dropout_keep(seed, ep * NH + h, g.p_drop) ? w * drop_scale : 0.f;
+      if (g.g_raw) gs[h] += gr[h];
+      g.rec[(int64_t)h * g.E_bound + j] = make_int2(d * (4 * kChunk), __float_as_int(w));
+    }
+  }
+  if (g.const_att) return;
+#pragma unroll
+  for (int h = 0; h < NHC; ++h) {
+    const float t = group_sum<64>(gs[h]);
+    if (lane == 0) g.G_aug[s * g.ldg + g.Dp + h] = t + 0.f;   // (as the src pass: + no g_corr)
   }
 }
 
@@ -729,6 +805,37 @@ extern "C" int gatx_edge_records(const float* S, const uint32_t* M_ord, const in
     default: edge_records_kernel<8><<<grid, 256, 0, st>>>(g); break;
   }
   GATX_LAUNCH_CHECK("edge_records");
+  return 0;
+}
+
+extern "C" int gatx_edge_records_src(const float* S, const uint32_t* M_ord, const float* den,
+                                     const int32_t* srowptr, const int32_t* scol,
+                                     const int32_t* seid, const int32_t* perm, int64_t N,
+                                     int64_t E_bound, int NH, int const_att, float dropout_p,
+                                     const uint64_t* seed, const float* g_raw, float* G_aug,
+                                     int64_t ldg, int64_t Dp, void* rec, gatx_stream_t s) {
+  GATX_REQUIRE(N >= 0 && E_bound >= 0 && NH >= 1 && NH <= 8 && N < (1ll << 25),
+               "edge_records_src: bad arguments");
+  GATX_REQUIRE(dropout_p == 0.f || seed != nullptr, "edge_records_src: dropout needs its seed");
+  if (N == 0) return 0;
+  SrcRecArgs g;
+  g.S = S; g.M_ord = M_ord; g.den = den; g.srowptr = srowptr; g.scol = scol; g.seid = seid;
+  g.perm = perm; g.N = N; g.E_bound = E_bound; g.NH = NH; g.const_att = const_att;
+  g.p_drop = dropout_p; g.seed = seed; g.g_raw = const_att ? nullptr : g_raw; g.G_aug = G_aug;
+  g.ldg = ldg; g.Dp = Dp; g.rec = (int2*)rec;
+  const unsigned grid = (unsigned)ceil_div(N, (int64_t)4);
+  hipStream_t st = (hipStream_t)s;
+  switch (NH) {
+    case 1: edge_records_src_kernel<1><<<grid, 256, 0, st>>>(g); break;
+    case 2: edge_records_src_kernel<2><<<grid, 256, 0, st>>>(g); break;
+    case 3: edge_records_src_kernel<3><<<grid, 256, 0, st>>>(g); break;
+    case 4: edge_records_src_kernel<4><<<grid, 256, 0, st>>>(g); break;
+    case 5: edge_records_src_kernel<5><<<grid, 256, 0, st>>>(g); break;
+    case 6: edge_records_src_kernel<6><<<grid, 256, 0, st>>>(g); break;
+    case 7: edge_records_src_kernel<7><<<grid, 256, 0, st>>>(g); break;
+    default: edge_records_src_kernel<8><<<grid, 256, 0, st>>>(g); break;
+  }
+  GATX_LAUNCH_CHECK("edge_records_src");
   return 0;
 }
 

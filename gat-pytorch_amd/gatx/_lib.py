@@ -65,6 +65,8 @@ SIGNATURES = {
     "gatx_graph_segments": (c_i, [P, P, c_i64, c_i, P, P, P, c_sz, P]),
     "gatx_graph_segments_max": (c_i, []),
     "gatx_edge_lds_rows": (c_i, []),
+    "gatx_edge_records_src": (c_i, [P, P, P, P, P, P, P, c_i64, c_i64, c_i, c_i, c_f, P, P, P, c_i64,
+                                    c_i64, P, P]),
     "gatx_edge_records": (c_i, [P, P, P, P, P, c_i64, c_i64, c_i, c_i, c_f, P, P, P, P, P, P]),
     "gatx_edge_lds_forward": (c_i, [P, c_i64, P, c_i64, P, c_i64, P, P, c_i64, c_i, c_i, P, P, c_i64,
                                     P, c_i64, c_i, c_f, P, P]),

@@ -682,12 +682,28 @@ def layer_backward(g_out, g_alpha, x, W, a, bias, graph: Graph, sh: LayerShape, 
                  ptr(g_alpha.contiguous()) if g_alpha is not None else None, ptr(g_raw),
                  ptr(gsd), ptr(G_aug), ldg, sh.Dp, *bwd_hub_args(graph, sh.NH, sh.F, dev, False),
                  s)
-    with _span("bwd_edge_src", binfo):
-        call("gatx_edge_backward_src_hubs", ptr(saved["S"]), ptr(saved["M_ord"]),
-             ptr(saved["den"]), ptr(graph.srowptr), ptr(graph.scol), ptr(graph.seid),
-             ptr(graph.perm), N, E2, sh.NH, sh.F, int(sh.concat), int(sh.const), float(p),
-             ptr(seed), ptr(go), ptr(g_raw), None, ptr(G_aug), ldg,
-             *bwd_hub_args(graph, sh.NH, sh.F, dev, True), s)
+    src_blocks = (lds_blocks(graph, sh) if sh.concat and sh.F % 4 == 0
+                  and tuning.get("edge_lds_bwd") else None)
+    if src_blocks is not None:
+        # the source pass as the forward's LDS walk over the transposed CSR, go's rows staged
+        # (csrc/edge_lds.hip: gatx_edge_records_src, then gatx_edge_lds_forward into G_aug)
+        segs, count, nblocks = src_blocks
+        trec = torch.empty((sh.NH, max(E2, 1)), dtype=torch.int64, device=dev)
+        with _span("bwd_edge_src", binfo + ("lds",)):
+            call("gatx_edge_records_src", ptr(saved["S"]), ptr(saved["M_ord"]),
+                 ptr(saved["den"]), ptr(graph.srowptr), ptr(graph.scol), ptr(graph.seid),
+                 ptr(graph.perm), N, E2, sh.NH, int(sh.const), float(p), ptr(seed),
+                 ptr(g_raw) if g_raw is not None else None, ptr(G_aug), ldg, sh.Dp, ptr(trec), s)
+            call("gatx_edge_lds_forward", ptr(go), sh.Dp, ptr(graph.srowptr), N, ptr(trec), E2,
+                 ptr(segs), ptr(count), nblocks, sh.NH, sh.F, None, ptr(G_aug), ldg, None, 0, 0,
+                 0.0, None, s)
+    else:
+        with _span("bwd_edge_src", binfo):
+            call("gatx_edge_backward_src_hubs", ptr(saved["S"]), ptr(saved["M_ord"]),
+                 ptr(saved["den"]), ptr(graph.srowptr), ptr(graph.scol), ptr(graph.seid),
+                 ptr(graph.perm), N, E2, sh.NH, sh.F, int(sh.concat), int(sh.const), float(p),
+                 ptr(seed), ptr(go), ptr(g_raw), None, ptr(G_aug), ldg,
+                 *bwd_hub_args(graph, sh.NH, sh.F, dev, True), s)
     if not sh.const:   # max()'s share, added into both logit-gradient columns of G_aug
         mws = torch.empty(lib.gatx_max_backward_workspace_bytes(), dtype=torch.uint8, device=dev)
         with _span("bwd_max", binfo):

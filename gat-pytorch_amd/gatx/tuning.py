@@ -21,6 +21,9 @@ threshold of one); the defaults are the measured-best choices (§
                         LDS-staged edge pass (csrc/edge_lds.hip) instead of the L2-gather one
   edge_lds_mean   1     head-mean layers take it too (gatx_edge_lds_mean_forward: every head
                         staged in turn, the mean kept in registers), round 6
+  edge_lds_bwd    1     the backward's source pass of a concat layer (F % 4 == 0) on such graphs:
+                        transposed records (gatx_edge_records_src) + the same LDS walk over go's
+                        rows (0: the L2-gather source pass), round 6
   side_stream     0     short independent launches (node blocks, GATModel's non-final alpha
                         passes) on a second stream, under the projection GEMM. Off since round 6:
                         with the windowed node-block build (~21 us serial) the fork / join gaps
@@ -55,6 +58,7 @@ DEFAULTS = {
     "skip_fold": 1,
     "edge_lds": 1,
     "edge_lds_mean": 1,
+    "edge_lds_bwd": 1,
     "side_stream": 0,
     "lds_min_edges": 1 << 18,
 }

@@ -436,6 +436,21 @@ int gatx_edge_lds_forward(const float* rows, int64_t row_stride, const int32_t* 
                           int out_features, const float* bias, float* out, int64_t out_ld,
                           const float* resid, int64_t resid_ld, int elu, float out_p,
                           const uint64_t* out_seed, gatx_stream_t stream);
+/* gatx_edge_records_src (round 6) — the records of the backward's source pass on the LDS walk
+ *   (the autograd of models/gat_layer.py:117-127 w.r.t. Wh is the forward aggregation on the
+ *   transposed CSR with go's rows): one wave per source s, per (head, transposed slot j) the
+ *   record {64 * scol[j], alpha~} in rec ([NH][E_bound] x 8 B; alpha~ recomputed from S, den,
+ *   M_ord and the dropout mask exactly as gatx_edge_backward_src does), and g_s_src[s, h] = the
+ *   sum of g_raw ([NH][E_bound], per CSR slot; nullable) over s's out-edges into
+ *   G_aug[s * ldg + Dp + h] (skipped with const_attention). Then gatx_edge_lds_forward(rows = go
+ *   with row stride NH * F, rowptr = srowptr, rec, ..., out = G_aug, out_ld = ldg, no bias / resid /
+ *   ELU / dropout) writes G_aug[s, 0 : NH * F) — concat layers with F % 4 == 0, N < 2^25. */
+int gatx_edge_records_src(const float* S, const uint32_t* M_ord, const float* den,
+                          const int32_t* srowptr, const int32_t* scol, const int32_t* seid,
+                          const int32_t* perm, int64_t num_nodes, int64_t E_bound, int num_heads,
+                          int const_attention, float dropout_p, const uint64_t* seed,
+                          const float* g_raw, float* G_aug, int64_t ldg, int64_t Dp, void* rec,
+                          gatx_stream_t stream);
 /* gatx_edge_lds_mean_forward (round 6) — head-mean layers (concat = False, models/gat_layer.py
  *   :128-135: out = mean over heads, then bias): one workgroup per (node block, 16-float chunk,
  *   destination range of <= 768 nodes) stages every head's chunk in turn and adds each head's

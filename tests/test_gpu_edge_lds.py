@@ -341,3 +341,38 @@ def test_side_alpha_pass_keeps_its_buffers(device, monkeypatch):
     assert torch.equal(o0, o1)
     for u, v in zip(a0, a1):
         assert torch.equal(u, v)
+
+
+@pytest.mark.parametrize("dropout", [0.0, 0.3])
+def test_lds_backward_source_pass_equals_gather(dropout, device, lds_on):
+    """tuning edge_lds_bwd (round 6): the backward's source pass of the concat layers as the LDS
+    walk over go's rows with transposed records (gatx_edge_records_src) equals the L2-gather
+    source pass — every parameter gradient and the input gradient, to fp32 summation order (the
+    walk adds each destination's terms in another fixed order); g_s_src is bitwise the same. With
+    dropout the records carry the attention dropout mask."""
+    import gatx
+    from gatx import data as gd
+    from gatx import tuning
+    torch.manual_seed(0)
+    model = gatx.GATModel(num_classes=16, num_input_node_features=48, num_layers=3,
+                          num_heads_per_layer=[4, 4, 6], heads_concat_per_layer=[True, True, False],
+                          head_output_features_per_layer=[48, 64, 64, 16],
+                          add_skip_connection=[False, True, False], dropout=dropout).to(device)
+    model.train()
+    b = gd.uniform_graph_batch(3, 1500, 30000, 48, feature_seed=2)
+    x0 = torch.from_numpy(b.x).to(device)
+    ei = torch.from_numpy(b.edge_index).to(device)
+    g_out = torch.randn(b.num_nodes, 16, device=device, generator=torch.Generator(device=device).manual_seed(5))
+    grads = []
+    for on in (0, 1):
+        tuning.set(edge_lds_bwd=on)
+        gatx.clear_graph_cache()
+        model.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        torch.manual_seed(7)   # the same dropout seeds in both runs
+        out = model(x, ei)
+        out.backward(g_out)
+        grads.append([x.grad.clone()] + [p.grad.clone() for p in model.parameters()])
+    for a, c in zip(*grads):
+        scale = max(1.0, c.abs().max().item())
+        assert (a - c).abs().max().item() <= 2e-5 * scale
