@@ -79,6 +79,66 @@ __global__ void __launch_bounds__(256) attn_norm_backward_kernel(
   }
 }
 
+// All layers in one pass (round 6): the layers share edge_index' and rowptr, so one read of dst and
+// of the degrees serves them all. Per layer the same per-thread partials, grid and block tree as
+// attn_norm_partial_kernel, so every layer's sum is bitwise the per-layer launch's.
+constexpr int kNormMaxLayers = 8;
+struct NormLayers {
+  const float* alpha[kNormMaxLayers];
+  int nh[kNormMaxLayers];
+};
+
+template <typename I>
+__global__ void __launch_bounds__(256) attn_norm_multi_partial_kernel(
+    NormLayers L, int nl, int64_t E2, const I* __restrict__ dst,
+    const int32_t* __restrict__ rowptr, float* __restrict__ part) {
+  float s[kNormMaxLayers];
+#pragma unroll
+  for (int l = 0; l < kNormMaxLayers; ++l) s[l] = 0.f;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E2;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const float deg = deg_of(rowptr, (int32_t)dst[e]);
+#pragma unroll
+    for (int l = 0; l < kNormMaxLayers; ++l) {
+      if (l >= nl) break;
+      const float* a = L.alpha[l] + e * L.nh[l];
+      for (int h = 0; h < L.nh[l]; ++h) s[l] += fabsf(excess(a[h], deg));
+    }
+  }
+  __shared__ float red[kNormMaxLayers][4];
+#pragma unroll
+  for (int l = 0; l < kNormMaxLayers; ++l) {
+    if (l >= nl) break;
+    const float t = group_sum<64>(s[l]);
+    if ((threadIdx.x & 63) == 0) red[l][threadIdx.x >> 6] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x < nl)
+    part[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] =
+        (red[threadIdx.x][0] + red[threadIdx.x][1]) + (red[threadIdx.x][2] + red[threadIdx.x][3]);
+}
+
+// the layers' finals in layer order: out = v_0, then out + v_1, ... (as the per-layer launches
+// with accumulate)
+__global__ void __launch_bounds__(256) attn_norm_multi_final_kernel(const float* __restrict__ part,
+                                                                    int nb, int nl, float scale,
+                                                                    float* __restrict__ out) {
+#pragma clang fp contract(off)   // v = sum * scale rounded, then acc + v: the per-layer finals' ops
+  __shared__ float red[4];
+  float acc = 0.f;
+  for (int l = 0; l < nl; ++l) {
+    float s = 0.f;
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) s += part[(int64_t)l * nb + b];
+    s = group_sum<64>(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    const float v = ((red[0] + red[1]) + (red[2] + red[3])) * scale;
+    acc = l == 0 ? v : acc + v;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = acc;
+}
+
 inline unsigned grid_for(int64_t n, int64_t cap) {
   const int64_t g = ceil_div(n > 0 ? n : 1, 256);
   return (unsigned)(g < cap ? g : cap);
@@ -110,6 +170,37 @@ extern "C" int gatx_attention_norm(const float* alpha, int64_t E2, int NH, const
   GATX_LAUNCH_CHECK("attention_norm");
   attn_norm_final_kernel<<<1, 256, 0, st>>>(part, (int)nb, scale, accumulate, out);
   GATX_LAUNCH_CHECK("attention_norm_final");
+  return 0;
+}
+
+extern "C" size_t gatx_attention_norm_multi_workspace_bytes(int num_layers) {
+  return sizeof(float) * kNormBlocks * (size_t)(num_layers > 0 ? num_layers : 1);
+}
+
+extern "C" int gatx_attention_norm_multi(const float* const* alphas, const int* num_heads,
+                                         int num_layers, int64_t E2, const void* dst,
+                                         int dst_is64, const int32_t* rowptr, float scale,
+                                         float* out, void* workspace, gatx_stream_t s) {
+  GATX_REQUIRE(E2 >= 0 && num_layers >= 1 && num_layers <= kNormMaxLayers,
+               "attention_norm_multi: bad sizes");
+  NormLayers L{};
+  for (int l = 0; l < num_layers; ++l) {
+    GATX_REQUIRE(alphas[l] != nullptr && num_heads[l] >= 1, "attention_norm_multi: bad layer");
+    L.alpha[l] = alphas[l];
+    L.nh[l] = num_heads[l];
+  }
+  hipStream_t st = (hipStream_t)s;
+  const unsigned nb = grid_for(E2, kNormBlocks);
+  float* part = (float*)workspace;
+  if (dst_is64)
+    attn_norm_multi_partial_kernel<int64_t><<<nb, 256, 0, st>>>(L, num_layers, E2,
+                                                                (const int64_t*)dst, rowptr, part);
+  else
+    attn_norm_multi_partial_kernel<int32_t><<<nb, 256, 0, st>>>(L, num_layers, E2,
+                                                                (const int32_t*)dst, rowptr, part);
+  GATX_LAUNCH_CHECK("attention_norm_multi");
+  attn_norm_multi_final_kernel<<<1, 256, 0, st>>>(part, (int)nb, num_layers, scale, out);
+  GATX_LAUNCH_CHECK("attention_norm_multi_final");
   return 0;
 }
 

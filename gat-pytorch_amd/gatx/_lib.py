@@ -137,6 +137,8 @@ SIGNATURES = {
     "gatx_attention_norm_workspace_bytes": (c_sz, []),
     "gatx_attention_norm": (c_i, [P, c_i64, c_i, P, c_i, P, c_f, c_i, P, P, P]),
     "gatx_attention_norm_backward": (c_i, [P, c_i64, c_i, P, c_i, P, P, c_f, P, P]),
+    "gatx_attention_norm_multi_workspace_bytes": (c_sz, [c_i]),
+    "gatx_attention_norm_multi": (c_i, [P, P, c_i, c_i64, P, c_i, P, c_f, P, P, P]),
 }
 
 

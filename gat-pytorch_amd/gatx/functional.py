@@ -8,6 +8,7 @@ SURVEY.md §8(a) a14 and oracle/gat_oracle.py:gat_layer_backward.
 """
 from __future__ import annotations
 
+import ctypes
 from contextlib import contextmanager
 
 import torch
@@ -1145,9 +1146,19 @@ class AttentionNormFunction(torch.autograd.Function):
             if a.dim() != 2 or a.size(0) != E2:
                 raise RuntimeError(f"attention {i} has shape {tuple(a.shape)}, edge_index has "
                                    f"{E2} edges")
-            with _span("attn_norm", (graph.num_nodes, E2, a.size(1))):
-                call("gatx_attention_norm", ptr(a), E2, a.size(1), *_dst_row(graph),
-                     ptr(graph.rowptr), scale, int(i > 0), ptr(out), ptr(ws), s)
+        if L <= 8:   # one pass over edge_index' for all layers (same bits as one per layer)
+            ptrs = (ctypes.c_void_p * L)(*[ptr(a) for a in alphas])
+            nhs = (ctypes.c_int * L)(*[a.size(1) for a in alphas])
+            wsm = torch.empty(lib.gatx_attention_norm_multi_workspace_bytes(L), dtype=torch.uint8,
+                              device=dev)
+            with _span("attn_norm", (graph.num_nodes, E2, sum(a.size(1) for a in alphas))):
+                call("gatx_attention_norm_multi", ctypes.addressof(ptrs), ctypes.addressof(nhs), L,
+                     E2, *_dst_row(graph), ptr(graph.rowptr), scale, ptr(out), ptr(wsm), s)
+        else:
+            for i, a in enumerate(alphas):
+                with _span("attn_norm", (graph.num_nodes, E2, a.size(1))):
+                    call("gatx_attention_norm", ptr(a), E2, a.size(1), *_dst_row(graph),
+                         ptr(graph.rowptr), scale, int(i > 0), ptr(out), ptr(ws), s)
         ctx.graph, ctx.scale = graph, scale
         ctx.save_for_backward(*alphas)
         return out.view(())

@@ -583,6 +583,14 @@ size_t gatx_attention_norm_workspace_bytes(void);
 int gatx_attention_norm(const float* alpha, int64_t E2, int NH, const void* dst, int dst_is64,
                         const int32_t* rowptr, float scale, int accumulate, float* out,
                         void* workspace, gatx_stream_t stream);
+/* All layers in one pass (round 6): alphas[l] (E2 x num_heads[l], l < num_layers <= 8; a host
+ * array of device pointers, read at launch) -> out[0] = the per-layer sums in layer order, each
+ * times scale — bitwise what num_layers gatx_attention_norm calls (accumulate = l > 0) give.
+ * workspace: gatx_attention_norm_multi_workspace_bytes(num_layers). */
+size_t gatx_attention_norm_multi_workspace_bytes(int num_layers);
+int gatx_attention_norm_multi(const float* const* alphas, const int* num_heads, int num_layers,
+                              int64_t E2, const void* dst, int dst_is64, const int32_t* rowptr,
+                              float scale, float* out, void* workspace, gatx_stream_t stream);
 /* g_alpha[e,h] = g[0] * scale * sign(alpha[e,h] * deg - 1) * deg (g: device scalar). */
 int gatx_attention_norm_backward(const float* alpha, int64_t E2, int NH, const void* dst,
                                  int dst_is64, const int32_t* rowptr, const float* g,

@@ -42,3 +42,30 @@ def test_bce_module_and_shape_check(device):
     # only writes the input's gradient)
     with pytest.raises(RuntimeError, match="target"):
         loss(x, torch.ones(3, 4, device=device, requires_grad=True))
+
+
+@pytest.mark.parametrize("nhs", [(4, 4, 6), (1,), (8, 2, 3, 1, 4)])
+def test_attention_norm_one_pass_equals_per_layer(nhs, device):
+    """gatx_attention_norm_multi (round 6: every layer's alpha in one pass over edge_index') is
+    bitwise the per-layer gatx_attention_norm launches accumulated in layer order
+    (models/GATModel.py:189-234)."""
+    import gatx
+    from gatx import data as gd
+    from gatx._lib import call, lib, ptr, stream
+    from gatx.functional import _dst_row, attention_norm
+    from gatx.graph import graph_cache
+    b = gd.uniform_graph_batch(3, 700, 9000, 8, feature_seed=3)
+    ei = torch.from_numpy(b.edge_index).to(device)
+    gatx.clear_graph_cache()
+    g = graph_cache.get(ei, b.num_nodes, True)
+    E2 = g.num_edges
+    gen = torch.Generator(device=device).manual_seed(9)
+    alphas = [torch.rand(E2, nh, device=device, generator=gen) for nh in nhs]
+    one = attention_norm(g.edge_index, alphas)
+    out = torch.empty(1, dtype=torch.float32, device=device)
+    ws = torch.empty(lib.gatx_attention_norm_workspace_bytes(), dtype=torch.uint8, device=device)
+    scale = 1.0 / (E2 * len(alphas))
+    for i, a in enumerate(alphas):
+        call("gatx_attention_norm", ptr(a), E2, a.size(1), *_dst_row(g), ptr(g.rowptr), scale,
+             int(i > 0), ptr(out), ptr(ws), stream())
+    assert torch.equal(one.view(1), out)
