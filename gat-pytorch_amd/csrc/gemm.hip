@@ -660,6 +660,12 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
     g.bm = g.bn = 32; g.tail_partial = nullptr;
     return launch_gemm_smallk(g, batch, stream);
   }
+  if (gemm_mode() >= 1 && n_split >= N && !sc &&
+      gemm_smalln_fits(M, N, K, a_kc, b_kc, accumulate, bias || resid || elu)) {
+    g.splits = 1; g.tail_s = 1; g.tiles_m = g.tiles_n = 1; g.dp_blocks = g.tail_rem = 0;
+    g.bm = g.bn = 32; g.tail_partial = nullptr;
+    return launch_gemm_smalln(g, batch, stream);
+  }
   const Kind kd = choose_kind(M, N);
   g.tiles_m = ceil_div(M, kd.bm);
   g.tiles_n = ceil_div(N, kd.bn);

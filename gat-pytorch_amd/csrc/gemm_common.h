@@ -289,6 +289,10 @@ int launch_gemm_x3(const gk::GemmArgs& g, bool a_kc, bool b_kc, int batch, int t
 bool gemm_smallk_fits(int64_t M, int64_t N, int64_t K, bool a_kc, bool b_kc, int accumulate,
                       bool resid);
 int launch_gemm_smallk(const gk::GemmArgs& g, int batch, hipStream_t stream);
+// gemm_smallk.hip: 64 < K <= 256, N <= 64 products, B n-contiguous, no epilogue (x3 arithmetic)
+bool gemm_smalln_fits(int64_t M, int64_t N, int64_t K, bool a_kc, bool b_kc, int accumulate,
+                      bool epilogue);
+int launch_gemm_smalln(const gk::GemmArgs& g, int batch, hipStream_t stream);
 // gemm_f16p.hip: the f16x3 kernel with B given as pre-split fp16 planes (tags 0 and 1)
 int launch_gemm_f16p(const gk::GemmArgs& g, int tag, hipStream_t stream);
 int launch_gemm_f16rc(const gk::GemmArgs& g, hipStream_t stream);

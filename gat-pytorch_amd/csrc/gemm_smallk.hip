@@ -215,7 +215,179 @@ __global__ void __launch_bounds__(64 * SK_WAVES, 1) gemm_smallk_kernel(GemmArgs 
   }
 }
 
+// Small-N GEMM, the same arithmetic: C_b = A_b B_b for N <= 64 and K <= 256, A k-contiguous and
+// B stored n-contiguous (B(k, n) = B[k * ldb + n]), no epilogue — the reassociated first
+// layer's backward g_Z[n, h] = go[n, h] . W_h (functional._reassoc_backward; PPI layer 0: 4 heads
+// x (44900 x 256) . (256 x 52)). On the tiled x3 kernel that product ran 91 us for 221 MB of
+// traffic: a 128 x 128 tile over 52 columns wastes 59% of its MFMA work and stages A through LDS
+// for a single column tile. Here, as gemm_smallk_kernel, each workgroup keeps its entry's whole
+// B (256 k x 64 columns) as three bf16 planes in LDS (96 KB) and its 8 waves stream 32-row
+// blocks of A straight from HBM into MFMA fragments, 64 k per chunk, the next chunk's loads
+// issued before this chunk's MFMAs; A is read once and C written once.
+constexpr int SN_WAVES = 8, SN_KMAX = 256, SN_NMAX = 64;
+constexpr int SN_KSLOTS = SN_KMAX / 8;
+constexpr int SN_PLANE = SN_KSLOTS * SN_NMAX * 16;   // bytes per bf16 plane of B
+constexpr int SN_CHUNK = 4;                            // k16 steps per chunk of A
+
+// VEC: A rows 16-byte aligned and K % 8 == 0 (float4 loads of whole 8-k groups).
+// VST: C rows 16-byte aligned and N % 4 == 0 (float4 stores).
+template <bool VEC, bool VST>
+__global__ void __launch_bounds__(64 * SN_WAVES, 1) gemm_smalln_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char wl[3 * SN_PLANE];
+  const int b = blockIdx.y;
+  const float* __restrict__ A = g.A + b * g.a_bs;
+  const float* __restrict__ B = g.B + b * g.b_bs;
+  const int K = (int)g.K, N = (int)g.N;
+  const int64_t M = g.M;
+  const int ncb = (N + 31) / 32;
+
+  // B -> [plane][k / 8][n][8 k] (gemm_smallk_kernel's layout); consecutive threads take
+  // consecutive n, i.e. consecutive addresses of one row of B
+  for (int t = threadIdx.x; t < SN_KSLOTS * SN_NMAX; t += 64 * SN_WAVES) {
+    const int kc = t / SN_NMAX, n = t % SN_NMAX;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = kc * 8 + j;
+      v[j] = (n < N && k < K) ? B[(int64_t)k * g.ldb + n] : 0.f;
+    }
+    uint4 h, m, l;
+    sk_split8(v, h, m, l);
+    const int o = (kc * SN_NMAX + n) * 16;
+    *(uint4*)(wl + o) = h;
+    *(uint4*)(wl + SN_PLANE + o) = m;
+    *(uint4*)(wl + 2 * SN_PLANE + o) = l;
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5;
+  const int nks = (K + 15) / 16;
+  const int nch = (nks + SN_CHUNK - 1) / SN_CHUNK;
+  const int64_t nrb = (M + 31) / 32;
+  // one chunk of a row block's A: 8 consecutive k per lane and k16 step (one MFMA fragment);
+  // rows past M read row M - 1 (not stored)
+  auto fetch = [&](int64_t rb, int c, float (&r)[SN_CHUNK][8]) {
+    const int64_t row = rb * 32 + (lane & 31);
+    const float* ar = A + (row < M ? row : M - 1) * g.lda;
+#pragma unroll
+    for (int s = 0; s < SN_CHUNK; ++s) {
+      const int k0 = 16 * (SN_CHUNK * c + s) + 8 * half;
+      if (VEC) {   // (a group at or past K loads k = 0..7 and is zeroed at its split)
+        const float4 p = *(const float4*)(ar + (k0 < K ? k0 : 0));
+        const float4 q = *(const float4*)(ar + (k0 < K ? k0 + 4 : 4));
+        r[s][0] = p.x; r[s][1] = p.y; r[s][2] = p.z; r[s][3] = p.w;
+        r[s][4] = q.x; r[s][5] = q.y; r[s][6] = q.z; r[s][7] = q.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[s][j] = k0 + j < K ? ar[k0 + j] : 0.f;
+      }
+    }
+  };
+  // row blocks dealt wave-major (block x, then x + gridDim.x, ...): every workgroup gets a
+  // share when the blocks are fewer than the waves (PPI: 351 per head for 512 waves)
+  int64_t rb = (int64_t)wave * gridDim.x + blockIdx.x;
+  const int64_t rstep = (int64_t)gridDim.x * SN_WAVES;
+  float cur[SN_CHUNK][8], nxt[SN_CHUNK][8];
+  if (rb < nrb) fetch(rb, 0, cur);
+  for (; rb < nrb; rb += rstep) {
+    floatx16 acc[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+#pragma unroll
+    for (int c = 0; c < SN_KMAX / (16 * SN_CHUNK); ++c) {
+      if (c >= nch) break;
+      if (c + 1 < nch) fetch(rb, c + 1, nxt);
+      else if (rb + rstep < nrb) fetch(rb + rstep, 0, nxt);
+      bf16x8 fa[SN_CHUNK][3];
+#pragma unroll
+      for (int s = 0; s < SN_CHUNK; ++s) {
+        if (VEC && 16 * (SN_CHUNK * c + s) + 8 * half >= K) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) cur[s][j] = 0.f;
+        }
+        uint4 h, m, l;
+        sk_split8(cur[s], h, m, l);
+        fa[s][0] = __builtin_bit_cast(bf16x8, h);
+        fa[s][1] = __builtin_bit_cast(bf16x8, m);
+        fa[s][2] = __builtin_bit_cast(bf16x8, l);
+      }
+#pragma unroll
+      for (int s = 0; s < SN_CHUNK; ++s) {
+        const int ks = SN_CHUNK * c + s;
+        if (ks >= nks) break;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          if (i >= ncb) break;
+          bf16x8 fb[3];
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+            fb[p] = *(const bf16x8*)(wl + p * SN_PLANE +
+                                     ((2 * ks + half) * SN_NMAX + i * 32 + (lane & 31)) * 16);
+          // small terms first: (l,h) (h,l) (m,m) (m,h) (h,m) (h,h), as gemm_smallk_kernel
+          constexpr int PLA[6] = {2, 0, 1, 1, 0, 0};
+          constexpr int PLB[6] = {0, 2, 1, 0, 1, 0};
+#pragma unroll
+          for (int t = 0; t < 6; ++t)   // C^T = B^T A^T: lane = output row, registers = columns
+            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[PLB[t]], fa[s][PLA[t]], acc[i],
+                                                             0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < SN_CHUNK; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cur[s][j] = nxt[s][j];
+    }
+    // lane l: output row rb*32 + (l & 31); registers 4j..4j+3: columns i*32 + 8j + 4*(l >> 5) + 0..3
+    const int64_t row = rb * 32 + (lane & 31);
+    if (row < M) {
+      float* base = g.C0 + b * g.c0_bs + row * g.ldc0;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        if (i >= ncb) break;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int col = i * 32 + 8 * j + 4 * half;
+          if (VST) {
+            if (col < N)
+              *(float4*)(base + col) =
+                  make_float4(acc[i][4 * j], acc[i][4 * j + 1], acc[i][4 * j + 2], acc[i][4 * j + 3]);
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (col + r < N) base[col + r] = acc[i][4 * j + r];
+          }
+        }
+      }
+    }
+  }
+}
+
 }  // namespace
+
+bool gemm_smalln_fits(int64_t M, int64_t N, int64_t K, bool a_kc, bool b_kc, int accumulate,
+                      bool epilogue) {
+  return a_kc && !b_kc && !accumulate && !epilogue && K > SK_KMAX && K <= SN_KMAX && N >= 1 &&
+         N <= SN_NMAX && M >= 32 * SN_WAVES;
+}
+
+int launch_gemm_smalln(const gk::GemmArgs& g, int batch, hipStream_t stream) {
+  GATX_REQUIRE(g.K <= SN_KMAX && g.N <= SN_NMAX && batch < 65536, "gemm_smalln: shape");
+  const int64_t nrb = ceil_div(g.M, 32);
+  const int64_t per = std::max<int64_t>(1, 256 / batch);
+  const unsigned gx = (unsigned)std::min<int64_t>(per, nrb);
+  dim3 grid(gx, (unsigned)batch);
+  const bool vec = ((uintptr_t)g.A % 16 == 0) && g.lda % 4 == 0 && g.a_bs % 4 == 0 && g.K % 8 == 0;
+  const bool vst = ((uintptr_t)g.C0 % 16 == 0) && g.ldc0 % 4 == 0 && g.c0_bs % 4 == 0 &&
+                   g.N % 4 == 0;
+  if (vec && vst) gemm_smalln_kernel<true, true><<<grid, 64 * SN_WAVES, 0, stream>>>(g);
+  else if (vec) gemm_smalln_kernel<true, false><<<grid, 64 * SN_WAVES, 0, stream>>>(g);
+  else if (vst) gemm_smalln_kernel<false, true><<<grid, 64 * SN_WAVES, 0, stream>>>(g);
+  else gemm_smalln_kernel<false, false><<<grid, 64 * SN_WAVES, 0, stream>>>(g);
+  GATX_LAUNCH_CHECK("gemm_smalln");
+  return 0;
+}
 
 bool gemm_smallk_fits(int64_t M, int64_t N, int64_t K, bool a_kc, bool b_kc, int accumulate,
                       bool resid) {

@@ -276,6 +276,45 @@ def test_gemm_smallk(device):
 
 
 @pytest.mark.gpu
+def test_gemm_smalln(device):
+    """The small-N path (64 < K <= 256, N <= 64, B n-contiguous: csrc/gemm_smallk.hip
+    gemm_smalln_kernel, the reassociated first layer's g_Z = go_h W_h) against float64 and beside
+    the f32 kernel: batched with strided heads as functional._reassoc_backward calls it, ragged
+    M / N / K, K % 8 != 0 and unaligned rows (scalar loads / stores); error relative to
+    sum|a||b| at the fp32 GEMM's level; bitwise repeatable; columns past N untouched."""
+    from gatx._lib import call, lib, ptr, stream
+    torch.manual_seed(6)
+    # (M, heads, N, K, A's per-head stride, B's row stride)
+    cases = [(44900 // 4, 4, 52, 256, 256, 52), (1000, 1, 33, 100, 101, 35), (777, 3, 64, 256, 256, 64),
+             (300, 2, 8, 72, 72, 8), (2049, 2, 17, 129, 130, 17), (513, 1, 4, 65, 68, 4)]
+    try:
+        for (M, NB, N, K, fa, ldb) in cases:
+            A = torch.randn(M, NB * fa, device=device) * torch.rand(M, 1, device=device) * 10
+            B = torch.randn(NB * K, ldb, device=device)
+            Av = A.view(M, NB, fa)[:, :, :K].double()
+            Bv = B.view(NB, K, ldb)[:, :, :N].double()
+            ref = torch.einsum("mbk,bkn->mbn", Av, Bv)
+            S = torch.einsum("mbk,bkn->mbn", Av.abs(), Bv.abs())
+            outs = []
+            for mode in (2, 2, 0):
+                lib.gatx_set_gemm_mode(mode)
+                # output heads N + 3 apart: the gap columns must stay NaN
+                C = torch.full((M, NB, N + 3), float("nan"), device=device)
+                call("gatx_gemm_f32_batched", NB, M, N, K, ptr(A), NB * fa, 1, fa, ptr(B), ldb, 1,
+                     K * ldb, ptr(C), NB * (N + 3), N + 3, 0, None, 0, None, 0, 0, 0, stream())
+                outs.append(C)
+            torch.cuda.synchronize()
+            assert torch.equal(outs[0][:, :, :N], outs[1][:, :, :N]), (M, NB, N, K)
+            for C in outs:
+                assert torch.isnan(C[:, :, N:]).all(), (M, NB, N, K)
+            rel = ((outs[0][:, :, :N].double() - ref).abs() / (S + 1.0)).max().item()
+            rel_f32 = ((outs[2][:, :, :N].double() - ref).abs() / (S + 1.0)).max().item()
+            assert rel <= max(1.5 * rel_f32, 3e-7) and rel < 1e-6, (M, NB, N, K, rel, rel_f32)
+    finally:
+        lib.gatx_set_gemm_mode(DEFAULT_GEMM_MODE)
+
+
+@pytest.mark.gpu
 def test_gemm_tail_split(device):
     """Shapes whose last wave of tiles is split along K (fix-up kernel sums the slices):
     same result as the unsplit GEMM to fp32 rounding, bitwise run to run, split output kept."""
