@@ -88,6 +88,9 @@ inline bool reduce4_ok(const GemmArgs& g, int batch) {
          g.ldc0 % 4 == 0 && (uintptr_t)g.C0 % 16 == 0;
 }
 
+}  // namespace
+
+// (outside the anonymous namespace: gemm_smallk.hip's split-K kernel reduces through it too)
 void launch_splitk_reduce(const GemmArgs& g, int batch, hipStream_t stream) {
   if (reduce4_ok(g, batch)) {
     const int64_t total4 = g.M * g.N / 4;
@@ -99,6 +102,8 @@ void launch_splitk_reduce(const GemmArgs& g, int batch, hipStream_t stream) {
                            stream>>>(g, batch);
   }
 }
+
+namespace {
 
 // Skinny weight gradients: C = A^T B with both operands row-contiguous (A(m, k) = A[k lda + m],
 // B(k, n) = B[k ldb + n]), at most 8 output rows and a long K (PPI's first-layer score gradient
@@ -708,6 +713,11 @@ static int gemm_impl(int64_t M, int64_t N, int64_t K, int batch, const float* A,
     }
     return 0;
   }
+  // long-K weight gradient into <= 64 columns with row-contiguous operands (the reassociated
+  // first layer's go_h^T Z_h): the row-streaming kernel of gemm_smallk.hip
+  if (tag == 2 && gemm_mode() >= 1 && n_split >= N && !sc && gemm_tn_fits(M, N, K, a_kc, b_kc) &&
+      launch_gemm_tn(g, batch, workspace, workspace_bytes, stream))
+    return 0;
   if (workspace && tag == 2) {   // explicit split-K into [M][N] slabs
     int sp = choose_splits(tiles, K, slots);
     while (sp > 1 && (size_t)sp * batch * M * N * sizeof(float) > workspace_bytes) --sp;

@@ -293,6 +293,14 @@ int launch_gemm_smallk(const gk::GemmArgs& g, int batch, hipStream_t stream);
 bool gemm_smalln_fits(int64_t M, int64_t N, int64_t K, bool a_kc, bool b_kc, int accumulate,
                       bool epilogue);
 int launch_gemm_smalln(const gk::GemmArgs& g, int batch, hipStream_t stream);
+// gemm_smallk.hip: C = A^T B, both row-contiguous, 8 < M <= 256, N <= 64, long K, split-K into
+// the workspace + splitk_reduce (x3 arithmetic); returns 0 without launching when the
+// workspace holds fewer than two slices
+bool gemm_tn_fits(int64_t M, int64_t N, int64_t K, bool a_kc, bool b_kc);
+int launch_gemm_tn(gk::GemmArgs g, int batch, void* workspace, size_t workspace_bytes,
+                   hipStream_t stream);
+// gemm.hip: sum the split-K slabs [z][b][M][N] into C through the epilogue
+void launch_splitk_reduce(const gk::GemmArgs& g, int batch, hipStream_t stream);
 // gemm_f16p.hip: the f16x3 kernel with B given as pre-split fp16 planes (tags 0 and 1)
 int launch_gemm_f16p(const gk::GemmArgs& g, int tag, hipStream_t stream);
 int launch_gemm_f16rc(const gk::GemmArgs& g, hipStream_t stream);

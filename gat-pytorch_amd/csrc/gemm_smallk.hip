@@ -364,7 +364,148 @@ __global__ void __launch_bounds__(64 * SN_WAVES, 1) gemm_smalln_kernel(GemmArgs 
   }
 }
 
+// Weight gradient over rows, the same arithmetic: C_b = A_b^T B_b with both operands stored
+// row-contiguous (A(m, k) = A[k * lda + m], B(k, n) = B[k * ldb + n]), M <= 256, N <= 64 and a
+// long K (the rows): the reassociated first layer's g_W_h = go_h^T Z_h (functional.
+// _reassoc_backward; PPI layer 0: 4 heads x (256 x 44900) . (44900 x 52)), which the tiled
+// split-K kernel ran at 74 us for 221 MB. One workgroup per (K slice, batch entry); wave w owns
+// output rows 32w..32w+31 and both 32-column blocks (32 accumulator registers). Per chunk of 64
+// rows the workgroup stages B's chunk once as bf16 planes in LDS (double-buffered, 48 KB: every
+// wave needs all of it) while each wave loads its own A columns straight into MFMA fragments
+// (lane = output row, 8 consecutive k = rows of A: 128 contiguous bytes per half-wave and row);
+// the next chunk's loads are issued before this chunk's MFMAs. Slice partials go to [z][b][M][N]
+// slabs summed in slice order by splitk_reduce_kernel (deterministic).
+constexpr int TN_WAVES = 8, TN_MMAX = 256, TN_NMAX = 64, TN_ROWS = 64;
+constexpr int TN_KSLOTS = TN_ROWS / 8;
+constexpr int TN_PLANE = TN_KSLOTS * TN_NMAX * 16;   // bytes per bf16 plane of a B chunk
+
+__global__ void __launch_bounds__(64 * TN_WAVES, 1) gemm_tn_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char bl[2][3 * TN_PLANE];
+  const int b = blockIdx.y, z = blockIdx.x;
+  const float* __restrict__ A = g.A + b * g.a_bs;
+  const float* __restrict__ B = g.B + b * g.b_bs;
+  const int M = (int)g.M, N = (int)g.N;
+  const int64_t k0 = (int64_t)z * g.k_per_split;
+  const int64_t k1 = min(g.K, k0 + g.k_per_split);
+  const int ncb = (N + 31) / 32;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5;
+  const int m = wave * 32 + (lane & 31);
+  const bool mact = wave * 32 < M;
+  // this thread's B staging item: k-slot ks (8 rows), column bn
+  const int ks = threadIdx.x / TN_NMAX, bn = threadIdx.x % TN_NMAX;
+  float braw[8], araw[4][8];
+  // unconditional loads from clamped addresses (a conditional load is a branch, and the
+  // compiler waited vmcnt(0) at every join: 131 us for this product). Rows past M and columns
+  // past N only feed outputs that are never stored; rows of the K tail are zeroed in B alone,
+  // when its chunk is staged (a select here would wait for each load at once)
+  const float* __restrict__ Bc = B + (bn < N ? bn : N - 1);
+  const float* __restrict__ Ac = A + (m < M ? m : M - 1);
+  auto fetch = [&](int64_t r0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t r = r0 + 8 * ks + j;
+      braw[j] = Bc[(r < k1 ? r : k1 - 1) * g.ldb];
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int64_t r = r0 + 16 * s + 8 * half + j;
+        araw[s][j] = Ac[(r < k1 ? r : k1 - 1) * g.lda];
+      }
+  };
+  floatx16 acc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+  const int64_t nch = k1 > k0 ? ceil_div(k1 - k0, (int64_t)TN_ROWS) : 0;
+  if (nch > 0) fetch(k0);
+  for (int64_t c = 0; c < nch; ++c) {
+    char* buf = bl[c & 1];
+    {
+      const int64_t r0 = k0 + c * TN_ROWS + 8 * ks;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) braw[j] = r0 + j < k1 ? braw[j] : 0.f;
+      uint4 h, mm, l;
+      sk_split8(braw, h, mm, l);
+      const int o = (ks * TN_NMAX + bn) * 16;
+      *(uint4*)(buf + o) = h;
+      *(uint4*)(buf + TN_PLANE + o) = mm;
+      *(uint4*)(buf + 2 * TN_PLANE + o) = l;
+    }
+    bf16x8 fa[4][3];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      uint4 h, mm, l;
+      sk_split8(araw[s], h, mm, l);
+      fa[s][0] = __builtin_bit_cast(bf16x8, h);
+      fa[s][1] = __builtin_bit_cast(bf16x8, mm);
+      fa[s][2] = __builtin_bit_cast(bf16x8, l);
+    }
+    // (one barrier per chunk: a wave writes buffer c & 1 again only after the barrier of chunk
+    // c + 1, which every wave reaches after its reads of chunk c)
+    __syncthreads();
+    if (c + 1 < nch) fetch(k0 + (c + 1) * TN_ROWS);
+    if (mact) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          if (i >= ncb) break;
+          bf16x8 fb[3];
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+            fb[p] = *(const bf16x8*)(buf + p * TN_PLANE +
+                                     ((2 * s + half) * TN_NMAX + i * 32 + (lane & 31)) * 16);
+          constexpr int PLA[6] = {2, 0, 1, 1, 0, 0};
+          constexpr int PLB[6] = {0, 2, 1, 0, 1, 0};
+#pragma unroll
+          for (int t = 0; t < 6; ++t)   // lane = output column, registers = rows
+            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][PLA[t]], fb[PLB[t]], acc[i],
+                                                             0, 0, 0);
+        }
+    }
+  }
+  if (!mact) return;
+  // lane l: column i*32 + (l & 31); register r: row wave*32 + 8(r >> 2) + 4(l >> 5) + (r & 3)
+  float* P = g.partial + ((int64_t)z * gridDim.y + b) * (int64_t)M * N;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int col = i * 32 + (lane & 31);
+    if (i >= ncb || col >= N) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = wave * 32 + 8 * (r >> 2) + 4 * half + (r & 3);
+      if (row < M) P[(int64_t)row * N + col] = acc[i][r];
+    }
+  }
+}
+
 }  // namespace
+
+bool gemm_tn_fits(int64_t M, int64_t N, int64_t K, bool a_kc, bool b_kc) {
+  return !a_kc && !b_kc && M > 8 && M <= TN_MMAX && N >= 1 && N <= TN_NMAX && K >= 4096;
+}
+
+// Slices: ~256 workgroups over the batch entries, each slice at least 512 rows; needs
+// slices x batch x M x N floats of workspace for the partials (returns 0: not launched).
+int launch_gemm_tn(gk::GemmArgs g, int batch, void* workspace, size_t workspace_bytes,
+                   hipStream_t stream) {
+  GATX_REQUIRE(g.M <= TN_MMAX && g.N <= TN_NMAX && batch < 65536, "gemm_tn: shape");
+  int64_t sp = std::max<int64_t>(2, std::min<int64_t>(256 / batch, g.K / 512));
+  while (sp > 1 && (!workspace || (size_t)sp * batch * g.M * g.N * sizeof(float) > workspace_bytes))
+    --sp;
+  if (sp < 2) return 0;
+  g.k_per_split = round_up(ceil_div(g.K, sp), (int64_t)TN_ROWS);
+  g.splits = (int)ceil_div(g.K, g.k_per_split);
+  g.partial = (float*)workspace;
+  gemm_tn_kernel<<<dim3((unsigned)g.splits, (unsigned)batch), 64 * TN_WAVES, 0, stream>>>(g);
+  GATX_LAUNCH_CHECK("gemm_tn");
+  launch_splitk_reduce(g, batch, stream);
+  GATX_LAUNCH_CHECK("splitk_reduce");
+  return 1;
+}
 
 bool gemm_smalln_fits(int64_t M, int64_t N, int64_t K, bool a_kc, bool b_kc, int accumulate,
                       bool epilogue) {

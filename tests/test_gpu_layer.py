@@ -315,6 +315,49 @@ def test_gemm_smalln(device):
 
 
 @pytest.mark.gpu
+def test_gemm_tn_rows(device):
+    """The long-K row-streaming weight gradient (C = A^T B, both row-contiguous, 8 < M <= 256,
+    N <= 64: csrc/gemm_smallk.hip gemm_tn_kernel + splitk_reduce, the reassociated first layer's
+    go_h^T Z_h) against float64 and beside the f32 kernel: batched with strided heads as
+    functional._reassoc_backward calls it, ragged M / N / K, accumulate; error relative to
+    sum|a||b| at the fp32 GEMM's level; bitwise repeatable."""
+    from gatx._lib import call, lib, ptr, stream
+    torch.manual_seed(7)
+    # (K rows, heads, M, N, A's row stride, B's row stride)
+    cases = [(44900 // 2, 4, 256, 52, 1024, 208), (5000, 1, 100, 33, 101, 35), (8191, 3, 200, 64, 600, 192),
+             (4096, 2, 9, 5, 20, 11)]
+    try:
+        for (K, NB, M, N, lda, ldb) in cases:
+            A = torch.randn(K, lda, device=device) * torch.rand(K, 1, device=device) * 10
+            B = torch.randn(K, ldb, device=device)
+            fa, fb = lda // NB, ldb // NB
+            Av = A[:, :NB * fa].view(K, NB, fa)[:, :, :M].double()
+            Bv = B[:, :NB * fb].view(K, NB, fb)[:, :, :N].double()
+            ref = torch.einsum("kbm,kbn->bmn", Av, Bv)
+            S = torch.einsum("kbm,kbn->bmn", Av.abs(), Bv.abs())
+            wb = lib.gatx_gemm_splitk_batched_workspace_bytes(NB, M, N, K)
+            ws = torch.empty(max(wb, 1), dtype=torch.uint8, device=device)
+            for acc in (0, 1):
+                C0 = torch.randn(NB, M, N, device=device)
+                outs = []
+                for mode in (2, 2, 0):
+                    lib.gatx_set_gemm_mode(mode)
+                    C = C0.clone()
+                    call("gatx_gemm_f32_splitk_batched", NB, M, N, K, ptr(A), 1, lda, fa, ptr(B),
+                         ldb, 1, fb, ptr(C), N, M * N, acc, ptr(ws), wb, stream())
+                    outs.append(C)
+                torch.cuda.synchronize()
+                assert torch.equal(outs[0], outs[1]), (K, NB, M, N)
+                want = ref + (C0.double() if acc else 0)
+                rel = ((outs[0].double() - want).abs() / (S + 1.0)).max().item()
+                rel_f32 = ((outs[2].double() - want).abs() / (S + 1.0)).max().item()
+                assert rel <= max(1.5 * rel_f32, 3e-7) and rel < 1e-6, (K, NB, M, N, acc, rel,
+                                                                         rel_f32)
+    finally:
+        lib.gatx_set_gemm_mode(DEFAULT_GEMM_MODE)
+
+
+@pytest.mark.gpu
 def test_gemm_tail_split(device):
     """Shapes whose last wave of tiles is split along K (fix-up kernel sums the slices):
     same result as the unsplit GEMM to fp32 rounding, bitwise run to run, split output kept."""
